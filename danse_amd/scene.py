@@ -1,0 +1,197 @@
+"""Synthetic acoustic scenes for the DANSE engine (input producer).
+
+Scene generation is not on the hot path; this module exists so that tests, the
+oracle and ``bench.py`` all feed the engine bit-identical inputs from a seed.
+It follows the *shape* of the reference's offline scene path
+(``trueRoom: false``, ``signalType: random``):
+
+* random impulse responses, uniform in [-0.5, 0.5], 0.2 s, no decay
+  (``siggen/utils.py:229-308``, ``siggen/classes.py:16-29``);
+* uniform [-1, 1] desired source with predefined 0.5 s pauses every 0.5 s, and
+  one continuous uniform noise source (``siggen/classes.py:32-64``);
+* SNR set at mic 0 (``siggen/utils.py:1421-1431``) and white self-noise per
+  sensor (``siggen/utils.py:1418``);
+* an energy VAD on the wet desired signal at each node's reference sensor
+  (``siggen/utils.py:834-939,1079-1133``).
+
+It is NOT a bit-exact restatement of ``siggen`` (different RNG streams, a
+vectorised VAD): parity is anchored by injecting the very same arrays into the
+reference, the oracle and the GPU engine.  All signals are rounded to float32
+(and kept as float64 values) so that the fp32 device path and the fp64 oracle
+consume exactly the same numbers.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+from scipy.signal import fftconvolve
+
+
+@dataclass
+class SceneNode:
+    """The fields of ``siggen.classes.Node`` (``siggen/classes.py:379-428``)
+    that the DANSE engine reads."""
+    index: int
+    nSensors: int
+    fs: float
+    data: np.ndarray            # [T x M] noisy mic signals
+    cleanspeech: np.ndarray     # [T x M] speech-only
+    cleannoise: np.ndarray      # [T x M] noise-only (incl. ref-sensor self-noise)
+    timeStamps: np.ndarray      # [T]
+    vad: np.ndarray             # [T x 1] per-sample VAD (0/1)
+    neighborsIdx: list = field(default_factory=list)
+    sro: float = 0.0
+    refSensorIdx: int = 0
+    vadPerFrame: np.ndarray = None
+    beta: float = 1.0
+    betaWext: float = 1.0
+
+
+@dataclass
+class Scene:
+    """A fully connected WASN (``siggen.classes.WASN``, ``siggen/classes.py:431``)."""
+    wasn: list
+    fs: float
+    seed: int
+
+    @property
+    def nNodes(self) -> int:
+        return len(self.wasn)
+
+    @property
+    def nSensorPerNode(self) -> list:
+        return [n.nSensors for n in self.wasn]
+
+    def get_vad_per_frame(self, frameLen: int, frameShift: int, minProportionActive: float = 0.5):
+        """Frame VAD, restating ``WASN.get_vad_per_frame``
+        (``siggen/classes.py:669-702``), including its crop quirk: when the
+        frame running past the end is met at index ``ii``, the output keeps
+        ``ii + 1`` entries (the last one stays 0)."""
+        for node in self.wasn:
+            node.vadPerFrame = vad_per_frame(node.vad[:, 0], frameLen, frameShift, minProportionActive)
+
+
+def vad_per_frame(vad: np.ndarray, frameLen: int, frameShift: int, minProp: float) -> np.ndarray:
+    n = len(vad)
+    nFrames = n // frameShift
+    out = np.zeros(nFrames, dtype=bool)
+    csum = np.concatenate(([0.0], np.cumsum(vad, dtype=np.float64)))
+    for ii in range(nFrames):
+        b, e = ii * frameShift, ii * frameShift + frameLen
+        if e > n:
+            return out[:ii + 1]
+        out[ii] = (csum[e] - csum[b]) >= frameLen * minProp
+    return out
+
+
+def _energy_vad(x: np.ndarray, fs: float, tw: float, energyDecrease_dB: float) -> np.ndarray:
+    """Short-time energy VAD: window of ``int(tw*fs)`` samples centred on each
+    sample, active if the window energy exceeds max(x^2)/10^(dB/10)
+    (shape of ``oracleVAD``, ``siggen/utils.py:1079-1133``)."""
+    thrs = np.amax(x ** 2) / (10 ** (energyDecrease_dB / 10))
+    nw = max(int(tw * fs), 1)
+    c = np.concatenate(([0.0], np.cumsum(x ** 2)))
+    idx = np.arange(len(x))
+    b = np.maximum(idx - nw // 2, 0)
+    e = np.minimum(idx + nw // 2, len(x))
+    energy = c[e] - c[b]
+    return (energy > thrs).astype(np.float64)
+
+
+def _f32(x: np.ndarray) -> np.ndarray:
+    return np.asarray(x, dtype=np.float32).astype(np.float64)
+
+
+def make_scene(
+    nSensorPerNode,
+    sigDur: float = 10.0,
+    fs: float = 16000.0,
+    seed: int = 0,
+    snr: float = 5.0,
+    selfnoiseSNR: float = 15.0,
+    irDuration: float = 0.2,
+    pauseDuration: float = 0.5,
+    pauseSpacing: float = 0.5,
+    vadEnergyDecrease_dB: float = 40.0,
+    vadWinLength: float = 0.04,
+    SROperNode=None,
+) -> Scene:
+    """Build a random-IR, random-signal fully connected WASN.
+
+    SROs are recorded per node (``SROperNode`` in ppm) but the signals are not
+    resampled here (the reference needs ``resampy`` for that, absent offline);
+    the time stamps follow ``siggen/utils.py:1579-1622`` (``t = n / fsSRO``).
+    """
+    rng = np.random.default_rng(seed)
+    K = len(nSensorPerNode)
+    T = int(sigDur * fs)
+    nIR = int(irDuration * fs)
+    sros = np.zeros(K) if SROperNode is None else np.asarray(SROperNode, dtype=float)
+
+    # Desired source: uniform noise with predefined pauses (0.5 s on / 0.5 s off).
+    d = rng.uniform(-1.0, 1.0, T)
+    t = np.arange(T) / fs
+    period = pauseDuration + pauseSpacing
+    d[(t % period) >= pauseSpacing] = 0.0
+    n = rng.uniform(-1.0, 1.0, T)
+
+    nodes = []
+    for k in range(K):
+        M = int(nSensorPerNode[k])
+        wetS = np.zeros((T, M))
+        wetN = np.zeros((T, M))
+        for m in range(M):
+            hd = rng.uniform(-0.5, 0.5, nIR)
+            hn = rng.uniform(-0.5, 0.5, nIR)
+            wetS[:, m] = fftconvolve(d, hd)[:T]
+            wetN[:, m] = fftconvolve(n, hn)[:T]
+        nodes.append([wetS, wetN])
+
+    # SNR at mic 0 of node 0 (single noise source).
+    Ps = np.mean(nodes[0][0][:, 0] ** 2)
+    Pn = np.mean(nodes[0][1][:, 0] ** 2)
+    gN = 10 ** (-(snr - 10 * np.log10(Ps / Pn)) / 20)
+
+    wasn = []
+    for k in range(K):
+        wetS, wetN = nodes[k]
+        wetN = wetN * gN
+        M = wetS.shape[1]
+        clean = wetS + wetN
+        sig = np.zeros_like(clean)
+        selfN = np.zeros_like(clean)
+        for m in range(M):
+            sn = rng.uniform(-1.0, 1.0, T)
+            Pc = np.mean(clean[:, m] ** 2)
+            Psn = np.mean(sn ** 2)
+            sn *= 10 ** (-(selfnoiseSNR - 10 * np.log10(Pc / Psn)) / 20)
+            selfN[:, m] = sn
+            sig[:, m] = clean[:, m] + sn
+        vad = _energy_vad(wetS[:, 0], fs, vadWinLength, vadEnergyDecrease_dB)
+        fsSRO = fs * (1 + sros[k] / 1e6)
+        node = SceneNode(
+            index=k,
+            nSensors=M,
+            fs=fsSRO,
+            data=_f32(sig),
+            cleanspeech=_f32(wetS),
+            cleannoise=_f32(wetN + selfN[:, :1]),
+            timeStamps=np.arange(T) / fsSRO,
+            vad=vad[:, None],
+            neighborsIdx=[q for q in range(K) if q != k],
+            sro=float(sros[k]),
+        )
+        wasn.append(node)
+    return Scene(wasn=wasn, fs=fs, seed=seed)
+
+
+def scene_digest(scene: Scene) -> str:
+    """sha256 over the float32 input bytes: pins that a scene regenerated from
+    its seed on another machine is the one the golden fixtures were made on."""
+    import hashlib
+    h = hashlib.sha256()
+    for node in scene.wasn:
+        h.update(node.data.astype(np.float32).tobytes())
+        h.update(node.vad.astype(np.uint8).tobytes())
+    return h.hexdigest()

@@ -1,0 +1,88 @@
+"""Case definitions shared by ``make_golden.py`` (reference side, build
+container only) and the tests (no reference import).  Each case names the
+reference configuration it mirrors."""
+from __future__ import annotations
+
+import numpy as np
+
+# sandbox YAML (config A) settings, config_files/sandbox_config.yaml:13-80
+SANDBOX = dict(simType='online', performGEVD=True, use1stFrameAsBasis=True,
+               filterInitType='fixedValue', filterInitFixedValue=1,
+               forcedBetaExternalFilters=0.7, t_expAvg50p=1, t_expAvg50pExternalFilters=1,
+               startComputeMetricsAt='after_200ms', covMatInitType='fully_random')
+# battery YAML (configs B-E), config_files/sandbox_config_battery20230919.yaml
+BATTERY = dict(simType='online', performGEVD=True, use1stFrameAsBasis=True,
+               filterInitType='selectFirstSensor', forcedBetaExternalFilters=0.7,
+               t_expAvg50p=1, t_expAvg50pExternalFilters=1, startComputeMetricsAt='after_200ms',
+               noFusionAtSingleSensorNodes=True)
+
+
+def _d(base, **kw):
+    out = dict(base)
+    out.update(kw)
+    return out
+
+
+ONLINE_CASES = [
+    # config A shape: K=2 x 1 mic, seq, GEVD r1, local + centralised + SSBC, SNR replay
+    dict(name='online_A_k2m1_seq', M=[1, 1], dur=2.0, seed=1, snr_replay=True,
+         danse=_d(SANDBOX, nodeUpdating='seq', computeLocal=True, computeCentralised=True,
+                  computeSingleSensorBroadcast=True)),
+    # config B shape (smaller K): asy GEVD r1, battery settings
+    dict(name='online_B_k4m3_asy', M=[3, 3, 3, 3], dur=2.0, seed=2,
+         danse=_d(BATTERY, nodeUpdating='asy')),
+    dict(name='online_B_k4m3_seq', M=[3, 3, 3, 3], dur=2.0, seed=2,
+         danse=_d(BATTERY, nodeUpdating='seq')),
+    # ragged nodes, GEVD rank 2, local + centralised, asy
+    dict(name='online_ragged_asy_r2', M=[2, 3, 2], dur=2.0, seed=3,
+         danse=_d(SANDBOX, nodeUpdating='asy', GEVDrank=2, computeLocal=True, computeCentralised=True)),
+    # MWF (no GEVD), seq and asy; no first-frame basis (eps-random SCM init path)
+    dict(name='online_mwf_seq', M=[2, 2], dur=2.0, seed=4,
+         danse=_d(SANDBOX, nodeUpdating='seq', performGEVD=False)),
+    dict(name='online_mwf_asy_nobasis', M=[2, 2, 2], dur=2.0, seed=5,
+         danse=_d(BATTERY, nodeUpdating='asy', performGEVD=False, use1stFrameAsBasis=False)),
+]
+
+BATCH_CASES = [
+    # d_batch: non frame-aligned length (quirk Q9)
+    dict(name='batch_k3m2_asy', M=[2, 2, 2], dur=2.01, seed=6,
+         danse=_d(BATTERY, simType='batch', nodeUpdating='asy', maxBatchUpdates=5)),
+    dict(name='batch_k3_seq_mwf', M=[1, 2, 3], dur=2.01, seed=7,
+         danse=_d(BATTERY, simType='batch', nodeUpdating='seq', maxBatchUpdates=4, performGEVD=False)),
+]
+
+SRO_EVENT_CASES = [
+    dict(name='events_sro_0_50_100_seq', M=[1, 1, 1], dur=4.0, sros=[0, 50, 100],
+         danse=_d(BATTERY, nodeUpdating='seq')),
+    dict(name='events_sro_0_100_200_asy', M=[1, 1, 1], dur=4.0, sros=[0, 100, 200],
+         danse=_d(BATTERY, nodeUpdating='asy')),
+    dict(name='events_sro_0_0_seq', M=[2, 2], dur=3.0, sros=[0, 0],
+         danse=_d(BATTERY, nodeUpdating='seq')),
+]
+
+KAT_CASES = [dict(name=f'kat_{"gevd" if g else "mwf"}_D{D}_r{r}', D=D, F=48, gevd=g, rank=r, ref=0, seed=100 + D + r)
+             for (D, g, r) in [(2, True, 1), (11, True, 1), (11, True, 2), (19, True, 1), (39, True, 1),
+                               (2, False, 1), (11, False, 1), (39, False, 1)]]
+
+
+def kat_inputs(case):
+    """Exponentially averaged rank-1 updates (the online SCM recursion,
+    ``d_classes.py:2086-2090``) from a random mixing: Ryy has a strong
+    rank-1 component over a spatially coloured noise floor."""
+    rng = np.random.default_rng(case['seed'])
+    F, D = case['F'], case['D']
+    beta = 0.978063
+    A = rng.standard_normal((F, D, D)) + 1j * rng.standard_normal((F, D, D))
+    a = rng.standard_normal((F, D)) + 1j * rng.standard_normal((F, D))
+    Rnn = np.zeros((F, D, D), dtype=complex)
+    Ryy = np.zeros((F, D, D), dtype=complex)
+    for t in range(3 * D + 10):
+        n = np.einsum('fij,fj->fi', A, rng.standard_normal((F, D)) + 1j * rng.standard_normal((F, D)))
+        s = a * (rng.standard_normal((F, 1)) + 1j * rng.standard_normal((F, 1))) * 3.0
+        nn = 1 / D * np.einsum('ij,ik->ijk', n, n.conj())
+        yy = 1 / D * np.einsum('ij,ik->ijk', n + s, (n + s).conj())
+        Rnn = beta * Rnn + (1 - beta) * nn
+        n2 = np.einsum('fij,fj->fi', A, rng.standard_normal((F, D)) + 1j * rng.standard_normal((F, D)))
+        yy = 1 / D * np.einsum('ij,ik->ijk', n2 + s, (n2 + s).conj())
+        Ryy = beta * Ryy + (1 - beta) * yy
+    return Ryy, Rnn

@@ -1,0 +1,121 @@
+"""Generate golden vectors by running the REFERENCE (p-didier/danse, imported
+through ``_refharness``) on seeded synthetic scenes.  Build-container only
+(needs /root/reference); the committed ``.npz`` files are the only thing that
+travels.  Inputs are not stored: they are regenerated from the seed by
+``danse_amd.scene.make_scene`` and pinned by a sha256 digest stored in each
+fixture.
+
+Usage:  python tests/golden/make_golden.py            (writes tests/golden/*.npz)
+"""
+from __future__ import annotations
+
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+sys.path.insert(0, str(HERE.parent.parent))
+sys.path.insert(0, str(HERE))
+
+import _refharness as H  # noqa: E402
+from danse_amd.scene import make_scene, scene_digest  # noqa: E402
+from golden_cases import ONLINE_CASES, BATCH_CASES, SRO_EVENT_CASES, KAT_CASES, kat_inputs  # noqa: E402
+
+
+def _run_online(ns, case):
+    sc = make_scene(case['M'], sigDur=case['dur'], seed=case['seed'])
+    p = H.make_params(ns, case['M'], **case['danse'])
+    w = H.to_ref_wasn(ns, sc)
+    p, w = H.prep(ns, p, w)
+    t0 = time.time()
+    dv, w = ns.core.danse(w, p.danseParams)
+    el = time.time() - t0
+    out = {'digest': scene_digest(sc), 'ref_seconds': el}
+    K = len(case['M'])
+    every = case.get('wEvery', 16)
+    asy = 'seq' not in case['danse']['nodeUpdating']
+    out['d'] = dv.d
+    out['dhat'] = dv.dhat[:, ::every, :]
+    for nm, fl in [('dLocal', 'computeLocal'), ('dCentr', 'computeCentralised'), ('dSSBC', 'computeSingleSensorBroadcast')]:
+        if case['danse'].get(fl, False):
+            out[nm] = getattr(dv, nm)
+    for k in range(K):
+        out[f'w_{k}'] = dv.wTilde[k][:, ::every, :]
+        if asy:
+            out[f'wExt_{k}'] = dv.wTildeExt[k][:, ::every, :]
+        if k < 2:
+            out[f'z_{k}'] = dv.zFullTD[k]
+        if case['danse'].get('computeLocal', False):
+            out[f'wLocal_{k}'] = dv.wLocal[k][:, ::every, :]
+        if case['danse'].get('computeCentralised', False):
+            out[f'wCentr_{k}'] = dv.wCentr[k][:, ::every, :]
+    out['startUpdates'] = np.array(dv.startUpdates)
+    out['nInternalFilterUps'] = np.array(dv.nInternalFilterUps)
+    if case.get('snr_replay', False):
+        sigs = ns.core.generate_signals_for_snr_computation(p.danseParams, dv, w, ns.core.danse)
+        for key in ['n', 's']:
+            out[f'snr_{key}'] = sigs[key]
+    return out
+
+
+def _run_batch(ns, case):
+    sc = make_scene(case['M'], sigDur=case['dur'], seed=case['seed'])
+    p = H.make_params(ns, case['M'], **case['danse'])
+    w = H.to_ref_wasn(ns, sc)
+    p, w = H.prep(ns, p, w)
+    t0 = time.time()
+    out_, w = ns.core.danse_batch(w, p.danseParams)
+    el = time.time() - t0
+    out = {'digest': scene_digest(sc), 'ref_seconds': el, 'd': out_.TDdesiredSignals_est,
+           'mmseCost': np.array(out_.mmseCost, dtype=float)}
+    for k in range(len(case['M'])):
+        out[f'w_{k}'] = out_.filters[k][:, :case['danse']['maxBatchUpdates'] + 1, :]
+    return out
+
+
+def _run_sro_events(ns, case):
+    sc = make_scene(case['M'], sigDur=case['dur'], seed=0, SROperNode=case['sros'])
+    p = H.make_params(ns, case['M'], **case['danse'])
+    # WASNparameters SROs so that prep/checks see them
+    p.wasnParams.SROperNode = np.array(case['sros'], dtype=float)
+    w = H.to_ref_wasn(ns, sc)
+    ev, fs, _ = ns.base.initialize_events(
+        np.stack([n.timeStamps for n in sc.wasn], axis=1), p.danseParams, w)
+    rows = []
+    for e in ev:
+        for ii in range(e.nEvents):
+            rows.append((e.t, int(e.nodes[ii]), 0 if e.type[ii] == 'bc' else 1, int(e.bypassUpdate[ii])))
+    rows = np.array(rows, dtype=[('t', 'f8'), ('node', 'i4'), ('type', 'i4'), ('bypass', 'i4')])
+    return {'events': rows, 'fs': fs, 'n_instants': len(ev)}
+
+
+def _run_kat(ns, case):
+    Ryy, Rnn = kat_inputs(case)
+    fn = ns.cl.update_w_gevd if case['gevd'] else ns.cl.update_w
+    w = fn(Ryy, Rnn, refSensorIdx=case['ref'], rank=case.get('rank', 1))
+    return {'w': w}
+
+
+def main():
+    ns = H.load()
+    only = sys.argv[1:]
+    jobs = [('online', c, _run_online) for c in ONLINE_CASES] + \
+           [('batch', c, _run_batch) for c in BATCH_CASES] + \
+           [('events', c, _run_sro_events) for c in SRO_EVENT_CASES] + \
+           [('kat', c, _run_kat) for c in KAT_CASES]
+    for kind, case, fn in jobs:
+        name = case['name']
+        if only and name not in only:
+            continue
+        t0 = time.time()
+        out = fn(ns, case)
+        np.savez_compressed(HERE / f'{name}.npz', **out)
+        sz = os.path.getsize(HERE / f'{name}.npz') / 1e6
+        print(f'{kind:7s} {name:28s} {time.time() - t0:7.1f}s  {sz:6.2f} MB', flush=True)
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,90 @@
+"""The CPU oracle (oracle/danse_ref_cpu.py) against golden vectors produced by
+the reference itself (tests/golden/make_golden.py).  CPU only."""
+import numpy as np
+import pytest
+
+from golden_cases import ONLINE_CASES, BATCH_CASES, SRO_EVENT_CASES, KAT_CASES, kat_inputs
+from danse_amd.scene import scene_digest
+from danse_amd.scheduler import initialize_events
+from oracle import danse_ref_cpu as O
+from _util import make_case_params, make_case_scene, rel_err
+
+TOL = 1e-10
+
+
+def _load(golden_dir, name):
+    return dict(np.load(golden_dir / f'{name}.npz', allow_pickle=False))
+
+
+@pytest.mark.parametrize('case', ONLINE_CASES, ids=[c['name'] for c in ONLINE_CASES])
+def test_online_oracle_matches_reference(case, golden_dir):
+    g = _load(golden_dir, case['name'])
+    sc = make_case_scene(case)
+    assert scene_digest(sc) == str(g['digest']), 'regenerated scene differs from the one the fixture was made on'
+    dp, wp = make_case_params(case)
+    dv = O.danse(sc, dp, vadMinProp=wp.vadMinProportionActive)
+    every = 16
+    assert rel_err(dv.d, g['d']) < TOL
+    assert rel_err(dv.dhat[:, ::every, :], g['dhat']) < TOL
+    for k in range(len(case['M'])):
+        assert rel_err(dv.wTilde[k][:, ::every, :], g[f'w_{k}']) < TOL
+        if f'wExt_{k}' in g:
+            assert rel_err(dv.wTildeExt[k][:, ::every, :], g[f'wExt_{k}']) < TOL
+        if f'z_{k}' in g:
+            assert rel_err(dv.zFullTD[k], g[f'z_{k}']) < TOL
+        if f'wLocal_{k}' in g:
+            assert rel_err(dv.wLocal[k][:, ::every, :], g[f'wLocal_{k}']) < TOL
+        if f'wCentr_{k}' in g:
+            assert rel_err(dv.wCentr[k][:, ::every, :], g[f'wCentr_{k}']) < TOL
+    for nm in ['dLocal', 'dCentr', 'dSSBC']:
+        if nm in g:
+            assert rel_err(getattr(dv, nm), g[nm]) < TOL
+    assert np.array_equal(np.array([s.start for s in dv.danse]), g['startUpdates'])
+    assert np.array_equal(dv.nInternalFilterUps, g['nInternalFilterUps'])
+    if case.get('snr_replay'):
+        sigs = O.generate_signals_for_snr_computation(sc, dp, dv, vadMinProp=wp.vadMinProportionActive)
+        assert rel_err(sigs['n'], g['snr_n']) < TOL
+        assert rel_err(sigs['s'], g['snr_s']) < TOL
+
+
+@pytest.mark.parametrize('case', BATCH_CASES, ids=[c['name'] for c in BATCH_CASES])
+def test_batch_oracle_matches_reference(case, golden_dir):
+    g = _load(golden_dir, case['name'])
+    sc = make_case_scene(case)
+    assert scene_digest(sc) == str(g['digest'])
+    dp, wp = make_case_params(case)
+    bv = O.danse_batch(sc, dp, vadMinProp=wp.vadMinProportionActive)
+    assert rel_err(bv.d, g['d']) < TOL
+    assert rel_err(np.array(bv.mmseCost, dtype=float), g['mmseCost']) < TOL
+    for k in range(len(case['M'])):
+        nb = case['danse']['maxBatchUpdates'] + 1
+        assert rel_err(bv.wTilde[k][:, :nb, :], g[f'w_{k}']) < TOL
+
+
+@pytest.mark.parametrize('case', SRO_EVENT_CASES, ids=[c['name'] for c in SRO_EVENT_CASES])
+def test_scheduler_matches_reference(case, golden_dir):
+    """Host event scheduler (danse_amd/scheduler.py) vs the reference's
+    initialize_events, including SRO clocks (quirks Q3, Q13)."""
+    g = _load(golden_dir, case['name'])
+    sc = make_case_scene(dict(case, seed=0), SROperNode=case['sros'])
+    dp, wp = make_case_params(case, SROperNode=case['sros'])
+    ev, fs = initialize_events([n.timeStamps for n in sc.wasn], [n.fs for n in sc.wasn], dp,
+                               [n.neighborsIdx for n in sc.wasn])
+    rows = [(e.t, int(e.nodes[ii]), 0 if e.type[ii] == 'bc' else 1, int(e.bypassUpdate[ii]))
+            for e in ev for ii in range(e.nEvents)]
+    ref = g['events']
+    assert len(ev) == int(g['n_instants'])
+    assert len(rows) == len(ref)
+    got = np.array(rows, dtype=ref.dtype)
+    for f in ref.dtype.names:
+        assert np.array_equal(got[f], ref[f]), f
+    assert np.array_equal(fs, g['fs'])
+
+
+@pytest.mark.parametrize('case', KAT_CASES, ids=[c['name'] for c in KAT_CASES])
+def test_filter_update_kat(case, golden_dir):
+    g = _load(golden_dir, case['name'])
+    Ryy, Rnn = kat_inputs(case)
+    fn = O.update_w_gevd if case['gevd'] else O.update_w
+    w = fn(Ryy, Rnn, refSensorIdx=case['ref'], rank=case['rank'])
+    assert rel_err(w, g['w']) < 1e-12
