@@ -1,0 +1,100 @@
+"""ctypes binding of the C-ABI in ``include/danse_mi355x.h``.
+
+The shared library ``libdanse_mi355x.so`` is built in-tree by
+``danse_amd.build.build()`` (hipcc, gfx950).  There is no fallback: if the
+library is missing or fails to load, every product entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+LIB_NAME = 'libdanse_mi355x.so'
+LIB_PATH = Path(__file__).resolve().parent / LIB_NAME
+
+_c_i32 = ctypes.c_int32
+_p_i32 = ctypes.POINTER(ctypes.c_int32)
+_p_f32 = ctypes.POINTER(ctypes.c_float)
+_p_u8 = ctypes.POINTER(ctypes.c_uint8)
+
+FAM_DANSE, FAM_LOCAL, FAM_CENTR, FAM_SSBC = 0, 1, 2, 3
+OP_KEEP, OP_SET, OP_AVG = 0, 1, 2
+FLAG_SOLVE = 0x10
+FLAG_EXT_TARGET = 0x20
+FLAG_PREGIVEN = 0x40
+EXT_COPY, EXT_RELAX, EXT_KEEP, EXT_REFONLY = 0, 1, 2, 3
+OUT_W, OUT_WEXT, OUT_D, OUT_DHAT, OUT_Z, OUT_DIAG = 0, 1, 2, 3, 4, 5
+
+
+class DanseCfg(ctypes.Structure):
+    _fields_ = [
+        ('S', _c_i32), ('K', _c_i32), ('M', _p_i32),
+        ('N', _c_i32), ('Ns', _c_i32), ('T', _c_i32), ('R', _c_i32),
+        ('k0', _c_i32), ('k1', _c_i32),
+        ('gevd', _c_i32), ('rank', _c_i32), ('ref', _c_i32), ('families', _c_i32),
+        ('alphaExt', ctypes.c_float),
+        ('extMode', _p_i32), ('beta', _p_f32), ('betaExt', _p_f32),
+        ('winAnalysis', _p_f32), ('winSynthesis', _p_f32),
+        ('bcEnd', _p_i32), ('upEnd', _p_i32), ('flags', _p_u8),
+        ('w0', _p_f32), ('wExt0', _p_f32), ('wExtTarget0', _p_f32), ('scmInit', _p_f32),
+        ('keepHistory', _c_i32),
+    ]
+
+
+# every symbol include/danse_mi355x.h declares, with its ctypes signature
+SIGNATURES = {
+    'danse_engine_create': (_c_i32, [ctypes.POINTER(DanseCfg), _c_i32, ctypes.POINTER(ctypes.c_void_p)]),
+    'danse_engine_destroy': (None, [ctypes.c_void_p]),
+    'danse_last_error': (ctypes.c_char_p, [ctypes.c_void_p]),
+    'danse_engine_set_inputs': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p]),
+    'danse_engine_reset': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p]),
+    'danse_engine_run': (_c_i32, [ctypes.c_void_p, _c_i32, _c_i32, ctypes.c_void_p, _c_i32]),
+    'danse_engine_bcast': (_c_i32, [ctypes.c_void_p, _c_i32, ctypes.c_void_p]),
+    'danse_engine_update': (_c_i32, [ctypes.c_void_p, _c_i32, ctypes.c_void_p]),
+    'danse_engine_finish': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p]),
+    'danse_engine_set_zspec': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p]),
+    'danse_engine_zspec': (_c_i32, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t)]),
+    'danse_engine_get': (_c_i32, [ctypes.c_void_p, _c_i32, _c_i32, _c_i32, ctypes.c_void_p, ctypes.c_size_t,
+                                  ctypes.c_void_p]),
+    'danse_engine_put': (_c_i32, [ctypes.c_void_p, _c_i32, _c_i32, _c_i32, ctypes.c_void_p, ctypes.c_size_t,
+                                  ctypes.c_void_p]),
+    'danse_engine_output_bytes': (_c_i32, [ctypes.c_void_p, _c_i32, _c_i32, _c_i32, ctypes.POINTER(ctypes.c_size_t)]),
+    'danse_wola_analysis': (_c_i32, [ctypes.c_void_p, _c_i32, _c_i32, ctypes.c_void_p, ctypes.c_void_p, _c_i32, _c_i32,
+                                     ctypes.c_void_p, ctypes.c_void_p]),
+    'danse_filter_update': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_i32,
+                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    'danse_batch_covmats': (_c_i32, [ctypes.c_void_p, _c_i32, _c_i32, _c_i32, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_void_p, ctypes.c_void_p]),
+}
+
+_lib = None
+
+
+def load_library(path: os.PathLike | None = None):
+    """Load (once) and type the HIP library.  Raises if it is absent."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = Path(path) if path is not None else LIB_PATH
+    if not p.exists():
+        raise RuntimeError(f'{p} not found: build the HIP extension first (python -c "import __graft_entry__ as g; g.build()")')
+    lib = ctypes.CDLL(str(p))
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib
+
+
+class DanseError(RuntimeError):
+    pass
+
+
+def check(rc: int, eng=None):
+    if rc != 0:
+        lib = load_library()
+        msg = lib.danse_last_error(eng)
+        raise DanseError((msg or b'').decode() or f'error {rc}')

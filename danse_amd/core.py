@@ -1,0 +1,75 @@
+"""Reference-API drivers (``danse_toolbox/d_core.py``) on the MI355X engine.
+
+``danse(wasnObj, p)`` is the drop-in for the reference's
+``danse_function`` (``d_core.py:26-102``): same arguments (a WASN whose nodes
+carry ``data``/``timeStamps``/``fs``/``vadPerFrame``/``neighborsIdx`` and a
+``DANSEparameters``), same returned fields.  ``danse_multi`` runs S
+same-shape scenes in one batched engine (the Monte-Carlo battery use).
+"""
+from __future__ import annotations
+
+import copy
+import time
+
+import numpy as np
+
+from .engine import DanseEngine, beta_from_t50p
+from .params import PreComputedFilters
+
+
+def prep_for_danse(p, wasnObj):
+    """``d_core.prep_for_danse`` (``d_core.py:466-547``): forgetting factors
+    per node and frame VAD."""
+    for node in wasnObj.wasn:
+        node.beta = (beta_from_t50p(p.danseParams.t_expAvg50p, node.fs, p.danseParams.Ns)
+                     if p.danseParams.forcedBeta is None else p.danseParams.forcedBeta)
+        node.betaWext = (beta_from_t50p(p.danseParams.t_expAvg50pExternalFilters, node.fs, p.danseParams.Ns)
+                         if p.danseParams.forcedBetaExternalFilters is None else p.danseParams.forcedBetaExternalFilters)
+    wasnObj.get_vad_per_frame(frameLen=p.danseParams.DFTsize, frameShift=p.danseParams.Ns,
+                              minProportionActive=p.wasnParams.vadMinProportionActive)
+    return p, wasnObj
+
+
+def danse_multi(scenes, p, device=0, graph=True, keepHistory=True, yin='data', pregiven=None):
+    """Run the online engine on S same-shape scenes at once; returns one
+    output object per scene."""
+    eng = DanseEngine(scenes, p, device=device, keepHistory=keepHistory, yin=yin, pregiven=pregiven)
+    try:
+        eng.run(graph=graph)
+        return eng.outputs()
+    finally:
+        eng.close()
+
+
+def danse(wasnObj, p, device=0, graph=True):
+    """``d_core.danse``: online fully connected DANSE of one WASN."""
+    t0 = time.perf_counter()
+    pg = p.preGivenFilters
+    yin = 'data'
+    pregiven = None
+    if pg.active:
+        yin = 'cleannoise' if pg.purpose == 'noise-only' else 'cleanspeech'
+        pregiven = pg
+    dv = danse_multi([wasnObj], p, device=device, graph=graph, yin=yin, pregiven=pregiven)[0]
+    dv.wallSeconds = time.perf_counter() - t0
+    return dv, wasnObj
+
+
+def generate_signals_for_snr_computation(pD, dv, wasnObj, danse_function=danse):
+    """``d_core.generate_signals_for_snr_computation`` (``d_core.py:550-599``):
+    noise-only and speech-only replays with the recorded filters."""
+    pU = copy.deepcopy(pD)
+    pU.preGivenFilters = PreComputedFilters(
+        active=True, internalFilters=dv.wTilde, externalFilters=dv.wTildeExt,
+        filtersCentr=getattr(dv, 'wCentr', []), filtersSSBC=getattr(dv, 'wSSBC', []),
+        filtersLocal=getattr(dv, 'wLocal', []), purpose='noise-only')
+    dv_n, _ = danse_function(wasnObj, pU)
+    pU.preGivenFilters.purpose = 'speech-only'
+    dv_s, _ = danse_function(wasnObj, pU)
+    out = {}
+    for key, src in (('n', dv_n), ('s', dv_s)):
+        out[key] = src.d
+        out[f'{key}_c'] = getattr(src, 'dCentr', None)
+        out[f'{key}_l'] = getattr(src, 'dLocal', None)
+        out[f'{key}_ssbc'] = getattr(src, 'dSSBC', None)
+    return out

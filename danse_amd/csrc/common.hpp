@@ -1,0 +1,131 @@
+// Common device helpers for the DANSE frame-update engine (gfx950 / CDNA4).
+//
+// Complex numbers are float2 {re, im}; all arithmetic is fp32 unless a kernel
+// is instantiated with double for the solve.  Cross-lane traffic inside a
+// lane group of G lanes (G = 16: DPP row broadcast, G = 64: v_readlane into an
+// SGPR) never goes through LDS.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define DANSE_DEV __device__ __forceinline__
+
+struct cf {
+  float re, im;
+};
+
+DANSE_DEV cf cmk(float r, float i) { return cf{r, i}; }
+DANSE_DEV cf operator+(cf a, cf b) { return cf{a.re + b.re, a.im + b.im}; }
+DANSE_DEV cf operator-(cf a, cf b) { return cf{a.re - b.re, a.im - b.im}; }
+DANSE_DEV cf operator*(cf a, cf b) { return cf{a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re}; }
+DANSE_DEV cf operator*(float s, cf a) { return cf{s * a.re, s * a.im}; }
+DANSE_DEV cf conjg(cf a) { return cf{a.re, -a.im}; }
+DANSE_DEV float abs2(cf a) { return a.re * a.re + a.im * a.im; }
+// a * conj(b)
+DANSE_DEV cf mulc(cf a, cf b) { return cf{a.re * b.re + a.im * b.im, a.im * b.re - a.re * b.im}; }
+// conj(a) * b
+DANSE_DEV cf cmul(cf a, cf b) { return cf{a.re * b.re + a.im * b.im, a.re * b.im - a.im * b.re}; }
+// acc += a * b
+DANSE_DEV void fma_c(cf& acc, cf a, cf b) {
+  acc.re = fmaf(a.re, b.re, fmaf(-a.im, b.im, acc.re));
+  acc.im = fmaf(a.re, b.im, fmaf(a.im, b.re, acc.im));
+}
+// acc -= a * b
+DANSE_DEV void fms_c(cf& acc, cf a, cf b) {
+  acc.re = fmaf(-a.re, b.re, fmaf(a.im, b.im, acc.re));
+  acc.im = fmaf(-a.re, b.im, fmaf(-a.im, b.re, acc.im));
+}
+// acc -= a * conj(b)
+DANSE_DEV void fms_cc(cf& acc, cf a, cf b) {
+  acc.re = fmaf(-a.re, b.re, fmaf(-a.im, b.im, acc.re));
+  acc.im = fmaf(-a.im, b.re, fmaf(a.re, b.im, acc.im));
+}
+DANSE_DEV cf cdiv_real(cf a, float s) {
+  float r = 1.0f / s;
+  return cf{a.re * r, a.im * r};
+}
+
+DANSE_DEV int lane_id() { return __lane_id(); }
+
+// ---------------------------------------------------------------------------
+// Lane-group broadcast: value of lane `SRC` of my group of G lanes.
+//   G == 64 : v_readlane_b32 (wave-uniform SGPR result)
+//   G == 16 : DPP row_newbcast (gfx90a+ "row share"), one VALU op, no LDS
+//   G == 4  : DPP quad_perm
+//   G == 32 : ds_bpermute
+// ---------------------------------------------------------------------------
+template <int G, int SRC>
+DANSE_DEV float gbcast(float x) {
+  static_assert(SRC >= 0 && SRC < G, "source lane out of group");
+  if constexpr (G == 64) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), SRC));
+  } else if constexpr (G == 4) {
+    constexpr int qp = SRC | (SRC << 2) | (SRC << 4) | (SRC << 6);   // DPP quad_perm
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), qp, 0xF, 0xF, false));
+  } else if constexpr (G == 16) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x150 + SRC, 0xF, 0xF, false));
+  } else {
+    int base = (lane_id() & ~(G - 1)) + SRC;
+    return __int_as_float(__builtin_amdgcn_ds_bpermute(base << 2, __float_as_int(x)));
+  }
+}
+
+template <int G, int SRC>
+DANSE_DEV cf gbcast(cf x) {
+  return cf{gbcast<G, SRC>(x.re), gbcast<G, SRC>(x.im)};
+}
+
+// Runtime source lane (wave-uniform for G == 64, group-uniform otherwise).
+template <int G>
+DANSE_DEV float gbcast_rt(float x, int src) {
+  if constexpr (G == 64) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), src));
+  } else {
+    int base = (lane_id() & ~(G - 1)) + src;
+    return __int_as_float(__builtin_amdgcn_ds_bpermute(base << 2, __float_as_int(x)));
+  }
+}
+template <int G>
+DANSE_DEV cf gbcast_rt(cf x, int src) {
+  return cf{gbcast_rt<G>(x.re, src), gbcast_rt<G>(x.im, src)};
+}
+
+// Sum over the G lanes of my group (result in every lane of the group).
+template <int G>
+DANSE_DEV float gsum(float x) {
+#pragma unroll
+  for (int m = 1; m < G; m <<= 1) x += __shfl_xor(x, m, G);
+  return x;
+}
+template <int G>
+DANSE_DEV cf gsum(cf x) {
+#pragma unroll
+  for (int m = 1; m < G; m <<= 1) {
+    x.re += __shfl_xor(x.re, m, G);
+    x.im += __shfl_xor(x.im, m, G);
+  }
+  return x;
+}
+template <int G>
+DANSE_DEV float gmax(float x) {
+#pragma unroll
+  for (int m = 1; m < G; m <<= 1) x = fmaxf(x, __shfl_xor(x, m, G));
+  return x;
+}
+template <int G>
+DANSE_DEV float gmin(float x) {
+#pragma unroll
+  for (int m = 1; m < G; m <<= 1) x = fminf(x, __shfl_xor(x, m, G));
+  return x;
+}
+// Group ballot: bit i set if lane i of my group has pred.
+template <int G>
+DANSE_DEV uint64_t gballot(bool pred) {
+  uint64_t b = __ballot(pred);
+  if constexpr (G == 64) {
+    return b;
+  } else {
+    const int sh = lane_id() & ~(G - 1);
+    return (b >> sh) & ((1ull << G) - 1ull);
+  }
+}

@@ -1,0 +1,762 @@
+// Host side of the C-ABI (include/danse_mi355x.h): engine state, launch
+// sequencing, hipGraph capture, and the fine-grained operators.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "kernels.hpp"
+
+using namespace danse;
+
+namespace {
+
+constexpr int kF = 513;
+
+struct Class {
+  int G, DMAX;
+  std::vector<FamNode> host;
+  std::vector<int> ids;
+  FamNode* dev = nullptr;
+  int* devIds = nullptr;
+};
+
+template <typename T>
+hipError_t dalloc(T** p, size_t n) {
+  if (n == 0) n = 1;
+  return hipMalloc((void**)p, n * sizeof(T));
+}
+
+}  // namespace
+
+struct danse_engine {
+  int dev = 0;
+  std::string err;
+  int S, K, MT, N, Ns, F, T, R, k0, k1;
+  int gevd, rank, ref, families, keepHistory;
+  float alphaExt;
+  std::vector<int> M, base, extMode;
+  std::vector<FamNode> fns;   // all family-nodes (owned nodes)
+  std::vector<int> chanList;
+  std::vector<Class> classes;
+  long long scmStride = 0, wStride = 0, wExtStride = 0, tgtStride = 0;
+  std::vector<long long> wExtNodeOff;
+  // device
+  int *dM = nullptr, *dBase = nullptr, *dBcEnd = nullptr, *dUpEnd = nullptr, *dChan = nullptr;
+  uint8_t* dFlags = nullptr;
+  float *dBeta = nullptr, *dBetaExt = nullptr, *dhA = nullptr, *dhS = nullptr, *dNorm = nullptr;
+  cf* dTw = nullptr;
+  long long* dWExtNodeOff = nullptr;
+  const float* y = nullptr;
+  cf *Yspec = nullptr, *Zspec = nullptr, *Ryy = nullptr, *Rnn = nullptr, *wHist = nullptr, *wExtHist = nullptr,
+     *wExtTarget = nullptr, *dhat = nullptr;
+  float *zPrev = nullptr, *zStream = nullptr, *d = nullptr;
+  int* diag = nullptr;
+  hipGraphExec_t graphExec = nullptr;
+  int graphR0 = -1, graphR1 = -1;
+  void* graphStream = nullptr;
+  bool ownZspec = true;
+  // initial-state copies for danse_engine_reset
+  std::vector<long long> initW0Off, initScmOff, extSrcOff, tgtOff;
+  cf *dW0 = nullptr, *dScm0 = nullptr, *dExt0 = nullptr, *dTgt0 = nullptr;
+  FamNode* dFnAll = nullptr;
+  long long *dInitW0Off = nullptr, *dInitScmOff = nullptr, *dExtSrcOff = nullptr, *dTgtOff = nullptr;
+};
+
+static thread_local std::string g_lastErr;
+
+#define HIPCHK(expr)                                                                  \
+  do {                                                                                \
+    hipError_t _e = (expr);                                                           \
+    if (_e != hipSuccess) {                                                           \
+      std::string m = std::string(#expr) + ": " + hipGetErrorString(_e);              \
+      if (eng) eng->err = m;                                                          \
+      g_lastErr = m;                                                                  \
+      return -2;                                                                      \
+    }                                                                                 \
+  } while (0)
+
+static int fail(danse_engine* eng, const std::string& m) {
+  if (eng) eng->err = m;
+  g_lastErr = m;
+  return -1;
+}
+
+static void pick_class(int D, int& G, int& DMAX) {
+  if (D <= 4) { G = 4; DMAX = 4; }
+  else if (D <= 8) { G = 16; DMAX = 8; }
+  else if (D <= 12) { G = 16; DMAX = 12; }
+  else if (D <= 16) { G = 16; DMAX = 16; }
+  else if (D <= 24) { G = 32; DMAX = 24; }
+  else if (D <= 32) { G = 32; DMAX = 32; }
+  else if (D <= 40) { G = 64; DMAX = 40; }
+  else { G = 64; DMAX = 64; }
+}
+
+// Re-initialise filters (slot 0 of the histories) and SCMs of every
+// (scene, family-node): one block row per (scene, family-node).
+__global__ void reset_fam_kernel(const FamNode* fns, int nFN, const long long* w0Off, const long long* scmOff,
+                                 const cf* w0, const cf* scm0, cf* wHist, long long wStride, cf* Ryy, cf* Rnn,
+                                 long long scmStride, int F) {
+  const int s = blockIdx.y / nFN;
+  const int i = blockIdx.y % nFN;
+  const FamNode fn = fns[i];
+  const int D = fn.D;
+  const long long nS = (long long)F * D * D;
+  const long long nW = (long long)F * D;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < nS; e += (long long)gridDim.x * blockDim.x) {
+    const cf v = scm0[scmOff[i] + e % ((long long)D * D)];
+    Ryy[s * scmStride + fn.scmOff + e] = v;
+    Rnn[s * scmStride + fn.scmOff + e] = v;
+    if (e < nW) wHist[s * wStride + fn.wOff + e] = w0[w0Off[i] + e];
+  }
+}
+
+__global__ void reset_ext_kernel(const int* M, int k0, int k1, const long long* srcOff, const long long* dstOff,
+                                 const long long* tgtOff, const cf* ext0, const cf* tgt0, cf* wExtHist,
+                                 long long wExtStride, cf* tgt, long long tgtStride, int F) {
+  const int nOwn = k1 - k0;
+  const int s = blockIdx.y / nOwn;
+  const int k = k0 + blockIdx.y % nOwn;
+  const long long n = (long long)F * M[k];
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+    wExtHist[s * wExtStride + dstOff[k] + e] = ext0[srcOff[k] + e];
+    tgt[s * tgtStride + tgtOff[k] + e] = tgt0[srcOff[k] + e];
+  }
+}
+
+int danse_engine_reset(danse_engine* eng, void* stream) {
+  if (!eng) return fail(eng, "null engine");
+  HIPCHK(hipSetDevice(eng->dev));
+  hipStream_t st = (hipStream_t)stream;
+  const int S = eng->S, K = eng->K, F = eng->F, R = eng->R;
+  HIPCHK(hipMemsetAsync(eng->zPrev, 0, (size_t)S * K * eng->N * sizeof(float), st));
+  HIPCHK(hipMemsetAsync(eng->zStream, 0, (size_t)S * K * R * eng->Ns * sizeof(float), st));
+  HIPCHK(hipMemsetAsync(eng->dhat, 0, (size_t)kMaxFam * S * K * R * F * sizeof(cf), st));
+  HIPCHK(hipMemsetAsync(eng->d, 0, (size_t)kMaxFam * S * K * eng->T * sizeof(float), st));
+  HIPCHK(hipMemsetAsync(eng->diag, 0, (size_t)S * K * kMaxFam * sizeof(int), st));
+  const int nFN = (int)eng->fns.size();
+  hipLaunchKernelGGL(reset_fam_kernel, dim3(64, S * nFN), dim3(256), 0, st, eng->dFnAll, nFN, eng->dInitW0Off,
+                     eng->dInitScmOff, eng->dW0, eng->dScm0, eng->wHist, eng->wStride, eng->Ryy, eng->Rnn,
+                     eng->scmStride, F);
+  HIPCHK(hipGetLastError());
+  hipLaunchKernelGGL(reset_ext_kernel, dim3(8, S * (eng->k1 - eng->k0)), dim3(256), 0, st, eng->dM, eng->k0, eng->k1,
+                     eng->dExtSrcOff, eng->dWExtNodeOff, eng->dTgtOff, eng->dExt0, eng->dTgt0, eng->wExtHist,
+                     eng->wExtStride, eng->wExtTarget, eng->tgtStride, F);
+  HIPCHK(hipGetLastError());
+  if (st == nullptr) HIPCHK(hipDeviceSynchronize());
+  return 0;
+}
+
+const char* danse_last_error(const danse_engine* eng) {
+  if (eng && !eng->err.empty()) return eng->err.c_str();
+  return g_lastErr.c_str();
+}
+
+int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
+  danse_engine* eng = nullptr;
+  if (!c || !out) return fail(nullptr, "null argument");
+  if (c->N != 1024) return fail(nullptr, "only DFTsize 1024 is supported by the HIP FFT");
+  if (c->K < 2 || c->S < 1 || c->R < 1) return fail(nullptr, "bad sizes");
+  if (c->k0 < 0 || c->k1 > c->K || c->k0 >= c->k1) return fail(nullptr, "bad owned node range");
+  if (c->rank < 1 || c->rank > kRMax) return fail(nullptr, "GEVD rank out of range [1, 4]");
+  eng = new danse_engine();
+  eng->dev = device;
+  HIPCHK(hipSetDevice(device));
+  eng->S = c->S; eng->K = c->K; eng->N = c->N; eng->Ns = c->Ns; eng->F = c->N / 2 + 1; eng->T = c->T;
+  eng->R = c->R; eng->k0 = c->k0; eng->k1 = c->k1; eng->gevd = c->gevd; eng->rank = c->rank; eng->ref = c->ref;
+  eng->families = c->families | 1; eng->keepHistory = c->keepHistory; eng->alphaExt = c->alphaExt;
+  const int K = c->K, S = c->S, F = eng->F, R = c->R;
+  eng->M.assign(c->M, c->M + K);
+  eng->extMode.assign(c->extMode, c->extMode + K);
+  eng->base.resize(K);
+  int mt = 0;
+  for (int k = 0; k < K; ++k) { eng->base[k] = mt; mt += eng->M[k]; }
+  eng->MT = mt;
+  if (c->ref < 0) return fail(eng, "bad reference sensor");
+  for (int k = 0; k < K; ++k)
+    if (c->ref >= eng->M[k]) return fail(eng, "referenceSensor must be < M_k for every node");
+
+  // ---- family-node table (owned nodes), channel lists
+  long long scmOff = 0, wOff = 0;
+  const long long histW = c->keepHistory ? (long long)R + 1 : 2;
+  for (int fam = 0; fam < kMaxFam; ++fam) {
+    if (!((eng->families >> fam) & 1)) continue;
+    for (int k = c->k0; k < c->k1; ++k) {
+      FamNode fn{};
+      fn.fam = fam; fn.k = k; fn.M = eng->M[k]; fn.extMode = (fam == DANSE_FAM_DANSE) ? eng->extMode[k] : -1;
+      fn.chanOff = (int)eng->chanList.size();
+      if (fam == DANSE_FAM_DANSE || fam == DANSE_FAM_SSBC) {
+        for (int m = 0; m < eng->M[k]; ++m) eng->chanList.push_back(eng->base[k] + m);
+        for (int q = 0; q < K; ++q)
+          if (q != k) eng->chanList.push_back(fam == DANSE_FAM_DANSE ? mt + q : eng->base[q]);
+        fn.D = eng->M[k] + K - 1;
+        fn.ref = c->ref;
+      } else if (fam == DANSE_FAM_LOCAL) {
+        for (int m = 0; m < eng->M[k]; ++m) eng->chanList.push_back(eng->base[k] + m);
+        fn.D = eng->M[k];
+        fn.ref = c->ref;
+      } else {
+        for (int ch = 0; ch < mt; ++ch) eng->chanList.push_back(ch);
+        fn.D = mt;
+        fn.ref = eng->base[k] + c->ref;
+      }
+      if (fn.D > 16) return fail(eng, "filter dimension > 16 not supported yet");
+      if (c->gevd && c->rank > fn.D) return fail(eng, "GEVD rank larger than a filter dimension");
+      fn.scmOff = scmOff;
+      scmOff += (long long)F * fn.D * fn.D;
+      fn.wOff = wOff;
+      wOff += histW * F * fn.D;
+      eng->fns.push_back(fn);
+    }
+  }
+  eng->scmStride = scmOff;
+  eng->wStride = wOff;
+  eng->wExtNodeOff.assign(K, 0);
+  long long eo = 0, to = 0;
+  for (int k = 0; k < K; ++k) {
+    eng->wExtNodeOff[k] = eo;
+    eo += histW * F * eng->M[k];
+  }
+  eng->wExtStride = eo;
+  std::vector<long long> tgtOff(K);
+  for (int k = 0; k < K; ++k) { tgtOff[k] = to; to += (long long)F * eng->M[k]; }
+  eng->tgtStride = to;
+  for (auto& fn : eng->fns) {
+    if (fn.fam == DANSE_FAM_DANSE) { fn.wExtOff = eng->wExtNodeOff[fn.k]; fn.tgtOff = tgtOff[fn.k]; }
+  }
+  for (size_t i = 0; i < eng->fns.size(); ++i) {
+    int G, DM;
+    pick_class(eng->fns[i].D, G, DM);
+    Class* cl = nullptr;
+    for (auto& x : eng->classes)
+      if (x.G == G && x.DMAX == DM) cl = &x;
+    if (!cl) { eng->classes.push_back(Class{G, DM, {}, {}, nullptr, nullptr}); cl = &eng->classes.back(); }
+    cl->host.push_back(eng->fns[i]);
+    cl->ids.push_back((int)i);
+  }
+
+  // ---- device allocations
+  HIPCHK(dalloc(&eng->dM, K));
+  HIPCHK(dalloc(&eng->dBase, K));
+  HIPCHK(dalloc(&eng->dBcEnd, (size_t)R * K));
+  HIPCHK(dalloc(&eng->dUpEnd, (size_t)R * K));
+  HIPCHK(dalloc(&eng->dChan, eng->chanList.size()));
+  HIPCHK(dalloc(&eng->dFlags, (size_t)R * S * kMaxFam * K));
+  HIPCHK(dalloc(&eng->dBeta, (size_t)S * K));
+  HIPCHK(dalloc(&eng->dBetaExt, (size_t)S * K));
+  HIPCHK(dalloc(&eng->dhA, (size_t)c->N));
+  HIPCHK(dalloc(&eng->dhS, (size_t)c->N));
+  HIPCHK(dalloc(&eng->dNorm, (size_t)c->Ns));
+  HIPCHK(dalloc(&eng->dTw, (size_t)c->N));
+  HIPCHK(dalloc(&eng->dWExtNodeOff, (size_t)K));
+  HIPCHK(hipMemcpy(eng->dM, eng->M.data(), K * sizeof(int), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(eng->dBase, eng->base.data(), K * sizeof(int), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(eng->dBcEnd, c->bcEnd, (size_t)R * K * sizeof(int), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(eng->dUpEnd, c->upEnd, (size_t)R * K * sizeof(int), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(eng->dChan, eng->chanList.data(), eng->chanList.size() * sizeof(int), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(eng->dFlags, c->flags, (size_t)R * S * kMaxFam * K, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(eng->dBeta, c->beta, (size_t)S * K * sizeof(float), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(eng->dBetaExt, c->betaExt, (size_t)S * K * sizeof(float), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(eng->dhA, c->winAnalysis, c->N * sizeof(float), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(eng->dhS, c->winSynthesis, c->N * sizeof(float), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(eng->dWExtNodeOff, eng->wExtNodeOff.data(), K * sizeof(long long), hipMemcpyHostToDevice));
+  {
+    // OLA normalisation h^2[n] + h^2[n + Ns] (d_base.py:1843-1852), in double then rounded
+    std::vector<float> nv(c->Ns);
+    const int nOv = c->N / c->Ns;
+    std::vector<double> acc(c->N + c->Ns, 0.0);
+    for (int ii = 0; ii < nOv; ++ii)
+      for (int n = 0; n < c->N; ++n) acc[ii * c->Ns + n] += (double)c->winAnalysis[n] * c->winAnalysis[n];
+    for (int n = 0; n < c->Ns; ++n) nv[n] = (float)acc[c->Ns + n];
+    HIPCHK(hipMemcpy(eng->dNorm, nv.data(), c->Ns * sizeof(float), hipMemcpyHostToDevice));
+    std::vector<cf> tw(c->N);
+    for (int m = 0; m < c->N; ++m) {
+      const double ang = -2.0 * M_PI * (double)m / (double)c->N;
+      tw[m] = cf{(float)std::cos(ang), (float)std::sin(ang)};
+    }
+    HIPCHK(hipMemcpy(eng->dTw, tw.data(), c->N * sizeof(cf), hipMemcpyHostToDevice));
+  }
+  for (auto& cl : eng->classes) {
+    HIPCHK(dalloc(&cl.dev, cl.host.size()));
+    HIPCHK(dalloc(&cl.devIds, cl.ids.size()));
+    HIPCHK(hipMemcpy(cl.dev, cl.host.data(), cl.host.size() * sizeof(FamNode), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(cl.devIds, cl.ids.data(), cl.ids.size() * sizeof(int), hipMemcpyHostToDevice));
+  }
+  const size_t MT = (size_t)eng->MT;
+  HIPCHK(dalloc(&eng->Yspec, 2 * S * MT * F));
+  HIPCHK(dalloc(&eng->Zspec, (size_t)K * S * F));
+  HIPCHK(dalloc(&eng->zPrev, (size_t)S * K * c->N));
+  HIPCHK(dalloc(&eng->zStream, (size_t)S * K * R * c->Ns));
+  HIPCHK(dalloc(&eng->Ryy, (size_t)S * eng->scmStride));
+  HIPCHK(dalloc(&eng->Rnn, (size_t)S * eng->scmStride));
+  HIPCHK(dalloc(&eng->wHist, (size_t)S * eng->wStride));
+  HIPCHK(dalloc(&eng->wExtHist, (size_t)S * eng->wExtStride));
+  HIPCHK(dalloc(&eng->wExtTarget, (size_t)S * eng->tgtStride));
+  HIPCHK(dalloc(&eng->dhat, (size_t)kMaxFam * S * K * R * F));
+  HIPCHK(dalloc(&eng->d, (size_t)kMaxFam * S * K * c->T));
+  HIPCHK(dalloc(&eng->diag, (size_t)S * K * kMaxFam));
+  HIPCHK(hipMemset(eng->Yspec, 0, 2 * S * MT * F * sizeof(cf)));
+  HIPCHK(hipMemset(eng->Zspec, 0, (size_t)K * S * F * sizeof(cf)));
+  HIPCHK(hipMemset(eng->zPrev, 0, (size_t)S * K * c->N * sizeof(float)));
+  HIPCHK(hipMemset(eng->zStream, 0, (size_t)S * K * R * c->Ns * sizeof(float)));
+  HIPCHK(hipMemset(eng->dhat, 0, (size_t)kMaxFam * S * K * R * F * sizeof(cf)));
+  HIPCHK(hipMemset(eng->d, 0, (size_t)kMaxFam * S * K * c->T * sizeof(float)));
+  HIPCHK(hipMemset(eng->diag, 0, (size_t)S * K * kMaxFam * sizeof(int)));
+  HIPCHK(hipMemset(eng->Ryy, 0, (size_t)S * eng->scmStride * sizeof(cf)));
+  HIPCHK(hipMemset(eng->Rnn, 0, (size_t)S * eng->scmStride * sizeof(cf)));
+  HIPCHK(hipMemset(eng->wHist, 0, (size_t)S * eng->wStride * sizeof(cf)));
+  HIPCHK(hipMemset(eng->wExtHist, 0, (size_t)S * eng->wExtStride * sizeof(cf)));
+
+  // ---- initial state: host arrays are per family-node over ALL K nodes
+  // (family-major); keep device copies so that danse_engine_reset() can
+  // re-initialise the state on a stream.
+  {
+    std::vector<cf> w0h, scmh;
+    long long w0Off = 0, scmInOff = 0;
+    for (int fam = 0; fam < kMaxFam; ++fam) {
+      if (!((eng->families >> fam) & 1)) continue;
+      for (int k = 0; k < K; ++k) {
+        int D = (fam == DANSE_FAM_LOCAL) ? eng->M[k] : (fam == DANSE_FAM_CENTR ? (int)MT : eng->M[k] + K - 1);
+        for (auto& x : eng->fns) {
+          if (x.fam == fam && x.k == k) {
+            eng->initW0Off.push_back((long long)w0h.size());
+            eng->initScmOff.push_back((long long)scmh.size());
+            for (long long e = 0; e < (long long)F * D; ++e)
+              w0h.push_back(c->w0 ? cf{c->w0[2 * (w0Off + e)], c->w0[2 * (w0Off + e) + 1]} : cf{0.0f, 0.0f});
+            for (long long e = 0; e < (long long)D * D; ++e)
+              scmh.push_back(c->scmInit ? cf{c->scmInit[2 * (scmInOff + e)], c->scmInit[2 * (scmInOff + e) + 1]}
+                                        : cf{0.0f, 0.0f});
+          }
+        }
+        w0Off += (long long)F * D;
+        scmInOff += (long long)D * D;
+      }
+    }
+    std::vector<cf> exth, tgth;
+    long long eOff = 0;
+    for (int k = 0; k < K; ++k) {
+      for (long long e = 0; e < (long long)F * eng->M[k]; ++e) {
+        exth.push_back(c->wExt0 ? cf{c->wExt0[2 * (eOff + e)], c->wExt0[2 * (eOff + e) + 1]} : cf{0.0f, 0.0f});
+        tgth.push_back(c->wExtTarget0 ? cf{c->wExtTarget0[2 * (eOff + e)], c->wExtTarget0[2 * (eOff + e) + 1]}
+                                      : cf{0.0f, 0.0f});
+      }
+      eOff += (long long)F * eng->M[k];
+    }
+    eng->tgtOff = tgtOff;
+    HIPCHK(dalloc(&eng->dW0, w0h.size()));
+    HIPCHK(dalloc(&eng->dScm0, scmh.size()));
+    HIPCHK(dalloc(&eng->dExt0, exth.size()));
+    HIPCHK(dalloc(&eng->dTgt0, tgth.size()));
+    HIPCHK(hipMemcpy(eng->dW0, w0h.data(), w0h.size() * sizeof(cf), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(eng->dScm0, scmh.data(), scmh.size() * sizeof(cf), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(eng->dExt0, exth.data(), exth.size() * sizeof(cf), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(eng->dTgt0, tgth.data(), tgth.size() * sizeof(cf), hipMemcpyHostToDevice));
+    eng->extSrcOff.assign(K, 0);
+    long long acc = 0;
+    for (int k = 0; k < K; ++k) { eng->extSrcOff[k] = acc; acc += (long long)F * eng->M[k]; }
+    HIPCHK(dalloc(&eng->dFnAll, eng->fns.size()));
+    HIPCHK(hipMemcpy(eng->dFnAll, eng->fns.data(), eng->fns.size() * sizeof(FamNode), hipMemcpyHostToDevice));
+    HIPCHK(dalloc(&eng->dInitW0Off, eng->fns.size()));
+    HIPCHK(dalloc(&eng->dInitScmOff, eng->fns.size()));
+    HIPCHK(hipMemcpy(eng->dInitW0Off, eng->initW0Off.data(), eng->fns.size() * sizeof(long long), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(eng->dInitScmOff, eng->initScmOff.data(), eng->fns.size() * sizeof(long long),
+                     hipMemcpyHostToDevice));
+    HIPCHK(dalloc(&eng->dExtSrcOff, K));
+    HIPCHK(dalloc(&eng->dTgtOff, K));
+    HIPCHK(hipMemcpy(eng->dExtSrcOff, eng->extSrcOff.data(), K * sizeof(long long), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(eng->dTgtOff, tgtOff.data(), K * sizeof(long long), hipMemcpyHostToDevice));
+  }
+  {
+    int rc = danse_engine_reset(eng, nullptr);
+    if (rc) return rc;
+  }
+  HIPCHK(hipDeviceSynchronize());
+  *out = eng;
+  return 0;
+}
+
+void danse_engine_destroy(danse_engine* eng) {
+  if (!eng) return;
+  (void)hipSetDevice(eng->dev);
+  if (eng->graphExec) (void)hipGraphExecDestroy(eng->graphExec);
+  void* ptrs[] = {eng->dM, eng->dBase, eng->dBcEnd, eng->dUpEnd, eng->dChan, eng->dFlags, eng->dBeta, eng->dBetaExt,
+                  eng->dhA, eng->dhS, eng->dNorm, eng->dTw, eng->dWExtNodeOff, eng->Yspec,
+                  eng->ownZspec ? eng->Zspec : nullptr, eng->Ryy,
+                  eng->Rnn, eng->wHist, eng->wExtHist, eng->wExtTarget, eng->dhat, eng->zPrev, eng->zStream, eng->d,
+                  eng->diag, eng->dW0, eng->dScm0, eng->dExt0, eng->dTgt0, eng->dFnAll, eng->dInitW0Off,
+                  eng->dInitScmOff, eng->dExtSrcOff, eng->dTgtOff};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  for (auto& cl : eng->classes) {
+    if (cl.dev) (void)hipFree(cl.dev);
+    if (cl.devIds) (void)hipFree(cl.devIds);
+  }
+  delete eng;
+}
+
+int danse_engine_set_inputs(danse_engine* eng, const float* yDev) {
+  if (!eng || !yDev) return fail(eng, "null argument");
+  eng->y = yDev;
+  return 0;
+}
+
+static BcastArgs make_bcast(danse_engine* e, int r, int synth, int bc) {
+  BcastArgs a{};
+  a.S = e->S; a.K = e->K; a.MT = e->MT; a.T = e->T; a.N = e->N; a.Ns = e->Ns; a.F = e->F; a.R = e->R;
+  a.r = r; a.k0 = e->k0; a.k1 = e->k1; a.families = e->families; a.doSynth = synth; a.doBcast = bc;
+  a.M = e->dM; a.base = e->dBase; a.bcEnd = e->dBcEnd; a.upEnd = e->dUpEnd; a.y = e->y;
+  a.Yspec = e->Yspec; a.Zspec = e->Zspec; a.zPrev = e->zPrev; a.zStream = e->zStream;
+  a.wExtHist = e->wExtHist; a.wExtNodeOff = e->dWExtNodeOff; a.wExtStride = e->wExtStride;
+  a.wExtHistory = e->keepHistory; a.dhat = e->dhat; a.d = e->d; a.hA = e->dhA; a.hS = e->dhS; a.normVal = e->dNorm;
+  a.tw = e->dTw;
+  return a;
+}
+
+static UpdateArgs make_update(danse_engine* e, int r) {
+  UpdateArgs a{};
+  a.S = e->S; a.K = e->K; a.MT = e->MT; a.F = e->F; a.R = e->R; a.r = r;
+  a.chanList = e->dChan; a.flags = e->dFlags; a.Yspec = e->Yspec; a.Zspec = e->Zspec;
+  a.Ryy = e->Ryy; a.Rnn = e->Rnn; a.scmStride = e->scmStride; a.wHist = e->wHist; a.wStride = e->wStride;
+  a.wHistory = e->keepHistory; a.wExtHist = e->wExtHist; a.wExtStride = e->wExtStride; a.wExtHistory = e->keepHistory;
+  a.wExtTarget = e->wExtTarget; a.tgtStride = e->tgtStride; a.dhat = e->dhat; a.beta = e->dBeta;
+  a.betaExt = e->dBetaExt; a.alphaExt = e->alphaExt; a.gevd = e->gevd; a.rank = e->rank; a.diag = e->diag;
+  return a;
+}
+
+template <int G, int DM>
+static void launch_update_cls(const UpdateArgs& a, int nFN, hipStream_t st) {
+  constexpr int NB = 64 / G;
+  const int nBB = (a.F + NB - 1) / NB;
+  const unsigned grid = (unsigned)(a.S * nFN * nBB);
+  hipLaunchKernelGGL((update_kernel<G, DM>), dim3(grid), dim3(64), 0, st, a);
+}
+
+static void launch_update(danse_engine* e, int r, hipStream_t st) {
+  for (auto& cl : e->classes) {
+    UpdateArgs a = make_update(e, r);
+    a.nFN = (int)cl.host.size();
+    a.fn = cl.dev;
+    a.famNodeId = cl.devIds;
+    switch (cl.DMAX) {
+      case 4: launch_update_cls<4, 4>(a, a.nFN, st); break;
+      case 8: launch_update_cls<16, 8>(a, a.nFN, st); break;
+      case 12: launch_update_cls<16, 12>(a, a.nFN, st); break;
+      case 16: launch_update_cls<16, 16>(a, a.nFN, st); break;
+      default: break;   // D > 16: rejected at create time (see pick_class)
+    }
+  }
+}
+
+static void launch_bcast(danse_engine* e, int r, int synth, int bc, hipStream_t st) {
+  BcastArgs a = make_bcast(e, r, synth, bc);
+  const unsigned grid = (unsigned)(e->S * (e->k1 - e->k0));
+  hipLaunchKernelGGL(bcast_kernel, dim3(grid), dim3(256), 0, st, a);
+}
+
+int danse_engine_bcast(danse_engine* eng, int32_t r, void* stream) {
+  if (!eng || !eng->y) return fail(eng, "inputs not set");
+  if (r < 0 || r >= eng->R) return fail(eng, "round out of range");
+  HIPCHK(hipSetDevice(eng->dev));
+  launch_bcast(eng, r, r > 0, 1, (hipStream_t)stream);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int danse_engine_update(danse_engine* eng, int32_t r, void* stream) {
+  if (!eng) return fail(eng, "null engine");
+  if (r < 0 || r >= eng->R) return fail(eng, "round out of range");
+  HIPCHK(hipSetDevice(eng->dev));
+  launch_update(eng, r, (hipStream_t)stream);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int danse_engine_finish(danse_engine* eng, void* stream) {
+  if (!eng) return fail(eng, "null engine");
+  HIPCHK(hipSetDevice(eng->dev));
+  launch_bcast(eng, eng->R, 1, 0, (hipStream_t)stream);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int danse_engine_run(danse_engine* eng, int32_t r0, int32_t r1, void* stream, int32_t graph) {
+  if (!eng || !eng->y) return fail(eng, "inputs not set");
+  if (r0 < 0 || r1 > eng->R || r0 >= r1) return fail(eng, "bad round range");
+  HIPCHK(hipSetDevice(eng->dev));
+  hipStream_t st = (hipStream_t)stream;
+  auto seq = [&](hipStream_t s) {
+    for (int r = r0; r < r1; ++r) {
+      launch_bcast(eng, r, r > 0, 1, s);
+      launch_update(eng, r, s);
+    }
+    if (r1 == eng->R) launch_bcast(eng, eng->R, 1, 0, s);
+  };
+  if (!graph) {
+    seq(st);
+    HIPCHK(hipGetLastError());
+    return 0;
+  }
+  if (!(eng->graphExec && eng->graphR0 == r0 && eng->graphR1 == r1)) {
+    if (eng->graphExec) {
+      (void)hipGraphExecDestroy(eng->graphExec);
+      eng->graphExec = nullptr;
+    }
+    hipStream_t cap = st;
+    bool own = false;
+    if (cap == nullptr) {
+      HIPCHK(hipStreamCreateWithFlags(&cap, hipStreamNonBlocking));
+      own = true;
+    }
+    hipGraph_t g;
+    HIPCHK(hipStreamBeginCapture(cap, hipStreamCaptureModeThreadLocal));
+    seq(cap);
+    HIPCHK(hipStreamEndCapture(cap, &g));
+    HIPCHK(hipGraphInstantiate(&eng->graphExec, g, nullptr, nullptr, 0));
+    HIPCHK(hipGraphDestroy(g));
+    if (own) HIPCHK(hipStreamDestroy(cap));
+    eng->graphR0 = r0;
+    eng->graphR1 = r1;
+  }
+  HIPCHK(hipGraphLaunch(eng->graphExec, st));
+  return 0;
+}
+
+int danse_engine_set_zspec(danse_engine* eng, void* ptr) {
+  if (!eng || !ptr) return fail(eng, "null argument");
+  HIPCHK(hipSetDevice(eng->dev));
+  if (eng->ownZspec && eng->Zspec) HIPCHK(hipFree(eng->Zspec));
+  eng->Zspec = (cf*)ptr;
+  eng->ownZspec = false;
+  if (eng->graphExec) {
+    (void)hipGraphExecDestroy(eng->graphExec);
+    eng->graphExec = nullptr;
+    eng->graphR0 = eng->graphR1 = -1;
+  }
+  return 0;
+}
+
+int danse_engine_zspec(danse_engine* eng, void** ptr, size_t* bytes) {
+  if (!eng || !ptr || !bytes) return fail(eng, "null argument");
+  *ptr = eng->Zspec;
+  *bytes = (size_t)eng->K * eng->S * eng->F * sizeof(cf);
+  return 0;
+}
+
+// Resolve the device region of an output.  For per-family-node outputs the
+// region is strided over scenes: (ptr, chunkBytes, sceneStrideBytes).
+static int out_region(danse_engine* e, int which, int family, int node, char** ptr, size_t* chunk, size_t* stride,
+                      int* nChunks) {
+  const int S = e->S, K = e->K, F = e->F;
+  *nChunks = S;
+  if (which == DANSE_OUT_W || which == DANSE_OUT_WEXT) {
+    if (node < e->k0 || node >= e->k1) return fail(e, "node not owned by this engine");
+    const long long hw = e->keepHistory ? (long long)e->R + 1 : 2;
+    if (which == DANSE_OUT_W) {
+      const FamNode* fn = nullptr;
+      for (auto& x : e->fns)
+        if (x.fam == family && x.k == node) fn = &x;
+      if (!fn) return fail(e, "family not computed");
+      *ptr = (char*)(e->wHist + fn->wOff);
+      *chunk = (size_t)hw * F * fn->D * sizeof(cf);
+      *stride = (size_t)e->wStride * sizeof(cf);
+    } else {
+      *ptr = (char*)(e->wExtHist + e->wExtNodeOff[node]);
+      *chunk = (size_t)hw * F * e->M[node] * sizeof(cf);
+      *stride = (size_t)e->wExtStride * sizeof(cf);
+    }
+    return 0;
+  }
+  *nChunks = 1;
+  *stride = 0;
+  if (which == DANSE_OUT_D) {
+    if (!((e->families >> family) & 1)) return fail(e, "family not computed");
+    *ptr = (char*)(e->d + (long long)family * S * K * e->T);
+    *chunk = (size_t)S * K * e->T * sizeof(float);
+  } else if (which == DANSE_OUT_DHAT) {
+    if (!((e->families >> family) & 1)) return fail(e, "family not computed");
+    *ptr = (char*)(e->dhat + (long long)family * S * K * e->R * F);
+    *chunk = (size_t)S * K * e->R * F * sizeof(cf);
+  } else if (which == DANSE_OUT_Z) {
+    *ptr = (char*)e->zStream;
+    *chunk = (size_t)S * K * e->R * e->Ns * sizeof(float);
+  } else if (which == DANSE_OUT_DIAG) {
+    *ptr = (char*)e->diag;
+    *chunk = (size_t)S * K * kMaxFam * sizeof(int);
+  } else {
+    return fail(e, "unknown output");
+  }
+  return 0;
+}
+
+int danse_engine_put(danse_engine* eng, int32_t which, int32_t family, int32_t node, const void* src, size_t bytes,
+                     void* stream) {
+  if (which != DANSE_OUT_W && which != DANSE_OUT_WEXT) return fail(eng, "only W / WEXT can be loaded");
+  char* p;
+  size_t chunk, stride;
+  int n;
+  int rc = out_region(eng, which, family, node, &p, &chunk, &stride, &n);
+  if (rc) return rc;
+  if (bytes < chunk * n) return fail(eng, "source too small");
+  HIPCHK(hipSetDevice(eng->dev));
+  HIPCHK(hipMemcpy2DAsync(p, stride, src, chunk, chunk, n, hipMemcpyDefault, (hipStream_t)stream));
+  HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  return 0;
+}
+
+int danse_engine_output_bytes(danse_engine* eng, int32_t which, int32_t family, int32_t node, size_t* bytes) {
+  char* p;
+  size_t chunk, stride;
+  int n;
+  int rc = out_region(eng, which, family, node, &p, &chunk, &stride, &n);
+  if (rc) return rc;
+  *bytes = chunk * n;
+  return 0;
+}
+
+int danse_engine_get(danse_engine* eng, int32_t which, int32_t family, int32_t node, void* dst, size_t bytes,
+                     void* stream) {
+  char* p;
+  size_t chunk, stride;
+  int n;
+  int rc = out_region(eng, which, family, node, &p, &chunk, &stride, &n);
+  if (rc) return rc;
+  if (bytes < chunk * n) return fail(eng, "destination too small");
+  HIPCHK(hipSetDevice(eng->dev));
+  if (n == 1) {
+    HIPCHK(hipMemcpyAsync(dst, p, chunk, hipMemcpyDefault, (hipStream_t)stream));
+  } else {
+    HIPCHK(hipMemcpy2DAsync(dst, chunk, p, stride, chunk, n, hipMemcpyDefault, (hipStream_t)stream));
+  }
+  HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  return 0;
+}
+
+
+// ---------------------------------------------------------------------------
+// Fine-grained operators
+// ---------------------------------------------------------------------------
+
+__global__ void __launch_bounds__(256) wola_analysis_kernel(const float* x, int T, const int* ends, const float* win,
+                                                            int N, int Ns, cf* out, const cf* tw) {
+  __shared__ cf b0[1024];
+  __shared__ cf b1[1024];
+  const int c = blockIdx.x;
+  load_frame(b0, x + (long long)c * T, ends[c], N, T, win);
+  __syncthreads();
+  cf* o = fft1024(b0, b1, tw);
+  const float inv = 1.0f / sqrtf((float)Ns);
+  const int F = N / 2 + 1;
+  for (int f = threadIdx.x; f < F; f += blockDim.x) out[(long long)c * F + f] = inv * o[f];
+}
+
+template <int G, int DMAX>
+__global__ void __launch_bounds__(64) filter_update_kernel(const cf* Ryy, const cf* Rnn, int B, int D, int gevd,
+                                                          int rank, int ref, cf* w, int* diag) {
+  constexpr int NB = 64 / G;
+  __shared__ SolverLDS<DMAX> lds[NB];
+  const int li = threadIdx.x & (G - 1);
+  const int gi = threadIdx.x / G;
+  int b = blockIdx.x * NB + gi;
+  const bool valid = b < B;
+  if (!valid) b = B - 1;
+  const bool act = li < D;
+  const int row = act ? li : 0;
+  cf A[DMAX], Bm[DMAX];
+  sfor<0, DMAX>([&](auto cc) {
+    constexpr int c = decltype(cc)::value;
+    const int cl = (c < D) ? c : D - 1;
+    const cf a = Ryy[((long long)b * D + row) * D + cl];
+    const cf n = Rnn[((long long)b * D + row) * D + cl];
+    A[c] = (act && c < D) ? a : cf{0.0f, 0.0f};
+    Bm[c] = (act && c < D) ? n : cf{0.0f, 0.0f};
+  });
+  bool ok = true;
+  cf wv;
+  if (gevd) wv = gevd_filter<G, DMAX>(A, Bm, lds[gi], li, D, rank, ref, ok);
+  else wv = mwf_filter<G, DMAX>(A, Bm, li, D, ref, ok);
+  if (act && valid) w[(long long)b * D + li] = wv;
+  if (diag && li == 0 && valid) diag[b] = ok ? 0 : 1;
+}
+
+template <int G, int DM>
+static void launch_fu(const cf* Ryy, const cf* Rnn, int B, int D, int gevd, int rank, int ref, cf* w, int* diag,
+                      hipStream_t st) {
+  constexpr int NB = 64 / G;
+  hipLaunchKernelGGL((filter_update_kernel<G, DM>), dim3((B + NB - 1) / NB), dim3(64), 0, st, Ryy, Rnn, B, D, gevd,
+                     rank, ref, w, diag);
+}
+
+// Batch SCMs: Ryy = mean over VAD frames of y y^H, Rnn over the others.
+// One workgroup per batch item b; thread (i, j) accumulates over frames.
+__global__ void batch_covmats_kernel(const cf* Y, int B, int Tf, int D, const uint8_t* vad, cf* Ryy, cf* Rnn) {
+  const int b = blockIdx.x;
+  const cf* Yb = Y + (long long)b * Tf * D;
+  int nv = 0, nn = 0;
+  for (int t = 0; t < Tf; ++t) (vad[t] ? nv : nn)++;
+  for (int e = threadIdx.x; e < D * D; e += blockDim.x) {
+    const int i = e / D, j = e % D;
+    cf sy = cf{0.0f, 0.0f}, sn = cf{0.0f, 0.0f};
+    for (int t = 0; t < Tf; ++t) {
+      const cf p = mulc(Yb[(long long)t * D + i], Yb[(long long)t * D + j]);
+      if (vad[t]) sy = sy + p;
+      else sn = sn + p;
+    }
+    Ryy[((long long)b * D + i) * D + j] = (nv > 0) ? (1.0f / nv) * sy : cf{NAN, NAN};
+    Rnn[((long long)b * D + i) * D + j] = (nn > 0) ? (1.0f / nn) * sn : cf{NAN, NAN};
+  }
+}
+
+int danse_wola_analysis(const float* x, int32_t C, int32_t T, const int32_t* ends, const float* win, int32_t N,
+                        int32_t Ns, float* out, void* stream) {
+  danse_engine* eng = nullptr;
+  if (N != 1024) return fail(nullptr, "only N = 1024");
+  static cf* tw = nullptr;
+  if (!tw) {
+    std::vector<cf> h(N);
+    for (int m = 0; m < N; ++m) {
+      const double ang = -2.0 * M_PI * m / N;
+      h[m] = cf{(float)std::cos(ang), (float)std::sin(ang)};
+    }
+    HIPCHK(dalloc(&tw, N));
+    HIPCHK(hipMemcpy(tw, h.data(), N * sizeof(cf), hipMemcpyHostToDevice));
+  }
+  hipLaunchKernelGGL(wola_analysis_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, x, T, ends, win, N, Ns,
+                     (cf*)out, tw);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int danse_filter_update(const float* Ryy, const float* Rnn, int32_t B, int32_t D, int32_t gevd, int32_t rank,
+                        int32_t ref, float* w, int32_t* diag, void* stream) {
+  danse_engine* eng = nullptr;
+  if (D < 1 || D > 64) return fail(nullptr, "D must be in [1, 64]");
+  if (gevd && (rank < 1 || rank > kRMax || rank > D)) return fail(nullptr, "bad rank");
+  if (ref < 0 || ref >= D) return fail(nullptr, "bad reference index");
+  int G, DM;
+  pick_class(D, G, DM);
+  hipStream_t st = (hipStream_t)stream;
+  const cf* a = (const cf*)Ryy;
+  const cf* n = (const cf*)Rnn;
+  cf* o = (cf*)w;
+  switch (DM) {
+    case 4: launch_fu<4, 4>(a, n, B, D, gevd, rank, ref, o, diag, st); break;
+    case 8: launch_fu<16, 8>(a, n, B, D, gevd, rank, ref, o, diag, st); break;
+    case 12: launch_fu<16, 12>(a, n, B, D, gevd, rank, ref, o, diag, st); break;
+    case 16: launch_fu<16, 16>(a, n, B, D, gevd, rank, ref, o, diag, st); break;
+    default: return fail(nullptr, "D > 16 not supported yet");
+  }
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int danse_batch_covmats(const float* Y, int32_t B, int32_t Tf, int32_t D, const uint8_t* vad, float* Ryy, float* Rnn,
+                        void* stream) {
+  danse_engine* eng = nullptr;
+  hipLaunchKernelGGL(batch_covmats_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, (const cf*)Y, B, Tf, D, vad,
+                     (cf*)Ryy, (cf*)Rnn);
+  HIPCHK(hipGetLastError());
+  return 0;
+}

@@ -1,0 +1,445 @@
+"""Host driver of the MI355X DANSE engine (device path only — no CPU fallback).
+
+Turns the reference's parameters + a batch of S same-shape scenes into the
+C-ABI configuration (``include/danse_mi355x.h``): integer round tables from
+the host scheduler, per-(round, scene, family, node) control bytes, initial
+filters / SCM slices, and device inputs held in torch tensors.  Outputs come
+back in the reference's layout (the ``dv`` fields consumed by
+``format_output`` / ``DANSEoutputs.from_variables``,
+``danse_toolbox/d_core.py:105-127``, ``danse_toolbox/d_post.py:41-133``).
+
+Control-byte derivation restates, per round i and node k:
+  * counters ``numUpdatesRyy/Rnn`` (``d_classes.py:2094-2100``) and the
+    first-frame-basis rule (``conditional_scm_updating``, 2203-2267), incl.
+    quirk Q11 (centralised SCM: centralised VAD, node counters);
+  * the start gate ``numUpdates > D`` (``check_covariance_matrices``,
+    1482-1540); the Hermitian/PSD/rank checks are evaluated on the device
+    (non-positive Cholesky pivot -> DIAG bit) instead of in fp64 on the host;
+  * seq bypass from the event matrix (``build_events_matrix``,
+    ``d_base.py:1160-1187``) and the external-filter timer
+    (``update_external_filters``, ``d_classes.py:1680-1694``).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib as L
+from .scheduler import initialize_events, compile_rounds
+
+
+def beta_from_t50p(t50p, fs, Ns):
+    """``prep_for_danse._get_beta_from_t50p`` (``d_core.py:485-503``)."""
+    return np.exp(np.log(0.5) / (t50p * fs / Ns))
+
+
+def init_complex_filter(size, refIdx, initType, fixedValue):
+    """``init_complex_filter`` (``d_base.py:2367-2414``) for the
+    deterministic init types (``random`` is not supported on the device)."""
+    if initType == 'selectFirstSensor':
+        w = np.zeros(size, dtype=np.complex128)
+        w[..., refIdx] = 1
+    elif initType == 'fixedValue':
+        w = np.full(size, fixedValue, dtype=np.complex128)
+    elif initType == 'selectFirstSensor_andFixedValue':
+        w = np.full(size, fixedValue, dtype=np.complex128)
+        w[..., refIdx] = 1
+    else:
+        raise NotImplementedError(f'filterInitType {initType!r} on the device path')
+    return w
+
+
+def init_scm_slice(p, Mtot):
+    """``init_covmats`` (``d_base.py:2417-2470``) with the seed of
+    ``init_from_wasn`` (``d_classes.py:553-571``), same-for-all-bins slice."""
+    if p.covMatInitType == 'batch_estimates':
+        raise NotImplementedError('covMatInitType batch_estimates')
+    if not p.covMatSameInitForAllFreqs or not p.covMatSameInitForAllNodes:
+        raise NotImplementedError('per-bin / per-node random SCM init on the device path')
+    rng = np.random.default_rng(p.seed)
+    dims = (Mtot, Mtot)
+    rand = 2 * rng.random(dims) - 1 + 1j * (2 * rng.random(dims) - 1)
+    if p.covMatInitType == 'fully_random':
+        return p.covMatRandomInitScaling * rand
+    eye = np.eye(Mtot) * p.covMatEyeInitScaling
+    if p.covMatInitType == 'eye_and_random':
+        return eye + p.covMatRandomInitScaling * rand
+    if p.covMatInitType == 'eye':
+        return eye
+    raise ValueError(p.covMatInitType)
+
+
+def _cf32(a):
+    return np.ascontiguousarray(np.asarray(a, dtype=np.complex64)).view(np.float32)
+
+
+def _ptr(a, ct):
+    return a.ctypes.data_as(ctypes.POINTER(ct)) if a is not None else None
+
+
+@dataclass
+class FamilyInfo:
+    fam: int
+    name: str
+    D: list       # per node
+    ref: list     # per node
+
+
+class DanseEngine:
+    """One engine = S same-shape scenes x K nodes on one device.
+
+    ``nodeRange`` (k0, k1) restricts the owned nodes (multi-GPU sharding);
+    the fused spectra of the other nodes must then be provided between
+    ``bcast`` and ``update`` (``danse_amd.dist``).
+    """
+
+    def __init__(self, scenes, p, vadMinProp=0.5, device=0, keepHistory=True, nodeRange=None,
+                 pregiven=None, yin='data'):
+        import torch
+        self.torch = torch
+        self.lib = L.load_library()
+        self.p = p
+        self.scenes = list(scenes)
+        sc0 = self.scenes[0]
+        self.S = S = len(self.scenes)
+        self.K = K = sc0.nNodes
+        self.M = [n.nSensors for n in sc0.wasn]
+        self.Mtot = int(sum(self.M))
+        self.N, self.Ns = p.DFTsize, p.Ns
+        self.F = self.N // 2 + 1
+        self.T = sc0.wasn[0].data.shape[0]
+        for sc in self.scenes:
+            if sc.nNodes != K or [n.nSensors for n in sc.wasn] != self.M or sc.wasn[0].data.shape[0] != self.T:
+                raise ValueError('all scenes of one engine must share the WASN shape')
+            if any(not np.array_equal(n.timeStamps, m.timeStamps) for n, m in zip(sc.wasn, sc0.wasn)):
+                raise ValueError('all scenes of one engine must share the node clocks')
+        if p.simType != 'online':
+            raise ValueError('DanseEngine runs the online engine (simType online)')
+        if p.desSigProcessingType != 'wola':
+            raise NotImplementedError('desSigProcessingType conv (T(z) estimate) on the device path')
+        if p.compensateSROs:
+            raise NotImplementedError('SRO compensation on the device path (next round)')
+        self.device = device
+        self.keepHistory = keepHistory
+        self.k0, self.k1 = nodeRange if nodeRange is not None else (0, K)
+        self.nIter = int((self.T - self.N) / self.Ns) + 1
+        neighbors = [list(n.neighborsIdx) for n in sc0.wasn]
+        for k in range(K):
+            if sorted(neighbors[k]) != [q for q in range(K) if q != k]:
+                raise NotImplementedError('device path covers fully connected WASNs')
+        events, fs = initialize_events([n.timeStamps for n in sc0.wasn], [n.fs for n in sc0.wasn], p, neighbors)
+        self.events, self.fsEv = events, fs
+        self.rt = compile_rounds(events, fs, p, K)
+        self.R = R = self.rt.nRounds
+        if R < 1:
+            raise ValueError('signal too short for one DANSE round')
+        if R > self.nIter:
+            raise ValueError('more rounds than reference iterations')
+        # families
+        fams = [L.FAM_DANSE]
+        if p.computeLocal:
+            fams.append(L.FAM_LOCAL)
+        if p.computeCentralised:
+            fams.append(L.FAM_CENTR)
+        if p.computeSingleSensorBroadcast:
+            fams.append(L.FAM_SSBC)
+        self.fams = fams
+        self.famMask = sum(1 << f for f in fams)
+        ref = p.referenceSensor
+        base = np.concatenate(([0], np.cumsum(self.M)[:-1])).astype(int)
+        self.base = base
+        self.Dfam = {
+            L.FAM_DANSE: [self.M[k] + K - 1 for k in range(K)],
+            L.FAM_LOCAL: list(self.M),
+            L.FAM_CENTR: [self.Mtot] * K,
+            L.FAM_SSBC: [self.M[k] + K - 1 for k in range(K)],
+        }
+        self.refFam = {
+            L.FAM_DANSE: [ref] * K, L.FAM_LOCAL: [ref] * K,
+            L.FAM_CENTR: [int(base[k] + ref) for k in range(K)], L.FAM_SSBC: [ref] * K,
+        }
+        if p.performGEVD:
+            for f in fams:
+                if min(self.Dfam[f]) < p.GEVDrank:
+                    raise ValueError('GEVD rank larger than a filter dimension')
+        self.pregiven = pregiven
+        self._build_flags()
+        self._build_cfg()
+        # inputs [S][Mtot][T] float32 on the device
+        y = np.empty((S, self.Mtot, self.T), dtype=np.float32)
+        for s, sc in enumerate(self.scenes):
+            for k, nd in enumerate(sc.wasn):
+                arr = getattr(nd, yin)
+                y[s, base[k]:base[k] + self.M[k], :] = arr.T
+        self.y = torch.from_numpy(y).to(f'cuda:{device}')
+        L.check(self.lib.danse_engine_set_inputs(self.eng, ctypes.c_void_p(self.y.data_ptr())), self.eng)
+        if pregiven is not None:
+            self._load_pregiven(pregiven)
+
+    # ------------------------------------------------------------------ #
+    def _build_flags(self):
+        p, S, K, R = self.p, self.S, self.K, self.R
+        fl = np.zeros((R, S, 4, K), dtype=np.uint8)
+        self.startRound = np.full((S, 4, K), -1, dtype=np.int64)
+        self.nSolves = np.zeros((S, 4, K), dtype=np.int64)
+        vad = np.zeros((S, K, R), dtype=bool)
+        for s, sc in enumerate(self.scenes):
+            for k, nd in enumerate(sc.wasn):
+                v = nd.vadPerFrame
+                if len(v) < R:
+                    raise ValueError('vadPerFrame shorter than the number of rounds')
+                vad[s, k] = v[:R]
+        self.vad = vad
+        cvad = (vad.astype(np.float64).sum(axis=1) / K).astype(bool)   # [S][R] (d_classes.py:905-911)
+        nY = np.cumsum(vad, axis=2)          # counters after the increment of round r
+        nN = np.arange(1, R + 1)[None, None, :] - nY
+        doSolve = self.rt.doSolve.T.astype(bool)    # [K][R]
+        t = self.rt.t
+        tOK = t >= p.startUpdatesAfterAtLeast
+        # external-filter target timer (asy)
+        extT = np.zeros((R, K), dtype=bool)
+        last = np.zeros(K)
+        for r in range(R):
+            for k in range(K):
+                if t[r] - last[k] >= p.timeBtwExternalFiltUpdates:
+                    extT[r, k] = True
+                    last[k] = t[r]
+        basis = p.use1stFrameAsBasis
+        for f in self.fams:
+            for k in range(K):
+                D = self.Dfam[f][k]
+                for s in range(S):
+                    v = cvad[s] if f == L.FAM_CENTR else vad[s, k]
+                    ny, nn = nY[s, k], nN[s, k]
+                    if basis:
+                        opY = np.where(v & (ny == 1), L.OP_SET, np.where(ny > 1, np.where(v, L.OP_AVG, L.OP_KEEP), L.OP_KEEP))
+                        opN = np.where(~v & (nn == 1), L.OP_SET, np.where(nn > 1, np.where(~v, L.OP_AVG, L.OP_KEEP), L.OP_KEEP))
+                    else:
+                        opY = np.where(v, L.OP_AVG, L.OP_KEEP)
+                        opN = np.where(~v, L.OP_AVG, L.OP_KEEP)
+                    gate = (ny > D) & (nn > D) & tOK
+                    started = np.maximum.accumulate(gate)
+                    if started.any():
+                        self.startRound[s, f, k] = int(np.argmax(started))
+                    solve = started & doSolve[k]
+                    if p.bypassUpdates:
+                        solve[:] = False
+                    self.nSolves[s, f, k] = int(solve.sum())
+                    b = opY.astype(np.uint8) | (opN.astype(np.uint8) << 2) | (solve.astype(np.uint8) * L.FLAG_SOLVE)
+                    if f == L.FAM_DANSE:
+                        b = b | (extT[:, k].astype(np.uint8) * L.FLAG_EXT_TARGET)
+                    if self.pregiven is not None:
+                        b = np.full(R, L.FLAG_PREGIVEN, dtype=np.uint8)
+                    fl[:, s, f, k] = b
+        self.flags = fl
+
+    def _build_cfg(self):
+        p, S, K, F = self.p, self.S, self.K, self.F
+        fi = dict(initType=p.filterInitType, fixedValue=p.filterInitFixedValue)
+        w0 = []
+        scm = []
+        sl = init_scm_slice(p, self.Mtot)
+        for f in [0, 1, 2, 3]:
+            if f not in self.fams:
+                continue
+            for k in range(K):
+                D = self.Dfam[f][k]
+                w0.append(init_complex_filter((F, D), self.refFam[f][k], **fi).ravel())
+                if f == L.FAM_LOCAL:
+                    scm.append(sl[:self.M[k], :self.M[k]].ravel())
+                elif f == L.FAM_CENTR:
+                    scm.append(sl.ravel())
+                else:
+                    scm.append(sl[:D, :D].ravel())
+        self._w0 = _cf32(np.concatenate(w0))
+        self._scm = _cf32(np.concatenate(scm))
+        ext = [init_complex_filter((F, self.M[k]), p.referenceSensor, **fi).ravel() for k in range(K)]
+        self._wExt0 = _cf32(np.concatenate(ext))
+        self._tgt0 = self._wExt0.copy()
+        extMode = []
+        for k in range(K):
+            if p.onlyBroadcastRefSensorSigs:
+                extMode.append(L.EXT_REFONLY)
+            elif self.M[k] == 1 and p.noFusionAtSingleSensorNodes:
+                extMode.append(L.EXT_KEEP)
+            elif p.noExternalFilterRelaxation or 'seq' in p.nodeUpdating:
+                extMode.append(L.EXT_COPY)
+            else:
+                extMode.append(L.EXT_RELAX)
+        self._extMode = np.array(extMode, dtype=np.int32)
+        beta = np.zeros((S, K), dtype=np.float32)
+        betaE = np.zeros((S, K), dtype=np.float32)
+        for s, sc in enumerate(self.scenes):
+            for k, nd in enumerate(sc.wasn):
+                beta[s, k] = p.forcedBeta if p.forcedBeta is not None else beta_from_t50p(p.t_expAvg50p, nd.fs, self.Ns)
+                betaE[s, k] = (p.forcedBetaExternalFilters if p.forcedBetaExternalFilters is not None
+                               else beta_from_t50p(p.t_expAvg50pExternalFilters, nd.fs, self.Ns))
+        self._beta, self._betaE = beta, betaE
+        self._M = np.array(self.M, dtype=np.int32)
+        self._hA = np.asarray(p.winWOLAanalysis, dtype=np.float32)
+        self._hS = np.asarray(p.winWOLAsynthesis, dtype=np.float32)
+        self._bc = np.ascontiguousarray(self.rt.bcEnd.astype(np.int32))
+        self._up = np.ascontiguousarray(self.rt.upEnd.astype(np.int32))
+        self._flags = np.ascontiguousarray(self.flags)
+        c = L.DanseCfg()
+        c.S, c.K, c.M = S, K, _ptr(self._M, ctypes.c_int32)
+        c.N, c.Ns, c.T, c.R = self.N, self.Ns, self.T, self.R
+        c.k0, c.k1 = self.k0, self.k1
+        c.gevd, c.rank, c.ref = int(bool(p.performGEVD)), int(p.GEVDrank), int(p.referenceSensor)
+        c.families = self.famMask
+        c.alphaExt = float(p.alphaExternalFilters)
+        c.extMode = _ptr(self._extMode, ctypes.c_int32)
+        c.beta, c.betaExt = _ptr(self._beta, ctypes.c_float), _ptr(self._betaE, ctypes.c_float)
+        c.winAnalysis, c.winSynthesis = _ptr(self._hA, ctypes.c_float), _ptr(self._hS, ctypes.c_float)
+        c.bcEnd, c.upEnd = _ptr(self._bc, ctypes.c_int32), _ptr(self._up, ctypes.c_int32)
+        c.flags = _ptr(self._flags, ctypes.c_uint8)
+        c.w0, c.wExt0, c.wExtTarget0 = (_ptr(self._w0, ctypes.c_float), _ptr(self._wExt0, ctypes.c_float),
+                                        _ptr(self._tgt0, ctypes.c_float))
+        c.scmInit = _ptr(self._scm, ctypes.c_float)
+        c.keepHistory = int(bool(self.keepHistory))
+        self._cfg = c
+        eng = ctypes.c_void_p()
+        L.check(self.lib.danse_engine_create(ctypes.byref(c), int(self.device), ctypes.byref(eng)))
+        self.eng = eng
+
+    def _load_pregiven(self, pg):
+        """Load recorded filter histories (reference layout [F][nIter+1][D])."""
+        R, F = self.R, self.F
+        name = {L.FAM_DANSE: 'internalFilters', L.FAM_LOCAL: 'filtersLocal', L.FAM_CENTR: 'filtersCentr',
+                L.FAM_SSBC: 'filtersSSBC'}
+        for f in self.fams:
+            for k in range(self.k0, self.k1):
+                D = self.Dfam[f][k]
+                arr = np.empty((self.S, R + 1, F, D), dtype=np.complex64)
+                for s in range(self.S):
+                    src = pg[s][name[f]][k] if isinstance(pg, (list, tuple)) else getattr(pg, name[f])[k]
+                    arr[s] = np.transpose(src[:, :R + 1, :], (1, 0, 2))
+                self._put(L.OUT_W, f, k, arr)
+            M = self.M[k]
+            arr = np.empty((self.S, R + 1, F, M), dtype=np.complex64)
+            for s in range(self.S):
+                src = pg[s]['externalFilters'][k] if isinstance(pg, (list, tuple)) else pg.externalFilters[k]
+                arr[s] = np.transpose(src[:, :R + 1, :], (1, 0, 2))
+            self._put(L.OUT_WEXT, 0, k, arr)
+
+    def _put(self, which, fam, node, arr):
+        arr = np.ascontiguousarray(arr)
+        L.check(self.lib.danse_engine_put(self.eng, which, fam, node, arr.ctypes.data_as(ctypes.c_void_p),
+                                          arr.nbytes, None), self.eng)
+
+    # ------------------------------------------------------------------ #
+    def stream_ptr(self, stream=None):
+        t = self.torch
+        st = stream if stream is not None else t.cuda.current_stream(self.device)
+        return ctypes.c_void_p(st.cuda_stream)
+
+    def run(self, graph=True, stream=None):
+        L.check(self.lib.danse_engine_run(self.eng, 0, self.R, self.stream_ptr(stream), int(bool(graph))), self.eng)
+        return self
+
+    def bcast(self, r, stream=None):
+        L.check(self.lib.danse_engine_bcast(self.eng, r, self.stream_ptr(stream)), self.eng)
+
+    def update(self, r, stream=None):
+        L.check(self.lib.danse_engine_update(self.eng, r, self.stream_ptr(stream)), self.eng)
+
+    def finish(self, stream=None):
+        L.check(self.lib.danse_engine_finish(self.eng, self.stream_ptr(stream)), self.eng)
+
+    def zspec(self):
+        ptr = ctypes.c_void_p()
+        nb = ctypes.c_size_t()
+        L.check(self.lib.danse_engine_zspec(self.eng, ctypes.byref(ptr), ctypes.byref(nb)), self.eng)
+        return ptr.value, nb.value
+
+    def _get(self, which, fam=0, node=0, dtype=np.complex64, shape=None):
+        nb = ctypes.c_size_t()
+        L.check(self.lib.danse_engine_output_bytes(self.eng, which, fam, node, ctypes.byref(nb)), self.eng)
+        out = np.empty(nb.value // np.dtype(dtype).itemsize, dtype=dtype)
+        L.check(self.lib.danse_engine_get(self.eng, which, fam, node, out.ctypes.data_as(ctypes.c_void_p),
+                                          out.nbytes, None), self.eng)
+        return out.reshape(shape) if shape is not None else out
+
+    def diagnostics(self):
+        return self._get(L.OUT_DIAG, dtype=np.int32, shape=(self.S, self.K, 4))
+
+    # ------------------------------------------------------------------ #
+    def outputs(self):
+        """Per scene, the ``dv`` fields in the reference layout."""
+        p, S, K, F, R = self.p, self.S, self.K, self.F, self.R
+        nI = self.nIter
+        fi = dict(initType=p.filterInitType, fixedValue=p.filterInitFixedValue)
+        res = [DanseOutputs() for _ in range(S)]
+        hist = R + 1 if self.keepHistory else 2
+        fname = {L.FAM_DANSE: ('wTilde', 'd', 'dhat'), L.FAM_LOCAL: ('wLocal', 'dLocal', 'dHatLocal'),
+                 L.FAM_CENTR: ('wCentr', 'dCentr', 'dHatCentr'), L.FAM_SSBC: ('wSSBC', 'dSSBC', 'dHatSSBC')}
+        for f in self.fams:
+            wn, dn, dhn = fname[f]
+            d = self._get(L.OUT_D, f, dtype=np.float32, shape=(S, K, self.T))
+            dh = self._get(L.OUT_DHAT, f, shape=(S, K, R, F))
+            for s in range(S):
+                setattr(res[s], dn, d[s].T.astype(np.float64))
+                full = np.zeros((F, nI, K), dtype=np.complex128)
+                full[:, :R, :] = np.transpose(dh[s], (2, 1, 0))
+                setattr(res[s], dhn, full)
+                setattr(res[s], wn, [None] * K)
+            for k in range(self.k0, self.k1):
+                D = self.Dfam[f][k]
+                w = self._get(L.OUT_W, f, k, shape=(S, hist, F, D))
+                init = init_complex_filter((F, D), self.refFam[f][k], **fi)
+                for s in range(S):
+                    full = np.empty((F, nI + 1, D), dtype=np.complex128)
+                    full[:] = init[:, None, :]
+                    if self.keepHistory:
+                        full[:, :R + 1, :] = np.transpose(w[s], (1, 0, 2))
+                    getattr(res[s], wn)[k] = full
+        z = self._get(L.OUT_Z, dtype=np.float32, shape=(S, K, R * self.Ns))
+        for s in range(S):
+            res[s].zFullTD = [z[s, k].astype(np.float64) for k in range(K)]
+            res[s].wTildeExt = [None] * K
+        for k in range(self.k0, self.k1):
+            M = self.M[k]
+            e = self._get(L.OUT_WEXT, 0, k, shape=(S, hist, F, M))
+            init = init_complex_filter((F, M), p.referenceSensor, **fi)
+            for s in range(S):
+                full = np.empty((F, nI + 1, M), dtype=np.complex128)
+                full[:] = init[:, None, :]
+                if self.keepHistory:
+                    full[:, :R + 1, :] = np.transpose(e[s], (1, 0, 2))
+                res[s].wTildeExt[k] = full
+        diag = self.diagnostics()
+        for s in range(S):
+            r = res[s]
+            r.startUpdates = self.startRound[s, 0] >= 0
+            r.startRound = self.startRound[s, 0].copy()
+            r.nInternalFilterUps = self.nSolves[s, 0].astype(np.float64)
+            r.diag = diag[s]
+            r.oVADframes = [self.scenes[s].wasn[k].vadPerFrame for k in range(K)]
+            r.neighbors = [list(n.neighborsIdx) for n in self.scenes[s].wasn]
+            r.fs = np.array([n.fs for n in self.scenes[s].wasn])
+            r.SROsppm = np.array([n.sro for n in self.scenes[s].wasn])
+            r.yin = [n.data for n in self.scenes[s].wasn]
+            r.timeInstants = np.stack([n.timeStamps for n in self.scenes[s].wasn], axis=1)
+            r.expAvgBeta = list(self._beta[s].astype(np.float64))
+            r.cleanSpeechSignalsAtNodes = [n.cleanspeech for n in self.scenes[s].wasn]
+            r.nIter = nI
+            r.nRounds = R
+        return res
+
+    def close(self):
+        if getattr(self, 'eng', None):
+            self.lib.danse_engine_destroy(self.eng)
+            self.eng = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class DanseOutputs:
+    """Container with the reference's ``DANSEvariables`` output field names."""
+    pass

@@ -116,49 +116,63 @@ def make_scene(
     vadEnergyDecrease_dB: float = 40.0,
     vadWinLength: float = 0.04,
     SROperNode=None,
+    nodes=None,
 ) -> Scene:
     """Build a random-IR, random-signal fully connected WASN.
+
+    Every node draws from its own RNG stream (``default_rng([seed, 1, k])``),
+    the two sources from ``default_rng([seed, 0])``, so any subset of nodes
+    can be generated on its own (``nodes``; multi-GPU ranks build only the
+    nodes they own).  Nodes outside ``nodes`` get all-zero signals.  The noise
+    gain that sets the SNR at mic 0 of node 0 always uses node 0.
 
     SROs are recorded per node (``SROperNode`` in ppm) but the signals are not
     resampled here (the reference needs ``resampy`` for that, absent offline);
     the time stamps follow ``siggen/utils.py:1579-1622`` (``t = n / fsSRO``).
     """
-    rng = np.random.default_rng(seed)
     K = len(nSensorPerNode)
     T = int(sigDur * fs)
     nIR = int(irDuration * fs)
     sros = np.zeros(K) if SROperNode is None else np.asarray(SROperNode, dtype=float)
+    want = set(range(K)) if nodes is None else set(int(k) for k in nodes)
 
+    src = np.random.default_rng([seed, 0])
     # Desired source: uniform noise with predefined pauses (0.5 s on / 0.5 s off).
-    d = rng.uniform(-1.0, 1.0, T)
+    d = src.uniform(-1.0, 1.0, T)
     t = np.arange(T) / fs
     period = pauseDuration + pauseSpacing
     d[(t % period) >= pauseSpacing] = 0.0
-    n = rng.uniform(-1.0, 1.0, T)
+    n = src.uniform(-1.0, 1.0, T)
 
-    nodes = []
-    for k in range(K):
+    def wet(k):
+        rng = np.random.default_rng([seed, 1, k])
         M = int(nSensorPerNode[k])
-        wetS = np.zeros((T, M))
-        wetN = np.zeros((T, M))
+        wS = np.zeros((T, M))
+        wN = np.zeros((T, M))
         for m in range(M):
-            hd = rng.uniform(-0.5, 0.5, nIR)
-            hn = rng.uniform(-0.5, 0.5, nIR)
-            wetS[:, m] = fftconvolve(d, hd)[:T]
-            wetN[:, m] = fftconvolve(n, hn)[:T]
-        nodes.append([wetS, wetN])
+            wS[:, m] = fftconvolve(d, rng.uniform(-0.5, 0.5, nIR))[:T]
+            wN[:, m] = fftconvolve(n, rng.uniform(-0.5, 0.5, nIR))[:T]
+        return rng, wS, wN
 
+    rng0, wS0, wN0 = wet(0)
     # SNR at mic 0 of node 0 (single noise source).
-    Ps = np.mean(nodes[0][0][:, 0] ** 2)
-    Pn = np.mean(nodes[0][1][:, 0] ** 2)
+    Ps = np.mean(wS0[:, 0] ** 2)
+    Pn = np.mean(wN0[:, 0] ** 2)
     gN = 10 ** (-(snr - 10 * np.log10(Ps / Pn)) / 20)
 
     wasn = []
     for k in range(K):
-        wetS, wetN = nodes[k]
-        wetN = wetN * gN
-        M = wetS.shape[1]
-        clean = wetS + wetN
+        M = int(nSensorPerNode[k])
+        fsSRO = fs * (1 + sros[k] / 1e6)
+        common = dict(index=k, nSensors=M, fs=fsSRO, timeStamps=np.arange(T) / fsSRO,
+                      neighborsIdx=[q for q in range(K) if q != k], sro=float(sros[k]))
+        if k not in want:
+            z = np.zeros((T, M))
+            wasn.append(SceneNode(data=z, cleanspeech=z, cleannoise=z, vad=np.zeros((T, 1)), **common))
+            continue
+        rng, wS, wN = (rng0, wS0, wN0) if k == 0 else wet(k)
+        wN = wN * gN
+        clean = wS + wN
         sig = np.zeros_like(clean)
         selfN = np.zeros_like(clean)
         for m in range(M):
@@ -168,21 +182,9 @@ def make_scene(
             sn *= 10 ** (-(selfnoiseSNR - 10 * np.log10(Pc / Psn)) / 20)
             selfN[:, m] = sn
             sig[:, m] = clean[:, m] + sn
-        vad = _energy_vad(wetS[:, 0], fs, vadWinLength, vadEnergyDecrease_dB)
-        fsSRO = fs * (1 + sros[k] / 1e6)
-        node = SceneNode(
-            index=k,
-            nSensors=M,
-            fs=fsSRO,
-            data=_f32(sig),
-            cleanspeech=_f32(wetS),
-            cleannoise=_f32(wetN + selfN[:, :1]),
-            timeStamps=np.arange(T) / fsSRO,
-            vad=vad[:, None],
-            neighborsIdx=[q for q in range(K) if q != k],
-            sro=float(sros[k]),
-        )
-        wasn.append(node)
+        vad = _energy_vad(wS[:, 0], fs, vadWinLength, vadEnergyDecrease_dB)
+        wasn.append(SceneNode(data=_f32(sig), cleanspeech=_f32(wS), cleannoise=_f32(wN + selfN[:, :1]),
+                              vad=vad[:, None], **common))
     return Scene(wasn=wasn, fs=fs, seed=seed)
 
 

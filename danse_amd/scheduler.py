@@ -205,6 +205,7 @@ class RoundTables:
     upEnd: np.ndarray
     doSolve: np.ndarray
     nRounds: int
+    t: np.ndarray = None        # [R] event instant of each round (float64)
 
 
 def compile_rounds(events, fs, p, nNodes: int) -> RoundTables:
@@ -212,7 +213,7 @@ def compile_rounds(events, fs, p, nNodes: int) -> RoundTables:
     every instant, broadcasts before updates) and emits integer tables.
     Raises NotImplementedError otherwise (asynchronous clocks go through the
     per-event path)."""
-    bcEnd, upEnd, doSolve = [], [], []
+    bcEnd, upEnd, doSolve, ts = [], [], [], []
     for ev in events:
         ks = list(ev.nodes)
         if ev.type != ['bc'] * nNodes + ['up'] * nNodes or ks != list(range(nNodes)) * 2:
@@ -224,5 +225,6 @@ def compile_rounds(events, fs, p, nNodes: int) -> RoundTables:
         bcEnd.append(be)
         upEnd.append(ue)
         doSolve.append([0 if b else 1 for b in ev.bypassUpdate[nNodes:]])
+        ts.append(ev.t)
     return RoundTables(np.array(bcEnd, dtype=np.int64), np.array(upEnd, dtype=np.int64),
-                       np.array(doSolve, dtype=np.int32), len(events))
+                       np.array(doSolve, dtype=np.int32), len(events), np.array(ts, dtype=np.float64))

@@ -1,0 +1,189 @@
+/*
+ * danse_mi355x.h — C-ABI of the MI355X DANSE frame-update engine.
+ *
+ * Drop-in boundary for the reference's swappable unit
+ *   danse_function(wasnObj, p) -> (dv, wasnObj)      tests/sandbox.py:112-129,
+ *                                                      danse_toolbox/d_core.py:26-102
+ * whose per-event operators are
+ *   dv.broadcast(t, fs, k)                            danse_toolbox/d_classes.py:1043-1128
+ *   dv.update_and_estimate(t, fs, k, bypass)          danse_toolbox/d_classes.py:1252-1330
+ * and whose batch counterparts are
+ *   batch_update_danse_covmats / perform_update / batch_estimate
+ *                                                      danse_toolbox/d_batch.py:127-152
+ *
+ * The reference has no FFI (it is pure Python); the binding a maintainer adds
+ * is the ctypes stub in INTEGRATION.md.  Conventions:
+ *   - plain pointers and sizes only; complex numbers are interleaved float32
+ *     {re, im}; device pointers are hipMalloc'd (or torch) GPU memory;
+ *   - the engine owns all of its device state; inputs are borrowed for the
+ *     duration of the call that receives them;
+ *   - every entry point returns 0 on success and a negative code on error;
+ *     danse_last_error() returns the message; no exception crosses the ABI;
+ *   - one engine per device/stream; not internally thread-safe.
+ */
+#ifndef DANSE_MI355X_H
+#define DANSE_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DANSE_MAX_FAMILIES 4   /* DANSE, local, centralised, single-sensor broadcast */
+
+enum danse_family {
+  DANSE_FAM_DANSE = 0,   /* wTilde / d / dhat                 d_classes.py:2290-2320 */
+  DANSE_FAM_LOCAL = 1,   /* wLocal / dLocal                   d_classes.py:2339-2350 */
+  DANSE_FAM_CENTR = 2,   /* wCentr / dCentr                   d_classes.py:2321-2338 */
+  DANSE_FAM_SSBC = 3     /* wSSBC / dSSBC                     d_classes.py:2351-2362 */
+};
+
+/* Per-round, per-(scene, family, node) control byte (host-computed schedule).
+ * bits 0-1: Ryy op   bits 2-3: Rnn op   (0 keep, 1 set to yy^H, 2 exp. average)
+ *           (spatial_covariance_matrix_update + conditional_scm_updating,
+ *            d_classes.py:2048-2267)
+ * bit 4   : solve (filter update: not bypassed and gate passed,
+ *           d_classes.py:1298-1313 / 2290-2362); else w[i+1] = w[i]
+ * bit 5   : refresh the asy external-filter target (timeBtwExternalFiltUpdates,
+ *           d_classes.py:1680-1694)                                         */
+#define DANSE_OP_KEEP 0
+#define DANSE_OP_SET 1
+#define DANSE_OP_AVG 2
+#define DANSE_FLAG_SOLVE 0x10
+#define DANSE_FLAG_EXT_TARGET 0x20
+#define DANSE_FLAG_PREGIVEN 0x40   /* w[i+1], wExt[i+1] pre-loaded (danse_engine_put):
+                                      update_using_pregiven_filters, d_classes.py:1338-1352 */
+
+/* External-filter update mode per node (update_external_filters,
+ * d_classes.py:1627-1694). */
+enum danse_ext_mode {
+  DANSE_EXT_COPY = 0,    /* seq or noExternalFilterRelaxation: wExt[i+1] = w[i+1][:M]     */
+  DANSE_EXT_RELAX = 1,   /* asy/sim: wExt[i+1] = b wExt[i] + (1-b) target; target update */
+  DANSE_EXT_KEEP = 2,    /* noFusionAtSingleSensorNodes and M_k == 1                      */
+  DANSE_EXT_REFONLY = 3  /* onlyBroadcastRefSensorSigs                                    */
+};
+
+typedef struct danse_cfg {
+  /* sizes */
+  int32_t S;            /* independent scenes (same shape) batched in one engine */
+  int32_t K;            /* nodes per scene (fully connected)                      */
+  const int32_t* M;     /* [K] sensors per node                                   */
+  int32_t N;            /* DFT size (DFTsize)                                     */
+  int32_t Ns;           /* hop (N * (1 - WOLAovlp))                               */
+  int32_t T;            /* samples per channel                                    */
+  int32_t R;            /* rounds (DANSE iterations) to run                       */
+  int32_t k0, k1;       /* nodes owned by this engine (multi-GPU sharding), [k0,k1) */
+  /* algorithm */
+  int32_t gevd;         /* performGEVD                                            */
+  int32_t rank;         /* GEVDrank                                               */
+  int32_t ref;          /* referenceSensor                                        */
+  int32_t families;     /* bitmask of enum danse_family                           */
+  float alphaExt;       /* alphaExternalFilters                                   */
+  const int32_t* extMode;   /* [K]                                                */
+  const float* beta;        /* [S*K] SCM forgetting factor per (scene, node)      */
+  const float* betaExt;     /* [S*K] external-filter forgetting factor            */
+  const float* winAnalysis; /* [N] */
+  const float* winSynthesis;/* [N] */
+  /* schedule (host-computed from the reference event matrix, d_base.py:513-1225) */
+  const int32_t* bcEnd;     /* [R*K] broadcast frame end sample  floor(t fs)       */
+  const int32_t* upEnd;     /* [R*K] update frame end  floor(t fs) - (N - Ns)      */
+  const uint8_t* flags;     /* [R*S*DANSE_MAX_FAMILIES*K] control bytes (above)    */
+  /* initial state, host memory (copied at create) */
+  const float* w0;          /* initial filters, per family f, node k (all K nodes,
+                               family-major): [F][D_fk] complex, same for every
+                               scene; NULL = zeros                                 */
+  const float* wExt0;       /* initial external filters, per node: [F][M_k] complex */
+  const float* wExtTarget0; /* initial external-filter targets, same layout        */
+  const float* scmInit;     /* initial SCM slice per family-node: [D][D] complex,
+                               tiled over bins and scenes (Ryy = Rnn); NULL = 0    */
+  int32_t keepHistory;      /* 1: keep w / wExt for every iteration (reference
+                               layout needs it for the SNR replay)                  */
+} danse_cfg;
+
+typedef struct danse_engine danse_engine;
+
+/* Output identifiers for danse_engine_get(). Layouts (device order):
+ *   DANSE_OUT_W      family f, node k: [S][R+1][F][D_fk] complex (2 slots if !keepHistory)
+ *   DANSE_OUT_WEXT   node k: [S][R+1][F][M_k] complex
+ *   DANSE_OUT_D      family f: [S][K][T] float (time-domain estimate)
+ *   DANSE_OUT_DHAT   family f: [S][K][R][F] complex
+ *   DANSE_OUT_Z      [S][K][R*Ns] float (zFullTD)
+ *   DANSE_OUT_DIAG   [S*K*4] int32 diagnostics (bit0: non-PD pivot met in a solve) */
+enum danse_output {
+  DANSE_OUT_W = 0,
+  DANSE_OUT_WEXT = 1,
+  DANSE_OUT_D = 2,
+  DANSE_OUT_DHAT = 3,
+  DANSE_OUT_Z = 4,
+  DANSE_OUT_DIAG = 5
+};
+
+/* Create / destroy.  `device` selects the HIP device. */
+int danse_engine_create(const danse_cfg* cfg, int device, danse_engine** out);
+void danse_engine_destroy(danse_engine* eng);
+const char* danse_last_error(const danse_engine* eng);   /* eng may be NULL */
+
+/* Re-initialise all state (filters, SCMs, z streams, estimates) to the
+ * configured initial values, asynchronously on `stream` (NULL: synchronous). */
+int danse_engine_reset(danse_engine* eng, void* stream);
+
+/* Borrow the input signals: device pointer to [S][sum_k M_k][T] float32,
+ * channel order node-major (node 0 mics, node 1 mics, ...). */
+int danse_engine_set_inputs(danse_engine* eng, const float* yDev);
+
+/* Run rounds [r0, r1) on `stream` (hipStream_t; NULL = default stream).
+ * graph != 0 captures the launch sequence in a hipGraph once and replays it. */
+int danse_engine_run(danse_engine* eng, int32_t r0, int32_t r1, void* stream, int32_t graph);
+
+/* Fine-grained per-round phases (multi-GPU: the caller all-gathers the fused
+ * spectra between them).  bcast(r) also synthesises the estimates of r-1. */
+int danse_engine_bcast(danse_engine* eng, int32_t r, void* stream);
+int danse_engine_update(danse_engine* eng, int32_t r, void* stream);
+int danse_engine_finish(danse_engine* eng, void* stream);   /* synthesis of the last round */
+
+/* Device pointer + byte size of the fused-signal spectra buffer [K][S][F]
+ * complex (node-major, so that a node range is one contiguous block). */
+int danse_engine_zspec(danse_engine* eng, void** ptr, size_t* bytes);
+/* Use a caller-owned buffer (same size and layout) for the fused spectra,
+ * e.g. a torch tensor that an RCCL all-gather fills in place. */
+int danse_engine_set_zspec(danse_engine* eng, void* ptr);
+
+/* Copy an output (enum danse_output) to `dst` (device or host pointer,
+ * hipMemcpyDefault).  `family` selects the estimator family and `node` the
+ * node for the per-node outputs (W, WEXT: all scenes, [S][...] contiguous);
+ * both are ignored where irrelevant.  Synchronises `stream`. */
+int danse_engine_get(danse_engine* eng, int32_t which, int32_t family, int32_t node, void* dst, size_t bytes,
+                     void* stream);
+/* Inverse of danse_engine_get for DANSE_OUT_W / DANSE_OUT_WEXT: load a full
+ * filter history (the SNR replay with pre-given filters). */
+int danse_engine_put(danse_engine* eng, int32_t which, int32_t family, int32_t node, const void* src, size_t bytes,
+                     void* stream);
+/* Byte size of an output. */
+int danse_engine_output_bytes(danse_engine* eng, int32_t which, int32_t family, int32_t node, size_t* bytes);
+
+/* ---- fine-grained operators, for tests and other callers ---- */
+
+/* WOLA analysis (build_ytilde, d_classes.py:1927-1934):
+ * out[c][F] = FFT(x[c][end-N:end] * win)[:F] / sqrt(Ns), zero-padded before 0.
+ * x: [C][T] float (device), ends: [C] int32 (device), out: [C][F] complex. */
+int danse_wola_analysis(const float* x, int32_t C, int32_t T, const int32_t* ends,
+                        const float* win, int32_t N, int32_t Ns, float* out, void* stream);
+
+/* Batched filter update on full SCM pairs (update_w / update_w_gevd,
+ * d_classes.py:3320-3387): Ryy, Rnn: [B][D][D] complex (device), w: [B][D].
+ * gevd != 0 -> rank-`rank` GEVD, else MWF. diag: [B] int32 or NULL. */
+int danse_filter_update(const float* Ryy, const float* Rnn, int32_t B, int32_t D, int32_t gevd,
+                        int32_t rank, int32_t ref, float* w, int32_t* diag, void* stream);
+
+/* Batch-mode SCM contraction (update_covmats_batch, d_classes.py:3272-3304):
+ * Y: [B][Tf][D] complex, vad: [Tf] uint8 -> Ryy, Rnn: [B][D][D] complex
+ * (means over VAD / non-VAD frames). */
+int danse_batch_covmats(const float* Y, int32_t B, int32_t Tf, int32_t D, const uint8_t* vad,
+                        float* Ryy, float* Rnn, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DANSE_MI355X_H */

@@ -398,6 +398,8 @@ class OnlineDANSE:
         events, fs = initialize_events(ts, nodeFs, p, self.neighbors)
         self.events, self.fsEv = events, fs
         nUp = 0
+        import time as _time
+        self.roundTimes = [(int(np.min(self.i)), _time.perf_counter())]
         for ev in events:
             for ii in range(ev.nEvents):
                 k = ev.nodes[ii]
@@ -408,6 +410,7 @@ class OnlineDANSE:
                         continue
                     self.update_and_estimate(ev.t, fs[k], k, ev.bypassUpdate[ii])
                     nUp += 1
+            self.roundTimes.append((int(np.min(self.i)), _time.perf_counter()))
             if self.maxRounds is not None and np.all(self.i >= self.maxRounds):
                 break
         self.nUpdateEvents = nUp

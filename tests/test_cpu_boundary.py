@@ -1,0 +1,90 @@
+"""CPU-side checks of the drop-in boundary: the C-ABI library builds/loads and
+exports every symbol include/danse_mi355x.h declares (no compute calls — no
+GPU here), the ctypes struct matches the header, and the host schedule tables."""
+import re
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def _header_functions():
+    txt = (ROOT / 'include' / 'danse_mi355x.h').read_text()
+    txt = re.sub(r'/\*.*?\*/', '', txt, flags=re.S)
+    return sorted(set(re.findall(r'\b(danse_[a-z_0-9]+)\s*\(', txt)))
+
+
+def test_library_exports_every_header_symbol():
+    from danse_amd import _lib as L
+    from danse_amd import build as B
+    B.build(verbose=False)
+    lib = L.load_library()
+    names = _header_functions()
+    assert len(names) >= 15
+    for n in names:
+        assert hasattr(lib, n), n
+        assert n in L.SIGNATURES, f'{n} missing from the ctypes signatures'
+
+
+def test_cfg_struct_matches_header_fields():
+    from danse_amd import _lib as L
+    txt = (ROOT / 'include' / 'danse_mi355x.h').read_text()
+    body = txt[txt.index('typedef struct danse_cfg {') + len('typedef struct danse_cfg {'):txt.index('} danse_cfg;')]
+    body = re.sub(r'/\*.*?\*/', '', body, flags=re.S)
+    fields = []
+    for decl in body.split(';'):
+        decl = decl.strip()
+        if not decl or decl.startswith('typedef'):
+            continue
+        fields += [x.strip().lstrip('*') for x in re.sub(r'^(const\s+)?\w+\**\s+', '', decl).split(',')]
+    assert [f for f, _ in L.DanseCfg._fields_] == fields
+
+
+def test_product_has_no_oracle_dependency():
+    """The product package must never import the oracle (test infrastructure)."""
+    for p in (ROOT / 'danse_amd').rglob('*.py'):
+        src = p.read_text()
+        assert 'import oracle' not in src and 'from oracle' not in src, p
+
+
+def test_round_tables_sync_schedule():
+    from danse_amd.scene import make_scene
+    from danse_amd.scheduler import initialize_events, compile_rounds
+    from _util import make_case_params
+    case = dict(M=[2, 2, 2], danse=dict(simType='online', nodeUpdating='seq'))
+    dp, wp = make_case_params(case)
+    sc = make_scene([2, 2, 2], sigDur=2.0, seed=0)
+    ev, fs = initialize_events([n.timeStamps for n in sc.wasn], [n.fs for n in sc.wasn], dp,
+                               [n.neighborsIdx for n in sc.wasn])
+    rt = compile_rounds(ev, fs, dp, 3)
+    T = 32000
+    assert rt.nRounds == (T - 1) // 512 - 2
+    j = np.arange(2, 2 + rt.nRounds)
+    assert np.array_equal(rt.bcEnd[:, 0], j * 512)
+    assert np.array_equal(rt.upEnd[:, 0], j * 512 - 512)
+    # seq: exactly one updating node per round, round robin
+    assert np.array_equal(rt.doSolve.sum(axis=1), np.ones(rt.nRounds))
+    assert np.array_equal(np.argmax(rt.doSolve, axis=1), np.arange(rt.nRounds) % 3)
+
+
+def test_compile_rounds_rejects_sro_schedule():
+    from danse_amd.scene import make_scene
+    from danse_amd.scheduler import initialize_events, compile_rounds
+    from _util import make_case_params
+    case = dict(M=[1, 1, 1], danse=dict(simType='online', nodeUpdating='asy'))
+    dp, wp = make_case_params(case, SROperNode=[0, 100, 200])
+    sc = make_scene([1, 1, 1], sigDur=2.0, seed=0, SROperNode=[0, 100, 200])
+    ev, fs = initialize_events([n.timeStamps for n in sc.wasn], [n.fs for n in sc.wasn], dp,
+                               [n.neighborsIdx for n in sc.wasn])
+    with pytest.raises(NotImplementedError):
+        compile_rounds(ev, fs, dp, 3)
+
+
+def test_yaml_config_loads():
+    from danse_amd.params import TestParameters
+    p = TestParameters().load_from_yaml(str(ROOT / 'config_files' / 'sandbox_config_offline.yaml'))
+    assert p.is_fully_connected_wasn()
+    assert p.danseParams.Ns == 512 and p.danseParams.performGEVD
+    assert list(p.wasnParams.nSensorPerNode) == [1, 1]
