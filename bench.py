@@ -141,24 +141,16 @@ def main():
     R, F = eng.R, eng.F
     stream = torch.cuda.current_stream()
 
-    zbuf = None
+    runner = None
     if shard == 'nodes' and world > 1:
-        zptr, znb = eng.zspec()
-        # all-gather in place on the engine's node-major [K][S][F] complex buffer
-        zbuf = torch.empty(znb // 4, dtype=torch.float32, device=f'cuda:{local}')
-        L.check(eng.lib.danse_engine_set_zspec(eng.eng, ctypes_void(zbuf.data_ptr())), eng.eng)
+        from danse_amd.dist import ShardedRun, ShardedEngine
+        runner = ShardedRun(ShardedEngine(eng))      # per-round in-place RCCL all-gather of fused spectra
 
     def one_pass():
-        L.check(eng.lib.danse_engine_reset(eng.eng, eng.stream_ptr()), eng.eng)
-        if shard == 'nodes' and world > 1:
-            chunk = zbuf.numel() // world
-            mine = zbuf[rank * chunk:(rank + 1) * chunk]
-            for r in range(R):
-                eng.bcast(r)
-                dist.all_gather_into_tensor(zbuf, mine)
-                eng.update(r)
-            eng.finish()
+        if runner is not None:
+            runner.run(reset=True)
         else:
+            L.check(eng.lib.danse_engine_reset(eng.eng, eng.stream_ptr()), eng.eng)
             eng.run(graph=not args.no_graph)
 
     for _ in range(args.warmup):
@@ -187,9 +179,8 @@ def main():
     evs = []
     for r in range(R):
         eng.bcast(r)
-        if zbuf is not None:
-            chunk = zbuf.numel() // world
-            dist.all_gather_into_tensor(zbuf, zbuf[rank * chunk:(rank + 1) * chunk])
+        if runner is not None:
+            runner.exchange()
         a = torch.cuda.Event(enable_timing=True)
         b = torch.cuda.Event(enable_timing=True)
         a.record(stream)

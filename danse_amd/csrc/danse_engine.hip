@@ -431,7 +431,10 @@ static void launch_update_cls(const UpdateArgs& a, int nFN, hipStream_t st) {
   constexpr int NB = 64 / G;
   const int nBB = (a.F + NB - 1) / NB;
   const unsigned grid = (unsigned)(a.S * nFN * nBB);
-  hipLaunchKernelGGL((update_kernel<G, DM>), dim3(grid), dim3(64), 0, st, a);
+  if (!a.gevd || a.rank == 1)
+    hipLaunchKernelGGL((update_kernel<G, DM, 1>), dim3(grid), dim3(64), 0, st, a);
+  else
+    hipLaunchKernelGGL((update_kernel<G, DM, kRMax>), dim3(grid), dim3(64), 0, st, a);
 }
 
 static void launch_update(danse_engine* e, int r, hipStream_t st) {
@@ -675,7 +678,7 @@ __global__ void __launch_bounds__(64) filter_update_kernel(const cf* Ryy, const 
   });
   bool ok = true;
   cf wv;
-  if (gevd) wv = gevd_filter<G, DMAX>(A, Bm, lds[gi], li, D, rank, ref, ok);
+  if (gevd) wv = gevd_filter<G, DMAX, kRMax>(A, Bm, lds[gi], li, D, rank, ref, ok);
   else wv = mwf_filter<G, DMAX>(A, Bm, li, D, ref, ok);
   if (act && valid) w[(long long)b * D + li] = wv;
   if (diag && li == 0 && valid) diag[b] = ok ? 0 : 1;

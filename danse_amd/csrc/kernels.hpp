@@ -231,7 +231,7 @@ struct UpdateArgs {
   int* diag;               // [S*K*kMaxFam]
 };
 
-template <int G, int DMAX>
+template <int G, int DMAX, int RMAX>
 __global__ void __launch_bounds__(64) update_kernel(const UpdateArgs a) {
   static_assert(DMAX <= G, "a lane group must hold every row");
   constexpr int NB = 64 / G;
@@ -327,7 +327,7 @@ __global__ void __launch_bounds__(64) update_kernel(const UpdateArgs a) {
     w = act ? wNext[act ? li : 0] : cf{0.0f, 0.0f};
   } else if (solve) {
     bool ok = true;
-    if (a.gevd) w = gevd_filter<G, DMAX>(A, B, lds[gi], li, D, a.rank, d.ref, ok);
+    if (a.gevd) w = gevd_filter<G, DMAX, RMAX>(A, B, lds[gi], li, D, a.rank, d.ref, ok);
     else w = mwf_filter<G, DMAX>(A, B, li, D, d.ref, ok);
     if (!ok && li == 0 && valid) atomicOr(&a.diag[(s * a.K + d.k) * kMaxFam + d.fam], 1);
   } else {

@@ -47,13 +47,8 @@ constexpr int kRMax = 4;   // largest supported GEVD rank
 template <int DMAX>
 struct SolverLDS {
   cf U[DMAX][DMAX + 1];     // transpose tile, then Householder vectors U[j][i]
-  float ta[DMAX];           // tridiagonal diagonal
-  float te2[DMAX];          // squared |sub-diagonal|
-  cf tb[DMAX];              // complex sub-diagonal T[i+1][i]
-  float x[kRMax][DMAX];     // eigenvectors of the real tridiagonal
-  float d[DMAX], dl[DMAX], du[DMAX], rhs[DMAX];   // inverse-iteration scratch
-  cf v[kRMax][DMAX];        // complex eigenvectors of T (after the phase fix)
-  float lam[kRMax];
+  float x[kRMax][DMAX];     // real tridiagonal eigenvectors (Gram-Schmidt of rank > 1)
+  cf tb[DMAX];              // complex sub-diagonal T[i+1][i] (phase fix)
 };
 
 // ---- Cholesky, rows in registers: on exit B[c] (c <= li) = L[li][c], 0 above.
@@ -155,7 +150,7 @@ DANSE_DEV void herm_transpose(cf (&X)[DMAX], cf (*U)[DMAX + 1], int li) {
 // Householder reduction of the Hermitian C (rows in A) to tridiagonal form.
 // Stores u_j in S.U[j][i], diag in S.ta, sub-diagonal in S.tb, |sub|^2 in S.te2.
 template <int G, int DMAX>
-DANSE_DEV void tridiag_rows(cf (&A)[DMAX], SolverLDS<DMAX>& S, int li, int D) {
+DANSE_DEV void tridiag_rows(cf (&A)[DMAX], SolverLDS<DMAX>& S, int li, int D, float& a, cf& b) {
   const bool act = li < D;
   sfor<0, (DMAX >= 2 ? DMAX - 2 : 0)>([&](auto jc) {
     constexpr int j = decltype(jc)::value;
@@ -195,9 +190,9 @@ DANSE_DEV void tridiag_rows(cf (&A)[DMAX], SolverLDS<DMAX>& S, int li, int D) {
       if (li < DMAX) S.U[j][li] = u;
     }
   });
-  // diagonal and sub-diagonal
-  float a = 0.0f;
-  cf b = cf{0.0f, 0.0f};
+  // diagonal and sub-diagonal element of my row
+  a = 0.0f;
+  b = cf{0.0f, 0.0f};
   sfor<0, DMAX>([&](auto cc) {
     constexpr int c = decltype(cc)::value;
     if (li == c) a = A[c].re;
@@ -205,154 +200,185 @@ DANSE_DEV void tridiag_rows(cf (&A)[DMAX], SolverLDS<DMAX>& S, int li, int D) {
       if (li == c) b = A[c - 1];
     }
   });
-  if (li < DMAX && li < D) S.ta[li] = a;
-  if (li >= 1 && li < D && li < DMAX) {
-    S.tb[li - 1] = b;
-    S.te2[li - 1] = abs2(b);
-  }
+  __syncthreads();   // Householder vectors in S.U visible to the back-transform
+}
+
+// The real tridiagonal, replicated in the registers of every lane of the
+// group; the complex sub-diagonal (needed once, for the phase fix) goes to LDS.
+template <int DMAX>
+struct Tri {
+  float a[DMAX];    // diagonal
+  float e2[DMAX];   // |sub-diagonal|^2, e2[i] = |T[i+1][i]|^2
+};
+
+template <int G, int DMAX>
+DANSE_DEV void gather_tri(Tri<DMAX>& T, float a, cf b, int D, cf* tb, int li) {
+  const float e2 = abs2(b);
+  sfor<0, DMAX>([&](auto cc) {
+    constexpr int c = decltype(cc)::value;
+    T.a[c] = (c < D) ? gbcast<G, c>(a) : 0.0f;
+    if constexpr (c + 1 < DMAX) {
+      const float ec = gbcast<G, c + 1>(e2);
+      T.e2[c] = (c + 1 < D) ? ec : 0.0f;
+    } else {
+      T.e2[c] = 0.0f;
+    }
+  });
+  if (li >= 1 && li < DMAX) tb[li - 1] = (li < D) ? b : cf{0.0f, 0.0f};
+  if (li == DMAX - 1 || li == D - 1) tb[DMAX - 1] = cf{0.0f, 0.0f};
   __syncthreads();
 }
 
-// Number of eigenvalues of the real symmetric tridiagonal (ta, sqrt(te2)) below x.
+// Number of eigenvalues of the real symmetric tridiagonal (a, sqrt(e2)) below x.
 template <int DMAX>
-DANSE_DEV int sturm_count(const SolverLDS<DMAX>& S, int D, float x, float pivmin) {
+DANSE_DEV int sturm_reg(const Tri<DMAX>& T, int D, float x, float pivmin) {
   int cnt = 0;
-  float q = S.ta[0] - x;
-  if (fabsf(q) <= pivmin) q = -pivmin;
-  cnt += (q < 0.0f);
-  for (int i = 1; i < D; ++i) {
-    q = (S.ta[i] - x) - S.te2[i - 1] / q;
-    if (fabsf(q) <= pivmin) q = -pivmin;
-    cnt += (q < 0.0f);
-  }
+  float q = 1.0f;
+  sfor<0, DMAX>([&](auto ic) {
+    constexpr int i = decltype(ic)::value;
+    if (i < D) {
+      float qn;
+      if constexpr (i == 0) qn = T.a[0] - x;
+      else qn = (T.a[i] - x) - __fdividef(T.e2[i - 1], q);
+      if (fabsf(qn) <= pivmin) qn = -pivmin;
+      q = qn;
+      cnt += (q < 0.0f) ? 1 : 0;
+    }
+  });
   return cnt;
 }
 
-// Top-R eigenvalues (descending) by multisection; stored in S.lam.
-template <int G, int DMAX>
-DANSE_DEV void top_eigvals(SolverLDS<DMAX>& S, int li, int D, int R) {
-  const bool act = li < D;
-  float lo_i = 0.0f, hi_i = 0.0f, e2max = 0.0f;
-  if (act) {
-    const float em = (li >= 1) ? sqrtf(S.te2[li - 1]) : 0.0f;
-    const float ep = (li + 1 < D) ? sqrtf(S.te2[li]) : 0.0f;
-    lo_i = S.ta[li] - em - ep;
-    hi_i = S.ta[li] + em + ep;
-    e2max = (li + 1 < D) ? S.te2[li] : 0.0f;
-  }
-  float lo = gmin<G>(act ? lo_i : 3.0e38f);
-  float hi = gmax<G>(act ? hi_i : -3.0e38f);
+// Top-R eigenvalues (descending) by multisection: every lane of the group
+// evaluates one Sturm count per pass, the bracket shrinks by (G + 1).
+template <int G, int DMAX, int RMAX>
+DANSE_DEV void top_eigvals(const Tri<DMAX>& T, int li, int D, int R, float (&lam)[kRMax], float& tnorm) {
+  float lo = 3.0e38f, hi = -3.0e38f, e2max = 0.0f;
+  tnorm = 0.0f;
+  sfor<0, DMAX>([&](auto ic) {
+    constexpr int i = decltype(ic)::value;
+    if (i < D) {
+      float em = 0.0f;
+      if constexpr (i >= 1) em = sqrtf(T.e2[i - 1]);
+      const float ep = (i + 1 < D) ? sqrtf(T.e2[i]) : 0.0f;
+      lo = fminf(lo, T.a[i] - em - ep);
+      hi = fmaxf(hi, T.a[i] + em + ep);
+      if (i + 1 < D) e2max = fmaxf(e2max, T.e2[i]);
+      tnorm = fmaxf(tnorm, fabsf(T.a[i]) + em + ep);
+    }
+  });
   const float scale = fmaxf(fabsf(lo), fabsf(hi));
-  const float pivmin = 1.0e-30f * fmaxf(1.0f, gmax<G>(e2max));
+  const float pivmin = 1.0e-30f * fmaxf(1.0f, e2max);
   lo -= 2.0f * 1.2e-7f * scale + pivmin;
   hi += 2.0f * 1.2e-7f * scale + pivmin;
-  // iterations: each shrinks the bracket by (G + 1)
   constexpr int NIT = (G >= 64) ? 5 : (G >= 16 ? 7 : 12);
-  for (int r = 0; r < R; ++r) {
-    float a = lo, b = hi;
-    const int target = D - r;   // count(x) >= target  <=>  x > lambda_r
-    for (int it = 0; it < NIT; ++it) {
-      const float x = a + (b - a) * (float)(li + 1) / (float)(G + 1);
-      const int cnt = sturm_count<DMAX>(S, D, x, pivmin);
-      const uint64_t m = gballot<G>(cnt >= target);
-      if (m == 0ull) {
-        a = a + (b - a) * (float)G / (float)(G + 1);
-      } else {
-        const int first = __builtin_ctzll(m);
-        const float xf = a + (b - a) * (float)(first + 1) / (float)(G + 1);
-        const float xp = a + (b - a) * (float)first / (float)(G + 1);
-        b = xf;
-        a = xp;
+  sfor<0, RMAX>([&](auto rc) {
+    constexpr int r = decltype(rc)::value;
+    if (r < R) {
+      float a = lo, b = hi;
+      const int target = D - r;   // count(x) >= target  <=>  x > lambda_r
+      for (int it = 0; it < NIT; ++it) {
+        const float step = (b - a) / (float)(G + 1);
+        const float x = a + step * (float)(li + 1);
+        const int cnt = sturm_reg<DMAX>(T, D, x, pivmin);
+        const uint64_t m = gballot<G>(cnt >= target);
+        if (m == 0ull) {
+          a = a + step * (float)G;
+        } else {
+          const int first = __builtin_ctzll(m);
+          const float na = a + step * (float)first;
+          b = a + step * (float)(first + 1);
+          a = na;
+        }
       }
+      lam[r] = 0.5f * (a + b);
+      hi = b;
     }
-    if (li == 0) S.lam[r] = 0.5f * (a + b);
-    hi = b;   // next eigenvalue is not above this one
-  }
-  __syncthreads();
+  });
 }
 
-// Eigenvectors of the real tridiagonal for S.lam[0..R), by inverse iteration
-// with partial pivoting (LAPACK dgtsv elimination) on lane 0 of the group,
-// Gram-Schmidt against earlier vectors; then the complex phase fix
-// v_i = phi_i x_i (phi_{i+1} = phi_i * tb_i / |tb_i|).  Results in S.v[r].
+// Eigenvector of the real tridiagonal for eigenvalue lam by inverse
+// iteration (LAPACK dgtsv elimination with partial pivoting, written with
+// selects so that the groups of a wave never diverge), Gram-Schmidt against
+// the R previous vectors in LDS.  All lanes of a group compute the same x.
 template <int DMAX>
-DANSE_DEV void tri_eigvecs_lane(SolverLDS<DMAX>& S, int D, int R, float tnorm) {
-  const float pert = 1.2e-7f * fmaxf(tnorm, 1e-30f);
-  for (int r = 0; r < R; ++r) {
-    const float lam = S.lam[r];
-    for (int i = 0; i < D; ++i) S.x[r][i] = 1.0f + 0.1f * (float)((i * 7919 + r * 104729) % 13) / 13.0f;
-    for (int it = 0; it < 3; ++it) {
-      for (int i = 0; i < D; ++i) {
-        S.d[i] = S.ta[i] - lam;
-        S.rhs[i] = S.x[r][i];
-        if (i + 1 < D) {
-          const float e = sqrtf(S.te2[i]);
-          S.dl[i] = e;
-          S.du[i] = e;
-        }
-      }
-      // elimination (dgtsv), rows i, i+1
-      for (int i = 0; i + 1 < D; ++i) {
-        if (fabsf(S.d[i]) >= fabsf(S.dl[i])) {
-          if (S.d[i] == 0.0f) S.d[i] = pert;
-          const float fact = S.dl[i] / S.d[i];
-          S.d[i + 1] -= fact * S.du[i];
-          S.rhs[i + 1] -= fact * S.rhs[i];
-          S.dl[i] = 0.0f;
-        } else {
-          const float fact = S.d[i] / S.dl[i];
-          S.d[i] = S.dl[i];
-          const float temp = S.d[i + 1];
-          S.d[i + 1] = S.du[i] - fact * temp;
-          if (i + 2 < D) {
-            S.dl[i] = S.du[i + 1];
-            S.du[i + 1] = -fact * S.dl[i];
-          } else {
-            S.dl[i] = 0.0f;
-          }
-          S.du[i] = temp;
-          const float tb = S.rhs[i];
-          S.rhs[i] = S.rhs[i + 1];
-          S.rhs[i + 1] = tb - fact * S.rhs[i + 1];
-        }
-      }
-      if (S.d[D - 1] == 0.0f) S.d[D - 1] = pert;
-      // back solve (upper, two super-diagonals du, dl)
-      S.rhs[D - 1] = S.rhs[D - 1] / S.d[D - 1];
-      if (D > 1) S.rhs[D - 2] = (S.rhs[D - 2] - S.du[D - 2] * S.rhs[D - 1]) / S.d[D - 2];
-      for (int i = D - 3; i >= 0; --i)
-        S.rhs[i] = (S.rhs[i] - S.du[i] * S.rhs[i + 1] - S.dl[i] * S.rhs[i + 2]) / S.d[i];
-      // Gram-Schmidt against earlier vectors, normalise
-      for (int q = 0; q < r; ++q) {
-        float dot = 0.0f;
-        for (int i = 0; i < D; ++i) dot += S.x[q][i] * S.rhs[i];
-        for (int i = 0; i < D; ++i) S.rhs[i] -= dot * S.x[q][i];
-      }
-      float nrm = 0.0f, mx = 0.0f;
-      for (int i = 0; i < D; ++i) mx = fmaxf(mx, fabsf(S.rhs[i]));
-      mx = (mx > 0.0f) ? mx : 1.0f;
-      for (int i = 0; i < D; ++i) {
-        const float t = S.rhs[i] / mx;
-        nrm += t * t;
-      }
-      const float inv = 1.0f / (mx * sqrtf(nrm));
-      for (int i = 0; i < D; ++i) S.x[r][i] = S.rhs[i] * inv;
-    }
-    // phase fix
-    cf phi = cf{1.0f, 0.0f};
-    for (int i = 0; i < D; ++i) {
-      S.v[r][i] = S.x[r][i] * phi;
+DANSE_DEV void tri_eigvec(const Tri<DMAX>& T, int D, float lam, float pert, int r, const float (*prev)[DMAX],
+                          float (&x)[DMAX]) {
+  sfor<0, DMAX>([&](auto ic) {
+    constexpr int i = decltype(ic)::value;
+    x[i] = (i < D) ? 1.0f + 0.1f * (float)((i * 7919 + r * 104729) % 13) / 13.0f : 0.0f;
+  });
+  for (int it = 0; it < 3; ++it) {
+    float d[DMAX], dl[DMAX], du[DMAX], rhs[DMAX];
+    sfor<0, DMAX>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      d[i] = T.a[i] - lam;
+      const float e = sqrtf(T.e2[i]);
+      dl[i] = e;
+      du[i] = e;
+      rhs[i] = x[i];
+    });
+    sfor<0, DMAX - 1>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
       if (i + 1 < D) {
-        const cf b = S.tb[i];
-        const float ab = sqrtf(abs2(b));
-        if (ab > 0.0f) phi = phi * cf{b.re / ab, b.im / ab};
+        const bool swap = fabsf(d[i]) < fabsf(dl[i]);
+        const float di = (d[i] == 0.0f) ? pert : d[i];
+        const float f1 = dl[i] / di;           // no interchange
+        const float f2 = d[i] / dl[i];         // interchange rows i, i+1
+        const float d1 = d[i + 1];
+        const float duI = du[i];
+        float du1 = 0.0f;
+        if constexpr (i + 1 < DMAX) du1 = du[i + 1];
+        const bool has2 = (i + 2 < D);
+        d[i] = swap ? dl[i] : di;
+        d[i + 1] = swap ? (duI - f2 * d1) : (d1 - f1 * duI);
+        dl[i] = (swap && has2) ? du1 : 0.0f;   // second super-diagonal
+        if constexpr (i + 1 < DMAX) {
+          if (has2) du[i + 1] = swap ? -f2 * du1 : du1;
+        }
+        du[i] = swap ? d1 : duI;
+        const float ri = rhs[i], ri1 = rhs[i + 1];
+        rhs[i] = swap ? ri1 : ri;
+        rhs[i + 1] = swap ? (ri - f2 * ri1) : (ri1 - f1 * ri);
       }
+    });
+    // back solve
+    sfor_down<DMAX, 0>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      if (i < D) {
+        float acc = rhs[i];
+        if constexpr (i + 1 < DMAX) {
+          if (i + 1 < D) acc -= du[i] * rhs[i + 1];
+        }
+        if constexpr (i + 2 < DMAX) {
+          if (i + 2 < D) acc -= dl[i] * rhs[i + 2];
+        }
+        const float di = (d[i] == 0.0f) ? pert : d[i];
+        rhs[i] = acc / di;
+      }
+    });
+    for (int q = 0; q < r; ++q) {
+      float dot = 0.0f;
+      sfor<0, DMAX>([&](auto ic) { constexpr int i = decltype(ic)::value; dot += prev[q][i] * rhs[i]; });
+      sfor<0, DMAX>([&](auto ic) { constexpr int i = decltype(ic)::value; rhs[i] -= dot * prev[q][i]; });
     }
+    float mx = 0.0f;
+    sfor<0, DMAX>([&](auto ic) { mx = fmaxf(mx, fabsf(rhs[decltype(ic)::value])); });
+    mx = (mx > 0.0f) ? mx : 1.0f;
+    const float imx = 1.0f / mx;
+    float nrm = 0.0f;
+    sfor<0, DMAX>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      rhs[i] *= imx;
+      nrm += rhs[i] * rhs[i];
+    });
+    const float inv = 1.0f / sqrtf(nrm);
+    sfor<0, DMAX>([&](auto ic) { constexpr int i = decltype(ic)::value; x[i] = (i < D) ? rhs[i] * inv : 0.0f; });
   }
 }
 
 // Full GEVD filter: A = Ryy rows, B = Rnn rows (both destroyed).  Returns w_li.
-template <int G, int DMAX>
+// RMAX bounds the (runtime) rank R at compile time.
+template <int G, int DMAX, int RMAX>
 DANSE_DEV cf gevd_filter(cf (&A)[DMAX], cf (&B)[DMAX], SolverLDS<DMAX>& S, int li, int D, int R, int ref,
                          bool& ok) {
   const bool act = li < D;
@@ -360,12 +386,15 @@ DANSE_DEV cf gevd_filter(cf (&A)[DMAX], cf (&B)[DMAX], SolverLDS<DMAX>& S, int l
   fwd_rows<G, DMAX>(A, B, li, D);             // A = L^{-1} Ryy
   herm_transpose<G, DMAX>(A, S.U, li);        // A = Ryy L^{-H}
   fwd_rows<G, DMAX>(A, B, li, D);             // A = L^{-1} Ryy L^{-H} = C
-  tridiag_rows<G, DMAX>(A, S, li, D);
-  top_eigvals<G, DMAX>(S, li, D, R);
-  float tn = act ? (fabsf(S.ta[li]) + ((li + 1 < D) ? sqrtf(S.te2[li]) : 0.0f)) : 0.0f;
-  tn = gmax<G>(tn);
-  if (li == 0) tri_eigvecs_lane<DMAX>(S, D, R, tn);
-  __syncthreads();
+  float ta;
+  cf tb;
+  tridiag_rows<G, DMAX>(A, S, li, D, ta, tb);
+  Tri<DMAX> T;
+  gather_tri<G, DMAX>(T, ta, tb, D, S.tb, li);
+  float lam[kRMax];
+  float tnorm;
+  top_eigvals<G, DMAX, RMAX>(T, li, D, R, lam, tnorm);
+  const float pert = 1.2e-7f * fmaxf(tnorm, 1e-30f);
   // g = L^H e_ref : g_i = conj(L[ref][i])
   cf g = cf{0.0f, 0.0f};
   sfor<0, DMAX>([&](auto cc) {
@@ -374,8 +403,32 @@ DANSE_DEV cf gevd_filter(cf (&A)[DMAX], cf (&B)[DMAX], SolverLDS<DMAX>& S, int l
     if (li == c) g = conjg(v);
   });
   cf w = cf{0.0f, 0.0f};
-  for (int r = 0; r < R; ++r) {
-    cf v = (act && li < DMAX) ? S.v[r][li] : cf{0.0f, 0.0f};
+  sfor<0, RMAX>([&](auto rc) {
+    constexpr int r = decltype(rc)::value;
+    if (r >= R) return;
+    float x[DMAX];
+    tri_eigvec<DMAX>(T, D, lam[r], pert, r, S.x, x);
+    // phase fix v_i = phi_i x_i (phi_{i+1} = phi_i * b_i / |b_i|); lane li keeps v_li
+    cf v = cf{0.0f, 0.0f};
+    cf phi = cf{1.0f, 0.0f};
+    sfor<0, DMAX>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      if (li == i) v = x[i] * phi;
+      const cf b = (i + 1 < D) ? S.tb[i] : cf{0.0f, 0.0f};
+      const float ab2 = abs2(b);
+      if (ab2 > 0.0f) {
+        const float iab = rsqrtf(ab2);
+        phi = phi * cf{b.re * iab, b.im * iab};
+      }
+    });
+    if (r + 1 < R) {
+      // keep x for Gram-Schmidt of the next eigenvectors
+      float xi = 0.0f;
+      sfor<0, DMAX>([&](auto ic) { constexpr int i = decltype(ic)::value; if (li == i) xi = x[i]; });
+      if (li < DMAX) S.x[r][li] = xi;
+      __syncthreads();
+    }
+    if (!act) v = cf{0.0f, 0.0f};
     // back-transform with the Householder vectors, last first
     for (int j = D - 3; j >= 0; --j) {
       const cf u = (act && li < DMAX) ? S.U[j][li] : cf{0.0f, 0.0f};
@@ -384,9 +437,9 @@ DANSE_DEV cf gevd_filter(cf (&A)[DMAX], cf (&B)[DMAX], SolverLDS<DMAX>& S, int l
     }
     const cf sr = gsum<G>(act ? cmul(v, g) : cf{0.0f, 0.0f});
     cf u = bwd_vec_h<G, DMAX>(v, B, li, D);
-    const float coef = 1.0f - 1.0f / S.lam[r];
+    const float coef = 1.0f - 1.0f / lam[r];
     w = w + coef * (u * sr);
-  }
+  });
   return act ? w : cf{0.0f, 0.0f};
 }
 

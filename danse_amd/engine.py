@@ -317,6 +317,7 @@ class DanseEngine:
                     src = pg[s][name[f]][k] if isinstance(pg, (list, tuple)) else getattr(pg, name[f])[k]
                     arr[s] = np.transpose(src[:, :R + 1, :], (1, 0, 2))
                 self._put(L.OUT_W, f, k, arr)
+        for k in range(self.k0, self.k1):
             M = self.M[k]
             arr = np.empty((self.S, R + 1, F, M), dtype=np.complex64)
             for s in range(self.S):

@@ -1,0 +1,115 @@
+"""TEST INFRASTRUCTURE: a float64 CPU stand-in for the device engine with the
+same round/phase interface (bcast(r) -> fused spectra of the owned nodes in a
+node-major [K][S][F] buffer -> update(r) consuming every node's spectrum), so
+that ``danse_amd.dist.ShardedRun`` can be exercised with the gloo backend on
+CPU.  Arithmetic comes from the oracle (oracle/danse_ref_cpu.py): same
+frames, same compression/OLA, same SCM recursion and filter updates; DANSE
+family only, round-synchronous schedule (no SROs)."""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from danse_amd.scheduler import initialize_events, compile_rounds
+from oracle import danse_ref_cpu as O
+
+
+class RoundEngine:
+    def __init__(self, scenes, p, nodeRange=None):
+        self.p = p
+        self.scenes = scenes
+        self.S = len(scenes)
+        sc0 = scenes[0]
+        self.K = K = sc0.nNodes
+        self.M = [n.nSensors for n in sc0.wasn]
+        self.N, self.Ns = p.DFTsize, p.Ns
+        self.F = self.N // 2 + 1
+        self.T = sc0.wasn[0].data.shape[0]
+        self.k0, self.k1 = nodeRange if nodeRange else (0, K)
+        ev, fs = initialize_events([n.timeStamps for n in sc0.wasn], [n.fs for n in sc0.wasn], p,
+                                   [n.neighborsIdx for n in sc0.wasn])
+        self.rt = compile_rounds(ev, fs, p, K)
+        self.R = self.rt.nRounds
+        self.torch_device = 'cpu'
+        self.zbuf = None
+        self.h, self.f = p.winWOLAanalysis, p.winWOLAsynthesis
+
+    def zspec_numel(self):
+        return self.K * self.S * self.F * 2
+
+    def set_zspec(self, t):
+        self.zbuf = t
+
+    def _z(self):
+        return self.zbuf.numpy().view(np.complex64).reshape(self.K, self.S, self.F)
+
+    def reset(self):
+        p, K, F = self.p, self.K, self.F
+        self.st = []
+        for s, sc in enumerate(self.scenes):
+            nodes = {}
+            for k in range(self.k0, self.k1):
+                D = self.M[k] + K - 1
+                nodes[k] = dict(
+                    Ryy=np.zeros((F, D, D), complex), Rnn=np.zeros((F, D, D), complex),
+                    w=O.init_complex_filter((F, self.R + 1, D), p.referenceSensor, p.filterInitType,
+                                            p.filterInitFixedValue),
+                    wExt=O.init_complex_filter((F, self.R + 1, self.M[k]), p.referenceSensor, p.filterInitType,
+                                               p.filterInitFixedValue),
+                    tgt=O.init_complex_filter((F, self.M[k]), p.referenceSensor, p.filterInitType,
+                                              p.filterInitFixedValue),
+                    zLocal=np.array([]), zs=np.zeros(self.R * self.Ns), d=np.zeros(self.T),
+                    nY=0, nN=0, start=False,
+                    beta=O.beta_from_t50p(p.t_expAvg50p, sc.wasn[k].fs, self.Ns),
+                    betaE=(p.forcedBetaExternalFilters if p.forcedBetaExternalFilters is not None
+                           else O.beta_from_t50p(p.t_expAvg50pExternalFilters, sc.wasn[k].fs, self.Ns)))
+            self.st.append(nodes)
+
+    def bcast(self, r):
+        zv = self._z()
+        N, Ns = self.N, self.Ns
+        for s, sc in enumerate(self.scenes):
+            for k in range(self.k0, self.k1):
+                n = self.st[s][k]
+                fr, _, _ = O.local_chunk(sc.wasn[k].data, int(self.rt.bcEnd[r, k]), N)
+                _, n['zLocal'] = O.compression_whole_chunk(fr, n['wExt'][:, r, :], self.h, self.f, n['zLocal'], Ns)
+                n['zs'][r * Ns:(r + 1) * Ns] = n['zLocal'][:Ns]
+                lo = (r + 1) * Ns - N
+                frame = np.zeros(N)
+                src = n['zs'][max(lo, 0):(r + 1) * Ns]
+                frame[N - len(src):] = src
+                zv[k, s] = (np.fft.fft(frame * self.h, N) / np.sqrt(Ns))[:self.F]
+
+    def update(self, r):
+        zv = self._z()
+        p, K, N, Ns = self.p, self.K, self.N, self.Ns
+        for s, sc in enumerate(self.scenes):
+            for k in range(self.k0, self.k1):
+                n = self.st[s][k]
+                fr, b, e = O.local_chunk(sc.wasn[k].data, int(self.rt.upEnd[r, k]), N)
+                yl = (np.fft.fft(fr * self.h[:, None], N, axis=0) / np.sqrt(Ns))[:self.F]
+                y = np.concatenate([yl] + [zv[q, s][:, None].astype(np.complex128) for q in range(K) if q != k], axis=1)
+                D = y.shape[1]
+                vad = bool(sc.wasn[k].vadPerFrame[r])
+                if vad:
+                    n['nY'] += 1
+                else:
+                    n['nN'] += 1
+                yy = 1 / D * np.einsum('ij,ik->ijk', y, y.conj())
+                if vad:
+                    n['Ryy'] = yy if n['nY'] == 1 else n['beta'] * n['Ryy'] + (1 - n['beta']) * yy
+                else:
+                    n['Rnn'] = yy if n['nN'] == 1 else n['beta'] * n['Rnn'] + (1 - n['beta']) * yy
+                if not n['start'] and n['nY'] > D and n['nN'] > D:
+                    n['start'] = True
+                if n['start'] and self.rt.doSolve[r, k]:
+                    n['w'][:, r + 1, :] = O.update_w_gevd(n['Ryy'], n['Rnn'], p.referenceSensor, p.GEVDrank)
+                else:
+                    n['w'][:, r + 1, :] = n['w'][:, r, :]
+                cur = n['w'][:, r + 1, :self.M[k]]
+                n['wExt'][:, r + 1, :] = n['betaE'] * n['wExt'][:, r, :] + (1 - n['betaE']) * n['tgt']
+                n['tgt'] = cur.copy()
+                O.desired_sig_chunk(n['w'][:, r + 1, :], y, self.f, np.sqrt(Ns), n['d'][b:e])
+
+    def finish(self):
+        pass
