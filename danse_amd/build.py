@@ -1,39 +1,79 @@
 """In-tree build of the HIP extension (gfx950): ``libdanse_mi355x.so``.
 
-Plain ``hipcc -shared -fPIC`` of ``csrc/danse_engine.hip`` (kernels in
-``csrc/*.hpp``); the output sits next to this file so that it travels with the
-repository snapshot to the GPU box.
+``hipcc -c -fPIC`` of ``csrc/danse_engine.hip`` (host engine, C-ABI, bcast /
+operator kernels) and of ``csrc/update_class.hip`` once per filter-size class
+(``-DDANSE_DMAX=N``, N = 2..16, see ``csrc/classes.hpp``), in parallel, then one
+``hipcc -shared`` link.  Objects go to ``danse_amd/_obj/``; the library sits
+next to this file so that it travels with the repository snapshot to the GPU
+box.
 """
 from __future__ import annotations
 
 import os
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 from pathlib import Path
 
 HERE = Path(__file__).resolve().parent
-SRC = HERE / 'csrc' / 'danse_engine.hip'
+CSRC = HERE / 'csrc'
+OBJ = HERE / '_obj'
 OUT = HERE / 'libdanse_mi355x.so'
 INC = HERE.parent / 'include'
+CLASSES = list(range(2, 17))
+FLAGS = ['--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC']
 
 
-def _sources():
-    return [SRC] + sorted((HERE / 'csrc').glob('*.hpp')) + [INC / 'danse_mi355x.h']
+def _units():
+    """(object name, source, extra flags) of every translation unit."""
+    u = [('danse_engine.o', CSRC / 'danse_engine.hip', [])]
+    for n in CLASSES:
+        u.append((f'update_d{n}.o', CSRC / 'update_class.hip', [f'-DDANSE_DMAX={n}']))
+    return u
+
+
+def _headers():
+    return sorted(CSRC.glob('*.hpp')) + [INC / 'danse_mi355x.h']
+
+
+def _stale(obj: Path, src: Path) -> bool:
+    if not obj.exists():
+        return True
+    t = obj.stat().st_mtime
+    return any(p.stat().st_mtime > t for p in [src] + _headers())
 
 
 def up_to_date() -> bool:
     if not OUT.exists():
         return False
     t = OUT.stat().st_mtime
-    return all(s.stat().st_mtime <= t for s in _sources())
+    return all(not _stale(OBJ / o, s) and (OBJ / o).stat().st_mtime <= t for o, s, _ in _units())
 
 
-def build(force: bool = False, verbose: bool = True) -> Path:
+def build(force: bool = False, verbose: bool = True, jobs: int | None = None) -> Path:
     if not force and up_to_date():
         return OUT
     hipcc = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
-    cmd = [hipcc, '--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC', '-shared',
-           f'-I{INC}', str(SRC), '-o', str(OUT) + '.tmp']
+    OBJ.mkdir(exist_ok=True)
+    todo = [(o, s, x) for o, s, x in _units() if force or _stale(OBJ / o, s)]
+
+    def compile_one(item):
+        o, s, x = item
+        cmd = [hipcc, *FLAGS, f'-I{INC}', *x, '-c', str(s), '-o', str(OBJ / o) + '.tmp']
+        if verbose:
+            print(' '.join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f'hipcc failed for {o}:\n{r.stderr}')
+        os.replace(str(OBJ / o) + '.tmp', OBJ / o)
+
+    n = jobs or min(16, os.cpu_count() or 4, max(1, len(todo)))
+    # heaviest classes first so the pool drains evenly
+    todo.sort(key=lambda it: -int(it[0][8:-2]) if it[0].startswith('update_d') else 0)
+    with ThreadPoolExecutor(max_workers=n) as ex:
+        list(ex.map(compile_one, todo))
+    cmd = [hipcc, '--offload-arch=gfx950', '-fPIC', '-shared', *[str(OBJ / o) for o, _, _ in _units()],
+           '-o', str(OUT) + '.tmp']
     if verbose:
         print(' '.join(cmd), flush=True)
     subprocess.run(cmd, check=True)

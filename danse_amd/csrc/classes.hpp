@@ -1,0 +1,47 @@
+// Size classes of the update / filter kernels.  Every filter dimension
+// D in [1, 16] gets its own compile-time DMAX (= D, D = 1 padded to 2) so the
+// unrolled lane-group solver does no padded work; D <= 4 runs 16 bins per
+// wavefront (G = 4 lanes per bin), larger D 4 bins (G = 16).  Each class is a
+// separate translation unit (update_class.hip compiled with -DDANSE_DMAX=N)
+// so the build parallelises; the engine dispatches by DMAX at launch time.
+#pragma once
+#include "kernels.hpp"
+
+namespace danse {
+
+constexpr int kMaxDMax = 16;
+constexpr int class_dmax(int D) { return D < 2 ? 2 : D; }
+constexpr int class_group(int DMAX) { return DMAX <= 4 ? 4 : 16; }
+
+#define DANSE_FOR_EACH_CLASS(X) \
+  X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16)
+
+#define DANSE_DECLARE_CLASS(N)                                                                      \
+  void launch_update_d##N(const UpdateArgs& a, hipStream_t st);                                     \
+  void launch_filter_update_d##N(const cf* Ryy, const cf* Rnn, int B, int D, int gevd, int rank,   \
+                                 int ref, cf* w, int* diag, hipStream_t st);
+DANSE_FOR_EACH_CLASS(DANSE_DECLARE_CLASS)
+#undef DANSE_DECLARE_CLASS
+
+inline bool launch_update_class(int DMAX, const UpdateArgs& a, hipStream_t st) {
+  switch (DMAX) {
+#define DANSE_CASE(N) \
+  case N: launch_update_d##N(a, st); return true;
+    DANSE_FOR_EACH_CLASS(DANSE_CASE)
+#undef DANSE_CASE
+    default: return false;
+  }
+}
+
+inline bool launch_filter_update_class(int DMAX, const cf* Ryy, const cf* Rnn, int B, int D, int gevd, int rank,
+                                       int ref, cf* w, int* diag, hipStream_t st) {
+  switch (DMAX) {
+#define DANSE_CASE(N) \
+  case N: launch_filter_update_d##N(Ryy, Rnn, B, D, gevd, rank, ref, w, diag, st); return true;
+    DANSE_FOR_EACH_CLASS(DANSE_CASE)
+#undef DANSE_CASE
+    default: return false;
+  }
+}
+
+}  // namespace danse

@@ -61,9 +61,9 @@ DANSE_DEV float gbcast(float x) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), SRC));
   } else if constexpr (G == 4) {
     constexpr int qp = SRC | (SRC << 2) | (SRC << 4) | (SRC << 6);   // DPP quad_perm
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), qp, 0xF, 0xF, false));
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), qp, 0xF, 0xF, true));
   } else if constexpr (G == 16) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x150 + SRC, 0xF, 0xF, false));
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x150 + SRC, 0xF, 0xF, true));
   } else {
     int base = (lane_id() & ~(G - 1)) + SRC;
     return __int_as_float(__builtin_amdgcn_ds_bpermute(base << 2, __float_as_int(x)));
@@ -90,34 +90,58 @@ DANSE_DEV cf gbcast_rt(cf x, int src) {
   return cf{gbcast_rt<G>(x.re, src), gbcast_rt<G>(x.im, src)};
 }
 
-// Sum over the G lanes of my group (result in every lane of the group).
-template <int G>
-DANSE_DEV float gsum(float x) {
-#pragma unroll
-  for (int m = 1; m < G; m <<= 1) x += __shfl_xor(x, m, G);
-  return x;
+// Butterfly exchange inside a DPP row (16 lanes) without LDS:
+//   xor 1, xor 2 : quad_perm [1,0,3,2] / [2,3,0,1]
+//   half swap    : row_half_mirror (lane i <-> 7 - i, quads 0/1 swap once the
+//                  values are quad-uniform)
+//   row swap     : row_mirror (lane i <-> 15 - i)
+template <int CTRL>
+DANSE_DEV float dpp_x(float x) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), CTRL, 0xF, 0xF, true));
 }
-template <int G>
-DANSE_DEV cf gsum(cf x) {
-#pragma unroll
-  for (int m = 1; m < G; m <<= 1) {
-    x.re += __shfl_xor(x.re, m, G);
-    x.im += __shfl_xor(x.im, m, G);
+template <int G, typename Op>
+DANSE_DEV float greduce(float x, Op op) {
+  static_assert(G == 4 || G == 16 || G == 32 || G == 64, "group size");
+  x = op(x, dpp_x<0xB1>(x));
+  x = op(x, dpp_x<0x4E>(x));
+  if constexpr (G >= 16) {
+    x = op(x, dpp_x<0x141>(x));
+    x = op(x, dpp_x<0x140>(x));
+  }
+  if constexpr (G == 32) {
+    x = op(x, __shfl_xor(x, 16, 32));
+  } else if constexpr (G == 64) {
+    const float a = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 0));
+    const float b = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 16));
+    const float c = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 32));
+    const float d = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 48));
+    x = op(op(a, b), op(c, d));
   }
   return x;
 }
+
+// Sum over the G lanes of my group (result in every lane of the group).
+template <int G>
+DANSE_DEV float gsum(float x) {
+  return greduce<G>(x, [](float a, float b) { return a + b; });
+}
+template <int G>
+DANSE_DEV cf gsum(cf x) {
+  return cf{gsum<G>(x.re), gsum<G>(x.im)};
+}
 template <int G>
 DANSE_DEV float gmax(float x) {
-#pragma unroll
-  for (int m = 1; m < G; m <<= 1) x = fmaxf(x, __shfl_xor(x, m, G));
-  return x;
+  return greduce<G>(x, [](float a, float b) { return fmaxf(a, b); });
 }
 template <int G>
 DANSE_DEV float gmin(float x) {
-#pragma unroll
-  for (int m = 1; m < G; m <<= 1) x = fminf(x, __shfl_xor(x, m, G));
-  return x;
+  return greduce<G>(x, [](float a, float b) { return fminf(a, b); });
 }
+// Hardware transcendental approximations (1 ulp; no IEEE divide/sqrt
+// expansion, no denormal rescaling).
+DANSE_DEV float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
+DANSE_DEV float frsq(float x) { return __builtin_amdgcn_rsqf(x); }
+DANSE_DEV float fsqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
 // Group ballot: bit i set if lane i of my group has pred.
 template <int G>
 DANSE_DEV uint64_t gballot(bool pred) {

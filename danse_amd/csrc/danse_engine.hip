@@ -7,7 +7,8 @@
 #include <string>
 #include <vector>
 
-#include "kernels.hpp"
+#include "bcast.hpp"
+#include "classes.hpp"
 
 using namespace danse;
 
@@ -85,14 +86,8 @@ static int fail(danse_engine* eng, const std::string& m) {
 }
 
 static void pick_class(int D, int& G, int& DMAX) {
-  if (D <= 4) { G = 4; DMAX = 4; }
-  else if (D <= 8) { G = 16; DMAX = 8; }
-  else if (D <= 12) { G = 16; DMAX = 12; }
-  else if (D <= 16) { G = 16; DMAX = 16; }
-  else if (D <= 24) { G = 32; DMAX = 24; }
-  else if (D <= 32) { G = 32; DMAX = 32; }
-  else if (D <= 40) { G = 64; DMAX = 40; }
-  else { G = 64; DMAX = 64; }
+  DMAX = class_dmax(D);
+  G = class_group(DMAX);
 }
 
 // Re-initialise filters (slot 0 of the histories) and SCMs of every
@@ -203,7 +198,7 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
         fn.D = mt;
         fn.ref = eng->base[k] + c->ref;
       }
-      if (fn.D > 16) return fail(eng, "filter dimension > 16 not supported yet");
+      if (fn.D > kMaxDMax) return fail(eng, "filter dimension > 16 not supported yet");
       if (c->gevd && c->rank > fn.D) return fail(eng, "GEVD rank larger than a filter dimension");
       fn.scmOff = scmOff;
       scmOff += (long long)F * fn.D * fn.D;
@@ -426,30 +421,13 @@ static UpdateArgs make_update(danse_engine* e, int r) {
   return a;
 }
 
-template <int G, int DM>
-static void launch_update_cls(const UpdateArgs& a, int nFN, hipStream_t st) {
-  constexpr int NB = 64 / G;
-  const int nBB = (a.F + NB - 1) / NB;
-  const unsigned grid = (unsigned)(a.S * nFN * nBB);
-  if (!a.gevd || a.rank == 1)
-    hipLaunchKernelGGL((update_kernel<G, DM, 1>), dim3(grid), dim3(64), 0, st, a);
-  else
-    hipLaunchKernelGGL((update_kernel<G, DM, kRMax>), dim3(grid), dim3(64), 0, st, a);
-}
-
 static void launch_update(danse_engine* e, int r, hipStream_t st) {
   for (auto& cl : e->classes) {
     UpdateArgs a = make_update(e, r);
     a.nFN = (int)cl.host.size();
     a.fn = cl.dev;
     a.famNodeId = cl.devIds;
-    switch (cl.DMAX) {
-      case 4: launch_update_cls<4, 4>(a, a.nFN, st); break;
-      case 8: launch_update_cls<16, 8>(a, a.nFN, st); break;
-      case 12: launch_update_cls<16, 12>(a, a.nFN, st); break;
-      case 16: launch_update_cls<16, 16>(a, a.nFN, st); break;
-      default: break;   // D > 16: rejected at create time (see pick_class)
-    }
+    launch_update_class(cl.DMAX, a, st);   // D > kMaxDMax rejected at create time
   }
 }
 
@@ -655,43 +633,6 @@ __global__ void __launch_bounds__(256) wola_analysis_kernel(const float* x, int 
   for (int f = threadIdx.x; f < F; f += blockDim.x) out[(long long)c * F + f] = inv * o[f];
 }
 
-template <int G, int DMAX>
-__global__ void __launch_bounds__(64) filter_update_kernel(const cf* Ryy, const cf* Rnn, int B, int D, int gevd,
-                                                          int rank, int ref, cf* w, int* diag) {
-  constexpr int NB = 64 / G;
-  __shared__ SolverLDS<DMAX> lds[NB];
-  const int li = threadIdx.x & (G - 1);
-  const int gi = threadIdx.x / G;
-  int b = blockIdx.x * NB + gi;
-  const bool valid = b < B;
-  if (!valid) b = B - 1;
-  const bool act = li < D;
-  const int row = act ? li : 0;
-  cf A[DMAX], Bm[DMAX];
-  sfor<0, DMAX>([&](auto cc) {
-    constexpr int c = decltype(cc)::value;
-    const int cl = (c < D) ? c : D - 1;
-    const cf a = Ryy[((long long)b * D + row) * D + cl];
-    const cf n = Rnn[((long long)b * D + row) * D + cl];
-    A[c] = (act && c < D) ? a : cf{0.0f, 0.0f};
-    Bm[c] = (act && c < D) ? n : cf{0.0f, 0.0f};
-  });
-  bool ok = true;
-  cf wv;
-  if (gevd) wv = gevd_filter<G, DMAX, kRMax>(A, Bm, lds[gi], li, D, rank, ref, ok);
-  else wv = mwf_filter<G, DMAX>(A, Bm, li, D, ref, ok);
-  if (act && valid) w[(long long)b * D + li] = wv;
-  if (diag && li == 0 && valid) diag[b] = ok ? 0 : 1;
-}
-
-template <int G, int DM>
-static void launch_fu(const cf* Ryy, const cf* Rnn, int B, int D, int gevd, int rank, int ref, cf* w, int* diag,
-                      hipStream_t st) {
-  constexpr int NB = 64 / G;
-  hipLaunchKernelGGL((filter_update_kernel<G, DM>), dim3((B + NB - 1) / NB), dim3(64), 0, st, Ryy, Rnn, B, D, gevd,
-                     rank, ref, w, diag);
-}
-
 // Batch SCMs: Ryy = mean over VAD frames of y y^H, Rnn over the others.
 // One workgroup per batch item b; thread (i, j) accumulates over frames.
 __global__ void batch_covmats_kernel(const cf* Y, int B, int Tf, int D, const uint8_t* vad, cf* Ryy, cf* Rnn) {
@@ -744,13 +685,8 @@ int danse_filter_update(const float* Ryy, const float* Rnn, int32_t B, int32_t D
   const cf* a = (const cf*)Ryy;
   const cf* n = (const cf*)Rnn;
   cf* o = (cf*)w;
-  switch (DM) {
-    case 4: launch_fu<4, 4>(a, n, B, D, gevd, rank, ref, o, diag, st); break;
-    case 8: launch_fu<16, 8>(a, n, B, D, gevd, rank, ref, o, diag, st); break;
-    case 12: launch_fu<16, 12>(a, n, B, D, gevd, rank, ref, o, diag, st); break;
-    case 16: launch_fu<16, 16>(a, n, B, D, gevd, rank, ref, o, diag, st); break;
-    default: return fail(nullptr, "D > 16 not supported yet");
-  }
+  if (D > kMaxDMax) return fail(nullptr, "D > 16 not supported yet");
+  launch_filter_update_class(DM, a, n, B, D, gevd, rank, ref, o, diag, st);
   HIPCHK(hipGetLastError());
   return 0;
 }
