@@ -9,12 +9,16 @@
 
 namespace danse {
 
-constexpr int kMaxDMax = 16;
-constexpr int class_dmax(int D) { return D < 2 ? 2 : D; }
-constexpr int class_group(int DMAX) { return DMAX <= 4 ? 4 : 16; }
+constexpr int kMaxDMax = 64;
+// D <= 16: exact classes (lane groups, solver.hpp); larger D rounds up to a
+// multiple of 8 and runs one bin per wavefront with runtime pivot loops over
+// the actual D (G = 64, solver64.hpp).
+constexpr int class_dmax(int D) { return D < 2 ? 2 : D <= 16 ? D : ((D + 7) / 8) * 8; }
+constexpr int class_group(int DMAX) { return DMAX <= 4 ? 4 : (DMAX <= 16 ? 16 : 64); }
 
 #define DANSE_FOR_EACH_CLASS(X) \
-  X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16)
+  X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16) X(24) X(32) X(40) \
+  X(48) X(56) X(64)
 
 #define DANSE_DECLARE_CLASS(N)                                                                      \
   void launch_update_d##N(const UpdateArgs& a, hipStream_t st);                                     \

@@ -198,7 +198,7 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
         fn.D = mt;
         fn.ref = eng->base[k] + c->ref;
       }
-      if (fn.D > kMaxDMax) return fail(eng, "filter dimension > 16 not supported yet");
+      if (fn.D > kMaxDMax) return fail(eng, "filter dimension > 64 not supported");
       if (c->gevd && c->rank > fn.D) return fail(eng, "GEVD rank larger than a filter dimension");
       fn.scmOff = scmOff;
       scmOff += (long long)F * fn.D * fn.D;
@@ -685,7 +685,6 @@ int danse_filter_update(const float* Ryy, const float* Rnn, int32_t B, int32_t D
   const cf* a = (const cf*)Ryy;
   const cf* n = (const cf*)Rnn;
   cf* o = (cf*)w;
-  if (D > kMaxDMax) return fail(nullptr, "D > 16 not supported yet");
   launch_filter_update_class(DM, a, n, B, D, gevd, rank, ref, o, diag, st);
   HIPCHK(hipGetLastError());
   return 0;

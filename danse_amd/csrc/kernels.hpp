@@ -65,6 +65,42 @@ struct UpdateArgs {
   int* diag;               // [S*K*kMaxFam]
 };
 
+// External filters (DANSE family, update_external_filters,
+// d_classes.py:1627-1694) and dhat = w^H yhat (d_base.py:2075, DC / Nyquist
+// forced real, quirk Q7) of one (scene, family-node, bin); lane li of the
+// bin's lane group holds w_li, dh is the group sum of conj(w) y.
+DANSE_DEV void node_bin_tail(const UpdateArgs& a, const FamNode& d, int s, int f, int li, uint8_t fl, bool pregiven,
+                             bool valid, cf w, cf y, cf dh) {
+  const int F = a.F;
+  const int r = a.r;
+  if (d.extMode >= 0 && !pregiven) {
+    const int M = d.M;
+    const long long eb = (long long)s * a.wExtStride + d.wExtOff;
+    const int eP = a.wExtHistory ? r : (r & 1);
+    const int eN = a.wExtHistory ? r + 1 : ((r + 1) & 1);
+    cf* eprev = a.wExtHist + eb + ((long long)eP * F + f) * M;
+    cf* enext = a.wExtHist + eb + ((long long)eN * F + f) * M;
+    cf* tgt = a.wExtTarget + (long long)s * a.tgtStride + d.tgtOff + (long long)f * M;
+    if (li < M && valid) {
+      cf ne;
+      if (d.extMode == 0) ne = w;
+      else if (d.extMode == 2) ne = eprev[li];
+      else if (d.extMode == 3) ne = cf{(li == d.ref) ? 1.0f : 0.0f, 0.0f};
+      else {
+        const float be = a.betaExt[s * a.K + d.k];
+        const cf tg = tgt[li];
+        ne = be * eprev[li] + (1.0f - be) * tg;
+        if (fl & DANSE_FLAG_EXT_TARGET) tgt[li] = (1.0f - a.alphaExt) * tg + a.alphaExt * w;
+      }
+      enext[li] = ne;
+    }
+  }
+  if (f == 0 || f == F - 1) dh.im = 0.0f;
+  if (li == 0 && valid) {
+    a.dhat[((((long long)d.fam * a.S + s) * a.K + d.k) * a.R + r) * F + f] = dh;
+  }
+}
+
 template <int G, int DMAX, int RMAX>
 __global__ void __launch_bounds__(64) update_kernel(const UpdateArgs a) {
   static_assert(DMAX <= G, "a lane group must hold every row");
@@ -165,36 +201,8 @@ __global__ void __launch_bounds__(64) update_kernel(const UpdateArgs a) {
   }
   if (act && valid && !pregiven) wNext[li] = w;
 
-  // ---- external filters (DANSE family)
-  if (d.extMode >= 0 && !pregiven) {
-    const int M = d.M;
-    const long long eb = (long long)s * a.wExtStride + d.wExtOff;
-    const int eP = a.wExtHistory ? r : (r & 1);
-    const int eN = a.wExtHistory ? r + 1 : ((r + 1) & 1);
-    cf* eprev = a.wExtHist + eb + ((long long)eP * F + f) * M;
-    cf* enext = a.wExtHist + eb + ((long long)eN * F + f) * M;
-    cf* tgt = a.wExtTarget + (long long)s * a.tgtStride + d.tgtOff + (long long)f * M;
-    if (li < M && valid) {
-      cf ne;
-      if (d.extMode == 0) ne = w;
-      else if (d.extMode == 2) ne = eprev[li];
-      else if (d.extMode == 3) ne = cf{(li == d.ref) ? 1.0f : 0.0f, 0.0f};
-      else {
-        const float be = a.betaExt[s * a.K + d.k];
-        const cf tg = tgt[li];
-        ne = be * eprev[li] + (1.0f - be) * tg;
-        if (fl & DANSE_FLAG_EXT_TARGET) tgt[li] = (1.0f - a.alphaExt) * tg + a.alphaExt * w;
-      }
-      enext[li] = ne;
-    }
-  }
-
-  // ---- dhat = w^H yhat (DC / Nyquist forced real, quirk Q7)
-  cf dh = gsum<G>(act ? cmul(w, y) : cf{0.0f, 0.0f});
-  if (f == 0 || f == F - 1) dh.im = 0.0f;
-  if (li == 0 && valid) {
-    a.dhat[((((long long)d.fam * a.S + s) * a.K + d.k) * a.R + r) * F + f] = dh;
-  }
+  const cf dh = gsum<G>(act ? cmul(w, y) : cf{0.0f, 0.0f});
+  node_bin_tail(a, d, s, f, li, fl, pregiven, valid, w, y, dh);
 }
 
 // Stand-alone batched filter update (danse_filter_update): one bin per lane
