@@ -180,7 +180,7 @@ def main():
     for r in range(R):
         eng.bcast(r)
         if runner is not None:
-            runner.exchange()
+            runner.exchange(r)
         a = torch.cuda.Event(enable_timing=True)
         b = torch.cuda.Event(enable_timing=True)
         a.record(stream)

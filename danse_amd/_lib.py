@@ -39,6 +39,7 @@ class DanseCfg(ctypes.Structure):
         ('bcEnd', _p_i32), ('upEnd', _p_i32), ('flags', _p_u8),
         ('w0', _p_f32), ('wExt0', _p_f32), ('wExtTarget0', _p_f32), ('scmInit', _p_f32),
         ('keepHistory', _c_i32),
+        ('zLag', _p_u8), ('zPhase', ctypes.POINTER(ctypes.c_double)),
     ]
 
 

@@ -21,7 +21,7 @@ struct BcastArgs {
   const int* upEnd;        // [R*K]
   const float* y;          // [S][MT][T]
   cf* Yspec;               // [2][S][MT][F]
-  cf* Zspec;               // [K][S][F]
+  cf* Zspec;               // [2][K][S][F] (slot r & 1)
   float* zPrev;            // [S][K][N]
   float* zStream;          // [S][K][R*Ns]
   const cf* wExtHist;      // per scene block (stride wExtStride) : node offsets wExtNodeOff
@@ -169,7 +169,7 @@ __global__ void __launch_bounds__(256) bcast_kernel(const BcastArgs a) {
   }
   __syncthreads();
   out = fft1024(b0, b1, a.tw);
-  cf* Zs = a.Zspec + ((long long)k * a.S + s) * F;
+  cf* Zs = a.Zspec + (((long long)(r & 1) * a.K + k) * a.S + s) * F;
   for (int f = tid; f < F; f += blockDim.x) Zs[f] = invSqNs * out[f];
 }
 

@@ -47,6 +47,8 @@ struct danse_engine {
   // device
   int *dM = nullptr, *dBase = nullptr, *dBcEnd = nullptr, *dUpEnd = nullptr, *dChan = nullptr;
   uint8_t* dFlags = nullptr;
+  uint8_t* dZLag = nullptr;
+  double* dZPhase = nullptr;
   float *dBeta = nullptr, *dBetaExt = nullptr, *dhA = nullptr, *dhS = nullptr, *dNorm = nullptr;
   cf* dTw = nullptr;
   long long* dWExtNodeOff = nullptr;
@@ -128,6 +130,7 @@ int danse_engine_reset(danse_engine* eng, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   const int S = eng->S, K = eng->K, F = eng->F, R = eng->R;
   HIPCHK(hipMemsetAsync(eng->zPrev, 0, (size_t)S * K * eng->N * sizeof(float), st));
+  HIPCHK(hipMemsetAsync(eng->Zspec, 0, (size_t)2 * K * S * F * sizeof(cf), st));
   HIPCHK(hipMemsetAsync(eng->zStream, 0, (size_t)S * K * R * eng->Ns * sizeof(float), st));
   HIPCHK(hipMemsetAsync(eng->dhat, 0, (size_t)kMaxFam * S * K * R * F * sizeof(cf), st));
   HIPCHK(hipMemsetAsync(eng->d, 0, (size_t)kMaxFam * S * K * eng->T * sizeof(float), st));
@@ -253,6 +256,14 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
   HIPCHK(hipMemcpy(eng->dUpEnd, c->upEnd, (size_t)R * K * sizeof(int), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(eng->dChan, eng->chanList.data(), eng->chanList.size() * sizeof(int), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(eng->dFlags, c->flags, (size_t)R * S * kMaxFam * K, hipMemcpyHostToDevice));
+  if (c->zLag) {
+    HIPCHK(dalloc(&eng->dZLag, (size_t)R * K * K));
+    HIPCHK(hipMemcpy(eng->dZLag, c->zLag, (size_t)R * K * K, hipMemcpyHostToDevice));
+  }
+  if (c->zPhase) {
+    HIPCHK(dalloc(&eng->dZPhase, (size_t)R * K * K));
+    HIPCHK(hipMemcpy(eng->dZPhase, c->zPhase, (size_t)R * K * K * sizeof(double), hipMemcpyHostToDevice));
+  }
   HIPCHK(hipMemcpy(eng->dBeta, c->beta, (size_t)S * K * sizeof(float), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(eng->dBetaExt, c->betaExt, (size_t)S * K * sizeof(float), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(eng->dhA, c->winAnalysis, c->N * sizeof(float), hipMemcpyHostToDevice));
@@ -282,7 +293,7 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
   }
   const size_t MT = (size_t)eng->MT;
   HIPCHK(dalloc(&eng->Yspec, 2 * S * MT * F));
-  HIPCHK(dalloc(&eng->Zspec, (size_t)K * S * F));
+  HIPCHK(dalloc(&eng->Zspec, (size_t)2 * K * S * F));
   HIPCHK(dalloc(&eng->zPrev, (size_t)S * K * c->N));
   HIPCHK(dalloc(&eng->zStream, (size_t)S * K * R * c->Ns));
   HIPCHK(dalloc(&eng->Ryy, (size_t)S * eng->scmStride));
@@ -294,7 +305,7 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
   HIPCHK(dalloc(&eng->d, (size_t)kMaxFam * S * K * c->T));
   HIPCHK(dalloc(&eng->diag, (size_t)S * K * kMaxFam));
   HIPCHK(hipMemset(eng->Yspec, 0, 2 * S * MT * F * sizeof(cf)));
-  HIPCHK(hipMemset(eng->Zspec, 0, (size_t)K * S * F * sizeof(cf)));
+  HIPCHK(hipMemset(eng->Zspec, 0, (size_t)2 * K * S * F * sizeof(cf)));
   HIPCHK(hipMemset(eng->zPrev, 0, (size_t)S * K * c->N * sizeof(float)));
   HIPCHK(hipMemset(eng->zStream, 0, (size_t)S * K * R * c->Ns * sizeof(float)));
   HIPCHK(hipMemset(eng->dhat, 0, (size_t)kMaxFam * S * K * R * F * sizeof(cf)));
@@ -377,7 +388,8 @@ void danse_engine_destroy(danse_engine* eng) {
   if (!eng) return;
   (void)hipSetDevice(eng->dev);
   if (eng->graphExec) (void)hipGraphExecDestroy(eng->graphExec);
-  void* ptrs[] = {eng->dM, eng->dBase, eng->dBcEnd, eng->dUpEnd, eng->dChan, eng->dFlags, eng->dBeta, eng->dBetaExt,
+  void* ptrs[] = {eng->dM, eng->dBase, eng->dBcEnd, eng->dUpEnd, eng->dChan, eng->dFlags, eng->dZLag, eng->dZPhase,
+                  eng->dBeta, eng->dBetaExt,
                   eng->dhA, eng->dhS, eng->dNorm, eng->dTw, eng->dWExtNodeOff, eng->Yspec,
                   eng->ownZspec ? eng->Zspec : nullptr, eng->Ryy,
                   eng->Rnn, eng->wHist, eng->wExtHist, eng->wExtTarget, eng->dhat, eng->zPrev, eng->zStream, eng->d,
@@ -414,6 +426,7 @@ static UpdateArgs make_update(danse_engine* e, int r) {
   UpdateArgs a{};
   a.S = e->S; a.K = e->K; a.MT = e->MT; a.F = e->F; a.R = e->R; a.r = r;
   a.chanList = e->dChan; a.flags = e->dFlags; a.Yspec = e->Yspec; a.Zspec = e->Zspec;
+  a.zLag = e->dZLag; a.zPhase = e->dZPhase;
   a.Ryy = e->Ryy; a.Rnn = e->Rnn; a.scmStride = e->scmStride; a.wHist = e->wHist; a.wStride = e->wStride;
   a.wHistory = e->keepHistory; a.wExtHist = e->wExtHist; a.wExtStride = e->wExtStride; a.wExtHistory = e->keepHistory;
   a.wExtTarget = e->wExtTarget; a.tgtStride = e->tgtStride; a.dhat = e->dhat; a.beta = e->dBeta;
@@ -522,7 +535,7 @@ int danse_engine_set_zspec(danse_engine* eng, void* ptr) {
 int danse_engine_zspec(danse_engine* eng, void** ptr, size_t* bytes) {
   if (!eng || !ptr || !bytes) return fail(eng, "null argument");
   *ptr = eng->Zspec;
-  *bytes = (size_t)eng->K * eng->S * eng->F * sizeof(cf);
+  *bytes = (size_t)2 * eng->K * eng->S * eng->F * sizeof(cf);
   return 0;
 }
 

@@ -45,7 +45,9 @@ struct UpdateArgs {
   const int* chanList;
   const uint8_t* flags;    // [R][S][kMaxFam][K]
   const cf* Yspec;         // [2][S][MT][F]
-  const cf* Zspec;         // [K][S][F]
+  const cf* Zspec;         // [2][K][S][F]: slot r & 1 holds the senders' round-r frames
+  const uint8_t* zLag;     // [R][K][K] or null: 1 = consume sender q's round r-1 frame (SROs)
+  const double* zPhase;    // [R][K][K] or null: SRO phase-compensation offsets (samples)
   cf* Ryy;                 // per scene stride scmStride
   cf* Rnn;
   long long scmStride;
@@ -64,6 +66,32 @@ struct UpdateArgs {
   int gevd, rank;
   int* diag;               // [S*K*kMaxFam]
 };
+
+// Observation vector entry of lane li (channel chanList[chanOff + li]) for
+// bin f: a local spectrum, or the fused spectrum of sender q (the frame of
+// round r or r-1, zLag) with the SRO phase compensation
+// yhat *= exp(-j 2 pi f phi / N) of compensate_sros (d_classes.py:1936-2046).
+DANSE_DEV cf load_y(const UpdateArgs& a, const FamNode& d, int s, int f, int li, bool act) {
+  const int F = a.F, r = a.r;
+  const int c = a.chanList[d.chanOff + (act ? li : 0)];
+  cf v;
+  if (c < a.MT) {
+    v = a.Yspec[(((long long)((r + 1) & 1) * a.S + s) * a.MT + c) * F + f];
+  } else {
+    const int q = c - a.MT;
+    const long long lk = ((long long)r * a.K + d.k) * a.K + q;
+    const int lag = a.zLag ? a.zLag[lk] : 0;
+    v = a.Zspec[((((long long)((r - lag) & 1)) * a.K + q) * a.S + s) * F + f];
+    if (a.zPhase) {
+      double t = (double)f * a.zPhase[lk] / (double)(2 * (F - 1));
+      t -= rint(t);
+      float sn, cs;
+      sincospif(-2.0f * (float)t, &sn, &cs);
+      v = v * cf{cs, sn};
+    }
+  }
+  return act ? v : cf{0.0f, 0.0f};
+}
 
 // External filters (DANSE family, update_external_filters,
 // d_classes.py:1627-1694) and dhat = w^H yhat (d_base.py:2075, DC / Nyquist
@@ -127,14 +155,7 @@ __global__ void __launch_bounds__(64) update_kernel(const UpdateArgs a) {
   const bool solve = (fl & DANSE_FLAG_SOLVE) != 0;
 
   // ---- observation vector yhat_li
-  cf y = cf{0.0f, 0.0f};
-  {
-    const int c = a.chanList[d.chanOff + (act ? li : 0)];
-    const cf* src = (c < a.MT) ? a.Yspec + (((long long)((r + 1) & 1) * a.S + s) * a.MT + c) * F
-                               : a.Zspec + ((long long)(c - a.MT) * a.S + s) * F;
-    const cf v = src[f];
-    y = act ? v : cf{0.0f, 0.0f};
-  }
+  const cf y = load_y(a, d, s, f, li, act);
   const float beta = a.beta[s * a.K + d.k];
   const float invD = 1.0f / (float)D;
   const long long matOff = (long long)s * a.scmStride + d.scmOff + (long long)f * D * D;

@@ -27,14 +27,7 @@ __global__ void __launch_bounds__(64) update_kernel_big(const UpdateArgs a) {
   const int opY = fl & 3, opN = (fl >> 2) & 3;
   const bool solve = (fl & DANSE_FLAG_SOLVE) != 0;
 
-  cf y = cf{0.0f, 0.0f};
-  {
-    const int c = a.chanList[d.chanOff + (act ? li : 0)];
-    const cf* src = (c < a.MT) ? a.Yspec + (((long long)((r + 1) & 1) * a.S + s) * a.MT + c) * F
-                               : a.Zspec + ((long long)(c - a.MT) * a.S + s) * F;
-    const cf v = src[f];
-    y = act ? v : cf{0.0f, 0.0f};
-  }
+  const cf y = load_y(a, d, s, f, li, act);
   const float beta = a.beta[s * a.K + d.k];
   const float invD = 1.0f / (float)D;
   const long long matOff = (long long)s * a.scmStride + d.scmOff + (long long)f * D * D;

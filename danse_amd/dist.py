@@ -41,11 +41,17 @@ class ShardedRun:
         n = engine.zspec_numel()
         self.zbuf = torch.zeros(n, dtype=torch.float32, device=engine.torch_device)
         engine.set_zspec(self.zbuf)
-        chunk = n // self.world
-        self.mine = self.zbuf[self.rank * chunk:(self.rank + 1) * chunk]
+        # the HIP engine keeps two round slots ([2][K][S][F], round r -> slot
+        # r & 1) so that SRO-lagged receivers can read the previous round
+        self.slots = getattr(engine, 'zspec_slots', 1)
+        per = n // self.slots
+        chunk = per // self.world
+        self.slot = [self.zbuf[i * per:(i + 1) * per] for i in range(self.slots)]
+        self.mine = [v[self.rank * chunk:(self.rank + 1) * chunk] for v in self.slot]
 
-    def exchange(self):
-        self.dist.all_gather_into_tensor(self.zbuf, self.mine, group=self.group)
+    def exchange(self, r=0):
+        i = r % self.slots
+        self.dist.all_gather_into_tensor(self.slot[i], self.mine[i], group=self.group)
 
     def run(self, reset=True):
         e = self.eng
@@ -53,7 +59,7 @@ class ShardedRun:
             e.reset()
         for r in range(e.R):
             e.bcast(r)
-            self.exchange()
+            self.exchange(r)
             e.update(r)
         e.finish()
         return self
@@ -66,6 +72,7 @@ class ShardedEngine:
         self.e = engine
         self.R, self.K, self.k0, self.k1 = engine.R, engine.K, engine.k0, engine.k1
         self.torch_device = f'cuda:{engine.device}'
+        self.zspec_slots = 2
 
     def zspec_numel(self):
         _, nb = self.e.zspec()

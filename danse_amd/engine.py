@@ -119,8 +119,6 @@ class DanseEngine:
             raise ValueError('DanseEngine runs the online engine (simType online)')
         if p.desSigProcessingType != 'wola':
             raise NotImplementedError('desSigProcessingType conv (T(z) estimate) on the device path')
-        if p.compensateSROs:
-            raise NotImplementedError('SRO compensation on the device path (next round)')
         self.device = device
         self.keepHistory = keepHistory
         self.k0, self.k1 = nodeRange if nodeRange is not None else (0, K)
@@ -133,6 +131,10 @@ class DanseEngine:
         self.events, self.fsEv = events, fs
         self.rt = compile_rounds(events, fs, p, K)
         self.R = R = self.rt.nRounds
+        if not self.rt.synchronous and (p.computeCentralised or p.computeSingleSensorBroadcast):
+            raise NotImplementedError('centralised / single-sensor-broadcast estimates with asynchronous (SRO) '
+                                      'clocks are not on the device path')
+        self._build_sro_tables(sc0)
         if R < 1:
             raise ValueError('signal too short for one DANSE round')
         if R > self.nIter:
@@ -179,6 +181,36 @@ class DanseEngine:
             self._load_pregiven(pregiven)
 
     # ------------------------------------------------------------------ #
+    def _build_sro_tables(self, sc0):
+        """Fused-frame lags and SRO phase-compensation offsets per (round,
+        node, sender), restating ``compensate_sros`` / ``update_sro_estimates``
+        (``d_classes.py:1936-2046,2364-2621``) with Oracle estimates
+        eps_q = (SRO_q - SRO_k) 1e-6: at update r, phi += flag (with
+        ``includeFSDflags``), the frame is compensated with phi, then
+        phi -= eps_q Ns."""
+        p, K, R = self.p, self.K, self.R
+        self._zLag = None if self.rt.synchronous else np.ascontiguousarray(self.rt.zLag[:R], dtype=np.uint8)
+        self._zPhase = None
+        if not p.compensateSROs:
+            return
+        if p.estimateSROs != 'Oracle':
+            raise NotImplementedError(f'estimateSROs={p.estimateSROs!r} on the device path (Oracle only)')
+        sro = np.array([nd.sro for nd in sc0.wasn], dtype=np.float64)
+        for sc in self.scenes:
+            if not np.array_equal(np.array([nd.sro for nd in sc.wasn], dtype=np.float64), sro):
+                raise ValueError('all scenes of one engine must share the node SROs')
+        ph = np.zeros((R, K, K), dtype=np.float64)
+        for k in range(K):
+            phi = np.zeros(K, dtype=np.float64)
+            nb = [q for q in range(K) if q != k]
+            est = (sro[nb] - sro[k]) * 1e-6
+            for r in range(R):
+                if p.includeFSDflags:
+                    phi[nb] += self.rt.flags[r, k, nb]
+                ph[r, k, :] = phi
+                phi[nb] -= est * self.Ns
+        self._zPhase = ph
+
     def _build_flags(self):
         p, S, K, R = self.p, self.S, self.K, self.R
         fl = np.zeros((R, S, 4, K), dtype=np.uint8)
@@ -196,16 +228,16 @@ class DanseEngine:
         nY = np.cumsum(vad, axis=2)          # counters after the increment of round r
         nN = np.arange(1, R + 1)[None, None, :] - nY
         doSolve = self.rt.doSolve.T.astype(bool)    # [K][R]
-        t = self.rt.t
+        t = self.rt.t                                # [R][K]
         tOK = t >= p.startUpdatesAfterAtLeast
         # external-filter target timer (asy)
         extT = np.zeros((R, K), dtype=bool)
         last = np.zeros(K)
         for r in range(R):
             for k in range(K):
-                if t[r] - last[k] >= p.timeBtwExternalFiltUpdates:
+                if t[r, k] - last[k] >= p.timeBtwExternalFiltUpdates:
                     extT[r, k] = True
-                    last[k] = t[r]
+                    last[k] = t[r, k]
         basis = p.use1stFrameAsBasis
         for f in self.fams:
             for k in range(K):
@@ -219,7 +251,7 @@ class DanseEngine:
                     else:
                         opY = np.where(v, L.OP_AVG, L.OP_KEEP)
                         opN = np.where(~v, L.OP_AVG, L.OP_KEEP)
-                    gate = (ny > D) & (nn > D) & tOK
+                    gate = (ny > D) & (nn > D) & tOK[:, k]
                     started = np.maximum.accumulate(gate)
                     if started.any():
                         self.startRound[s, f, k] = int(np.argmax(started))
@@ -299,6 +331,8 @@ class DanseEngine:
                                         _ptr(self._tgt0, ctypes.c_float))
         c.scmInit = _ptr(self._scm, ctypes.c_float)
         c.keepHistory = int(bool(self.keepHistory))
+        c.zLag = _ptr(self._zLag, ctypes.c_uint8)
+        c.zPhase = _ptr(self._zPhase, ctypes.c_double)
         self._cfg = c
         eng = ctypes.c_void_p()
         L.check(self.lib.danse_engine_create(ctypes.byref(c), int(self.device), ctypes.byref(eng)))

@@ -193,38 +193,102 @@ def build_events_matrix(up_t, bc_t, nodeUpdating='seq', firstUpdatingNode=0, min
 
 @dataclass
 class RoundTables:
-    """Per-round integer schedule for synchronous fully connected wholeChunk
-    DANSE (every node broadcasts, then every node updates, once per round).
+    """Per-round integer schedule of fully connected wholeChunk DANSE.  Device
+    round r = DANSE iteration r of every node: phase A runs every node's
+    broadcast r, phase B every node's update r.
 
-    bcEnd[r, k]   sample index one past the broadcast frame's end (floor(t fs))
-    upEnd[r, k]   same for the update frame, already shifted by -(N - Ns)
-    doSolve[r, k] 1 if the filter update is not bypassed (seq round robin)
-    nRounds       number of rounds (= number of DANSE iterations per node)
+    bcEnd[r, k]    sample index one past the broadcast frame's end (floor(t fs))
+    upEnd[r, k]    same for the update frame, already shifted by -(N - Ns)
+    doSolve[r, k]  1 if the filter update is not bypassed (seq round robin)
+    zLag[r, k, q]  0: node k's update r consumes sender q's fused frame of
+                   round r; 1: of round r-1 (SRO clocks, quirk Q13)
+    flags[r, k, q] full-sample-drift buffer flags (process_incoming_signals_
+                   buffers, d_classes.py:1745-1807)
+    nRounds        number of rounds (= DANSE iterations per node)
+    t[r, k]        instant (reference time axis) of node k's update r
+    synchronous    every node shares every instant (no SROs)
     """
     bcEnd: np.ndarray
     upEnd: np.ndarray
     doSolve: np.ndarray
     nRounds: int
-    t: np.ndarray = None        # [R] event instant of each round (float64)
+    t: np.ndarray = None
+    zLag: np.ndarray = None
+    flags: np.ndarray = None
+    synchronous: bool = True
 
 
 def compile_rounds(events, fs, p, nNodes: int) -> RoundTables:
-    """Checks that the schedule is round-synchronous (no SROs: all nodes share
-    every instant, broadcasts before updates) and emits integer tables.
-    Raises NotImplementedError otherwise (asynchronous clocks go through the
-    per-event path)."""
-    bcEnd, upEnd, doSolve, ts = [], [], [], []
+    """Turns the reference event list into integer round tables.
+
+    Replays the events in the reference's order (``d_core.py:66-90``) with
+    the buffer bookkeeping of ``fill_buffers`` / ``process_incoming_signals_
+    buffers`` (``d_classes.py:1185-1224,1701-1807``): every broadcast adds Ns
+    samples to each neighbour's buffer, every update empties it.  The fused
+    frame a node consumes is the last N received samples of the sender's
+    stream; the device keeps the sender spectra of the last two rounds, so a
+    schedule is accepted when every update consumes the sender's round r or
+    r-1 frame (SRO drift below Ns samples).  Raises NotImplementedError for
+    anything else (fewSamples broadcasts, larger drifts)."""
+    if p.broadcastType != 'wholeChunk':
+        raise NotImplementedError('fewSamples broadcasts are not on the device round path')
+    K, N, Ns = nNodes, p.DFTsize, p.Ns
+    bc = [[] for _ in range(K)]
+    up = [[] for _ in range(K)]
+    solve = [[] for _ in range(K)]
+    tUp = [[] for _ in range(K)]
+    buf = np.zeros((K, K), dtype=np.int64)      # buf[k, q]: samples from q waiting at k
+    recv = np.zeros((K, K), dtype=np.int64)     # total samples of q's stream received by k
+    lag = [[] for _ in range(K)]
+    flg = [[] for _ in range(K)]
+    sync = True
     for ev in events:
         ks = list(ev.nodes)
-        if ev.type != ['bc'] * nNodes + ['up'] * nNodes or ks != list(range(nNodes)) * 2:
-            raise NotImplementedError('schedule is not round-synchronous (SROs or fewSamples)')
-        if p.broadcastType != 'wholeChunk':
-            raise NotImplementedError('fewSamples broadcasts use the per-event path')
-        be = [int(np.floor(ev.t * fs[k])) for k in range(nNodes)]
-        ue = [int(np.floor(ev.t * fs[k])) - (p.DFTsize - p.Ns) for k in range(nNodes)]
-        bcEnd.append(be)
-        upEnd.append(ue)
-        doSolve.append([0 if b else 1 for b in ev.bypassUpdate[nNodes:]])
-        ts.append(ev.t)
-    return RoundTables(np.array(bcEnd, dtype=np.int64), np.array(upEnd, dtype=np.int64),
-                       np.array(doSolve, dtype=np.int32), len(events), np.array(ts, dtype=np.float64))
+        if ev.type != ['bc'] * K + ['up'] * K or ks != list(range(K)) * 2:
+            sync = False
+        for ii, (k, typ) in enumerate(zip(ks, ev.type)):
+            k = int(k)
+            if typ == 'bc':
+                if len(bc[k]) != len(up[k]):
+                    raise NotImplementedError('two broadcasts of a node without an update in between')
+                bc[k].append(int(np.floor(ev.t * fs[k])))
+                for q in range(K):
+                    if q != k:
+                        buf[q, k] += Ns
+                        recv[q, k] += Ns
+            else:
+                r = len(up[k])
+                if len(bc[k]) != r + 1:
+                    raise NotImplementedError('update without its broadcast')
+                up[k].append(int(np.floor(ev.t * fs[k])) - (N - Ns))
+                solve[k].append(0 if ev.bypassUpdate[ii] else 1)
+                tUp[k].append(ev.t)
+                lr = np.zeros(K, dtype=np.int64)
+                fr = np.zeros(K, dtype=np.int64)
+                for q in range(K):
+                    if q == k:
+                        continue
+                    Bq = buf[k, q]
+                    if r == 0:
+                        fr[q] = 0 if Bq == N else (-(N - Bq) if Bq < N else (Bq - N))
+                    else:
+                        fr[q] = 0 if Bq == Ns else (-(Ns - Bq) if Bq < Ns else (Bq - Ns))
+                    d = (r + 1) * Ns - recv[k, q]
+                    if d not in (0, Ns):
+                        raise NotImplementedError(f'node {k} update {r} consumes sender {q} {d} samples behind '
+                                                  '(drift beyond one chunk)')
+                    lr[q] = d // Ns
+                    buf[k, q] = 0
+                lag[k].append(lr)
+                flg[k].append(fr)
+    R = min(len(u) for u in up)
+    if R < 1:
+        return RoundTables(np.zeros((0, K), np.int64), np.zeros((0, K), np.int64), np.zeros((0, K), np.int32), 0,
+                           np.zeros((0, K)), np.zeros((0, K, K), np.uint8), np.zeros((0, K, K), np.int64), sync)
+    bcEnd = np.array([b[:R] for b in bc], dtype=np.int64).T
+    upEnd = np.array([u[:R] for u in up], dtype=np.int64).T
+    doSolve = np.array([x[:R] for x in solve], dtype=np.int32).T
+    zLag = np.stack([np.stack(l[:R]) for l in lag], axis=1).astype(np.uint8)     # [R][K][K]
+    flags = np.stack([np.stack(f[:R]) for f in flg], axis=1)                   # [R][K][K]
+    t = np.array([x[:R] for x in tUp], dtype=np.float64).T
+    return RoundTables(bcEnd, upEnd, doSolve, R, t, zLag, flags, sync)

@@ -100,6 +100,15 @@ typedef struct danse_cfg {
                                tiled over bins and scenes (Ryy = Rnn); NULL = 0    */
   int32_t keepHistory;      /* 1: keep w / wExt for every iteration (reference
                                layout needs it for the SNR replay)                  */
+  /* asynchronous clocks (SROs), host-computed from the event order
+   * (fill_buffers / process_incoming_signals_buffers, d_classes.py:1185-1224,
+   * 1701-1807; quirk Q13).  NULL = synchronous schedule.                    */
+  const uint8_t* zLag;      /* [R*K*K] 1: node k's update r consumes sender q's
+                               fused frame of round r-1 instead of round r      */
+  const double* zPhase;     /* [R*K*K] SRO phase-compensation offset phi (samples)
+                               of sender q's channel at node k's update r:
+                               yhat *= exp(-j 2 pi f phi / N) (compensate_sros,
+                               d_classes.py:1936-2046); NULL = no compensation  */
 } danse_cfg;
 
 typedef struct danse_engine danse_engine;
@@ -143,8 +152,10 @@ int danse_engine_bcast(danse_engine* eng, int32_t r, void* stream);
 int danse_engine_update(danse_engine* eng, int32_t r, void* stream);
 int danse_engine_finish(danse_engine* eng, void* stream);   /* synthesis of the last round */
 
-/* Device pointer + byte size of the fused-signal spectra buffer [K][S][F]
- * complex (node-major, so that a node range is one contiguous block). */
+/* Device pointer + byte size of the fused-signal spectra buffer [2][K][S][F]
+ * complex: round r writes slot r & 1 (node-major within a slot, so that a
+ * node range is one contiguous block); an update may read slot (r-1) & 1
+ * (zLag). */
 int danse_engine_zspec(danse_engine* eng, void** ptr, size_t* bytes);
 /* Use a caller-owned buffer (same size and layout) for the fused spectra,
  * e.g. a torch tensor that an RCCL all-gather fills in place. */

@@ -8,6 +8,8 @@ from danse_amd.scene import make_scene
 
 
 def make_case_params(case, SROperNode=None):
+    if SROperNode is None:
+        SROperNode = case.get('sros')
     dp = P.DANSEparameters(**case['danse'])
     wp = P.WASNparameters(trueRoom=False, signalType='random', nSensorPerNode=list(case['M']),
                           SROperNode=np.zeros(len(case['M'])) if SROperNode is None else np.asarray(SROperNode),
@@ -19,6 +21,8 @@ def make_case_params(case, SROperNode=None):
 
 
 def make_case_scene(case, **kw):
+    if 'sros' in case and 'SROperNode' not in kw:
+        kw['SROperNode'] = case['sros']
     return make_scene(case['M'], sigDur=case['dur'], seed=case.get('seed', 0), **kw)
 
 

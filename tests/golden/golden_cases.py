@@ -41,6 +41,13 @@ ONLINE_CASES = [
          danse=_d(SANDBOX, nodeUpdating='seq', performGEVD=False)),
     dict(name='online_mwf_asy_nobasis', M=[2, 2, 2], dur=2.0, seed=5,
          danse=_d(BATTERY, nodeUpdating='asy', performGEVD=False, use1stFrameAsBasis=False)),
+    # config C shape (fewer nodes): SROs, Oracle SRO estimates, phase compensation with
+    # full-sample-drift flags (d_classes.py:1936-2046, 2364-2621; quirks Q3, Q5, Q13)
+    dict(name='online_C_sro_comp_asy', M=[2, 3, 2], dur=3.0, seed=8, sros=[0, 100, 200],
+         danse=_d(BATTERY, nodeUpdating='asy', compensateSROs=True, includeFSDflags=True, estimateSROs='Oracle',
+                  computeLocal=True)),
+    dict(name='online_C_sro_noflags_seq', M=[2, 2, 2, 2], dur=3.0, seed=9, sros=[50, 0, 200, 120],
+         danse=_d(BATTERY, nodeUpdating='seq', compensateSROs=True, includeFSDflags=False, estimateSROs='Oracle')),
 ]
 
 BATCH_CASES = [

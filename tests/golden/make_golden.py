@@ -26,8 +26,11 @@ from golden_cases import ONLINE_CASES, BATCH_CASES, SRO_EVENT_CASES, KAT_CASES, 
 
 
 def _run_online(ns, case):
-    sc = make_scene(case['M'], sigDur=case['dur'], seed=case['seed'])
+    sros = case.get('sros')
+    sc = make_scene(case['M'], sigDur=case['dur'], seed=case['seed'], SROperNode=sros)
     p = H.make_params(ns, case['M'], **case['danse'])
+    if sros is not None:
+        p.wasnParams.SROperNode = np.array(sros, dtype=float)
     w = H.to_ref_wasn(ns, sc)
     p, w = H.prep(ns, p, w)
     t0 = time.time()

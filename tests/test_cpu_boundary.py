@@ -69,7 +69,12 @@ def test_round_tables_sync_schedule():
     assert np.array_equal(np.argmax(rt.doSolve, axis=1), np.arange(rt.nRounds) % 3)
 
 
-def test_compile_rounds_rejects_sro_schedule():
+def test_round_tables_sro_schedule():
+    """SRO clocks (quirk Q13): node 2 (fastest) updates before node 1 before
+    node 0 at every round, so a faster receiver consumes a slower sender's
+    frame of the previous round (lag 1); the first update sees an empty
+    buffer (flag -N) from a lagging sender and Ns of N samples otherwise
+    (flag -Ns, quirk Q5); later buffers hold exactly Ns (flag 0)."""
     from danse_amd.scene import make_scene
     from danse_amd.scheduler import initialize_events, compile_rounds
     from _util import make_case_params
@@ -78,8 +83,29 @@ def test_compile_rounds_rejects_sro_schedule():
     sc = make_scene([1, 1, 1], sigDur=2.0, seed=0, SROperNode=[0, 100, 200])
     ev, fs = initialize_events([n.timeStamps for n in sc.wasn], [n.fs for n in sc.wasn], dp,
                                [n.neighborsIdx for n in sc.wasn])
+    rt = compile_rounds(ev, fs, dp, 3)
+    assert not rt.synchronous
+    lag = np.array([[0, 0, 0], [1, 0, 0], [1, 1, 0]])
+    assert all(np.array_equal(rt.zLag[r], lag) for r in range(rt.nRounds))
+    assert np.array_equal(rt.flags[0], np.array([[0, -512, -512], [-1024, 0, -512], [-1024, -1024, 0]]))
+    assert not np.any(rt.flags[1:])
+    # frame ends: floor(t * fs_k) on each node's own clock (quirk Q3)
+    assert np.all(np.abs(rt.bcEnd - (np.arange(2, 2 + rt.nRounds) * 512)[:, None]) <= 1)
+    assert np.array_equal(rt.upEnd, rt.bcEnd - 512)
+
+
+def test_compile_rounds_rejects_few_samples():
+    from danse_amd.scene import make_scene
+    from danse_amd.scheduler import initialize_events, compile_rounds
+    from _util import make_case_params
+    case = dict(M=[1, 1], danse=dict(simType='online', nodeUpdating='seq', broadcastType='fewSamples',
+                                     broadcastLength=8))
+    dp, wp = make_case_params(case)
+    sc = make_scene([1, 1], sigDur=1.0, seed=0)
+    ev, fs = initialize_events([n.timeStamps for n in sc.wasn], [n.fs for n in sc.wasn], dp,
+                               [n.neighborsIdx for n in sc.wasn])
     with pytest.raises(NotImplementedError):
-        compile_rounds(ev, fs, dp, 3)
+        compile_rounds(ev, fs, dp, 2)
 
 
 def test_yaml_config_loads():
