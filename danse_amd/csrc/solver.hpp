@@ -25,7 +25,7 @@
 // which equals the reference's W = X diag(1-1/s) X^{-1}, w = W[:, ref] with
 // X^H Rnn X = I (scipy.linalg.eigh(Ryy, Rnn), descending order).
 //
-// MWF path: w = Ryy^{-1}(Ryy - Rnn) e_ref = e_ref - L^{-H} L^{-1} Rnn e_ref
+// MWF path: w = Ryy^{-1}(Ryy - Rnn) e_ref = L^{-H} L^{-1} (Ryy - Rnn) e_ref
 // with Ryy = L L^H.
 #pragma once
 #include <type_traits>
@@ -438,21 +438,23 @@ DANSE_DEV cf gevd_filter(cf (&A)[DMAX], cf (&B)[DMAX], SolverLDS<DMAX>& S, int l
 }
 
 // MWF filter: A = Ryy rows, B = Rnn rows (rows of lanes >= D zero).  Returns w_li.
+// w = Ryy^{-1} (Ryy - Rnn) e_ref: the difference column is formed first, as
+// the reference does (np.linalg.inv(Ryy) @ (Ryy - Rnn)), which keeps the
+// speech-dominated cancellation out of the solve.
 template <int G, int DMAX>
 DANSE_DEV cf mwf_filter(cf (&A)[DMAX], const cf (&B)[DMAX], SolverLDS<DMAX>& S, int li, int D, int ref, bool& ok) {
   const bool act = li < D;
-  pad_identity<DMAX>(A, li, D);
-  float invd;
-  ok = chol_rows<G, DMAX>(A, li, invd);
   cf r = cf{0.0f, 0.0f};
   sfor<0, DMAX>([&](auto cc) {
     constexpr int c = decltype(cc)::value;
-    if (c == ref) r = B[c];
+    if (c == ref) r = A[c] - B[c];
   });
+  pad_identity<DMAX>(A, li, D);
+  float invd;
+  ok = chol_rows<G, DMAX>(A, li, invd);
   cf t = fwd_vec<G, DMAX>(r, A, invd, li);
   herm_transpose<G, DMAX>(A, S.U, li);        // columns of L
-  cf u = bwd_vec_h<G, DMAX>(t, A, invd, li);
-  cf w = cf{(li == ref) ? 1.0f : 0.0f, 0.0f} - u;
+  cf w = bwd_vec_h<G, DMAX>(t, A, invd, li);
   return act ? w : cf{0.0f, 0.0f};
 }
 

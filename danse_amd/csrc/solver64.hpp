@@ -411,13 +411,12 @@ DANSE_DEV cf gevd_filter(Row<DMAX>& A, Row<DMAX>& B, LDS<DMAX>& S, int li, int D
 template <int DMAX>
 DANSE_DEV cf mwf_filter(Row<DMAX>& A, const Row<DMAX>& B, LDS<DMAX>& S, int li, int D, int ref, bool& ok) {
   const bool act = li < D;
+  const cf r = rget(A, ref) - rget(B, ref);   // (Ryy - Rnn)[li][ref], as the reference forms it
   float invd;
   ok = chol<DMAX>(A, S.U, li, D, invd);
-  const cf r = rget(B, ref);    // Rnn[li][ref]
   const cf t = fwd_vec<DMAX>(r, A, invd, li, D);
   herm_transpose<DMAX>(A, S.U, li);
-  const cf u = bwd_vec_h<DMAX>(t, A, invd, li, D);
-  const cf w = cf{(li == ref) ? 1.0f : 0.0f, 0.0f} - u;
+  const cf w = bwd_vec_h<DMAX>(t, A, invd, li, D);
   return act ? w : cf{0.0f, 0.0f};
 }
 
