@@ -2,7 +2,7 @@
 
 ``hipcc -c -fPIC`` of ``csrc/danse_engine.hip`` (host engine, C-ABI, bcast /
 operator kernels) and of ``csrc/update_class.hip`` once per filter-size class
-(``-DDANSE_DMAX=N``, N = 2..16 and 24..64 in steps of 8, see
+(``-DDANSE_DMAX=N``, N = 1..16 and 24..64 in steps of 8, see
 ``csrc/classes.hpp``), in parallel, then one
 ``hipcc -shared`` link.  Objects go to ``danse_amd/_obj/``; the library sits
 next to this file so that it travels with the repository snapshot to the GPU
@@ -21,7 +21,7 @@ CSRC = HERE / 'csrc'
 OBJ = HERE / '_obj'
 OUT = HERE / 'libdanse_mi355x.so'
 INC = HERE.parent / 'include'
-CLASSES = list(range(2, 17)) + [24, 32, 40, 48, 56, 64]
+CLASSES = list(range(1, 17)) + [24, 32, 40, 48, 56, 64]
 FLAGS = ['--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC']
 
 

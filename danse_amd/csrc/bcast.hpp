@@ -2,11 +2,28 @@
 // for the round structure): WOLA analysis, compression z = wExt^H y, WOLA
 // synthesis of z and of the estimates, and the analysis of the z frame that
 // every receiving node uses.  Host translation unit only (danse_engine.hip).
+//
+// One 256-thread workgroup per (scene, node); every 1024-point FFT is owned
+// by ONE wavefront (wfft.hpp), so the four waves run independent transforms
+// side by side:
+//   phase 1  the broadcast-frame analyses of the node's M mics (and the
+//            update-frame analyses when the update frame is not the previous
+//            broadcast frame), round-robin over the waves; each wave keeps
+//            its partial sum of conj(wExt) yhat in registers;
+//   phase 2  wave 0: fused spectrum = sum of the partials (fixed order),
+//            z synthesis + OLA normalisation (d_base.py:1759-1868), stream
+//            append (fill_buffers, d_classes.py:1185-1224) and the analysis of
+//            the z frame the receivers consume (d_classes.py:1701-1807,
+//            1893-1934); waves 1..3: synthesis of the previous round's
+//            estimates (get_desired_sig_chunk, d_base.py:2027-2084).
 #pragma once
 #include "fft.hpp"
 #include "kernels.hpp"
+#include "wfft.hpp"
 
 namespace danse {
+
+constexpr int kBcWaves = 4;
 
 struct BcastArgs {
   int S, K, MT, T, N, Ns, F, R;
@@ -37,6 +54,7 @@ struct BcastArgs {
 };
 
 // y[(frame end - N) .. frame end) * win, zero before sample 0 -> buf (complex, imag 0)
+// (workgroup-cooperative form, used by the stand-alone analysis operator)
 DANSE_DEV void load_frame(cf* buf, const float* __restrict__ x, int end, int N, int T,
                           const float* __restrict__ win) {
   for (int n = threadIdx.x; n < N; n += blockDim.x) {
@@ -46,131 +64,165 @@ DANSE_DEV void load_frame(cf* buf, const float* __restrict__ x, int end, int N, 
   }
 }
 
+// The same frame in the wave-FFT input layout (lane l: samples l + 64 j).
+DANSE_DEV void load_frame_wave(cf (&v)[16], const float* __restrict__ x, int end, int T,
+                               const float* __restrict__ win) {
+  const int l = __lane_id();
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int n = l + 64 * j;
+    const int idx = end - 1024 + n;
+    const float s = (idx >= 0 && idx < T) ? x[idx] : 0.0f;
+    v[j] = cf{s * win[n], 0.0f};
+  }
+}
+
+// sqrt(Ns) * real(ifft(Hermitian extension of X[0..F))) through a forward
+// FFT of the conjugate: input element n of the wave layout.
+DANSE_DEV cf herm_ext_conj(const cf* __restrict__ X, int n, int F) {
+  return (n < F) ? conjg(X[n]) : X[1024 - n];
+}
+
 __global__ void __launch_bounds__(256) bcast_kernel(const BcastArgs a) {
-  __shared__ cf b0[1024];
-  __shared__ cf b1[1024];
-  __shared__ cf zacc[513];
+  __shared__ cf fftLds[kBcWaves][wfft::kLdsElems];
+  __shared__ cf part[kBcWaves][513];
   __shared__ float zq[1024];
-  __shared__ int anyNZ;
-  const int tid = threadIdx.x;
+  const int wv = threadIdx.x >> 6;
   const int N = a.N, Ns = a.Ns, F = a.F;
   const int nOwn = a.k1 - a.k0;
   const int s = blockIdx.x / nOwn;
   const int k = a.k0 + blockIdx.x % nOwn;
   const float sqNs = sqrtf((float)Ns);
   const float invSqNs = 1.0f / sqNs;
+  const float sc = sqNs / (float)N;
   const int r = a.r;
+  cf* L = fftLds[wv];
 
-  // ---- synthesis of the estimates of round r-1, all families
+  // ---- phase 1: analyses, per-wave partial fused spectra
+  if (a.doBcast) {
+    const int Mk = a.M[k];
+    const int bEnd = a.bcEnd[r * a.K + k];
+    const int uEnd = a.upEnd[r * a.K + k];
+    const bool needUp = (r == 0) || (uEnd != a.bcEnd[(r - 1) * a.K + k]);
+    const cf* wx = a.wExtHist + (long long)s * a.wExtStride + a.wExtNodeOff[k] +
+                   (a.wExtHistory ? (long long)r * F * Mk : 0);
+    cf zp[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) zp[c] = cf{0.0f, 0.0f};
+    const int nJobs = needUp ? 2 * Mk : Mk;
+    for (int j = wv; j < nJobs; j += kBcWaves) {
+      const bool up = j >= Mk;
+      const int m = up ? j - Mk : j;
+      const int ch = a.base[k] + m;
+      cf v[16];
+      load_frame_wave(v, a.y + ((long long)s * a.MT + ch) * a.T, up ? uEnd : bEnd, a.T, a.hA);
+      wfft::fft1024(v, L, a.tw);
+      cf* dst = a.Yspec + (((long long)((up ? r + 1 : r) & 1) * a.S + s) * a.MT + ch) * F;
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        const int f = wfft::out_index(c);
+        if (f < F) {
+          const cf Y = invSqNs * v[c];
+          dst[f] = Y;
+          if (!up) zp[c] = zp[c] + cmul(wx[(long long)f * Mk + m], Y);
+        }
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      const int f = wfft::out_index(c);
+      if (f < F) part[wv][f] = zp[c];
+    }
+  }
+  __syncthreads();
+
+  if (a.doBcast && wv == 0) {
+    // ---- z synthesis: sqrt(Ns) * real(ifft(herm-ext(zhat))) * f, OLA with the previous frame
+    const int l = __lane_id();
+    cf v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int n = l + 64 * j;
+      const int nn = (n < F) ? n : N - n;
+      cf z = part[0][nn];
+#pragma unroll
+      for (int w = 1; w < kBcWaves; ++w) z = z + part[w][nn];
+      if (nn == 0 || nn == F - 1) z.im = 0.0f;
+      v[j] = (n < F) ? conjg(z) : z;
+    }
+    wfft::fft1024(v, L, a.tw);
+    float* zpv = a.zPrev + ((long long)s * a.K + k) * N;
+    bool nz = false;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) nz = nz || (zpv[l + 64 * j] != 0.0f);
+    const bool prevNZ = __ballot(nz) != 0ull;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      const int n = wfft::out_index(c);
+      float zc = sc * v[c].re * a.hS[n];
+      if (prevNZ) {
+        float t = (n < N - Ns) ? zpv[n + Ns] : 0.0f;
+        t += zc;
+        if (n < Ns) t = t / a.normVal[n];
+        zc = t;
+      }
+      zq[n] = zc;
+    }
+    wfft::wave_sync();
+    float* zs = a.zStream + ((long long)s * a.K + k) * ((long long)a.R * Ns);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int n = l + 64 * j;
+      zpv[n] = zq[n];
+      if (n < Ns) zs[(long long)r * Ns + n] = zq[n];
+    }
+    // ---- z frame the receivers consume at round r: stream samples [(r+1)Ns - N, (r+1)Ns)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int n = l + 64 * j;
+      const long long idx = (long long)(r + 1) * Ns - N + n;
+      float t;
+      if (idx < 0) t = 0.0f;
+      else if (idx >= (long long)r * Ns) t = zq[idx - (long long)r * Ns];
+      else t = zs[idx];
+      v[j] = cf{t * a.hA[n], 0.0f};
+    }
+    wfft::fft1024(v, L, a.tw);
+    cf* Zs = a.Zspec + (((long long)(r & 1) * a.K + k) * a.S + s) * F;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      const int f = wfft::out_index(c);
+      if (f < F) Zs[f] = invSqNs * v[c];
+    }
+  }
+
+  // ---- synthesis of the estimates of round r-1, one family per wave
   if (a.doSynth) {
     const int rp = r - 1;
     const int end = a.upEnd[rp * a.K + k];
+    const int w0 = a.doBcast ? 1 : 0;
+    const int nW = kBcWaves - w0;
+    int job = 0;
     for (int fam = 0; fam < kMaxFam; ++fam) {
       if (!((a.families >> fam) & 1)) continue;
-      const cf* dh = a.dhat + ((((long long)fam * a.S + s) * a.K + k) * a.R + rp) * F;
-      // forward FFT of conj(Hermitian extension) gives N * conj(ifft); real part is what we need
-      for (int n = tid; n < N; n += blockDim.x) {
-        cf X;
-        if (n < F) X = conjg(dh[n]);
-        else X = dh[N - n];
-        b0[n] = X;
+      if (wv == w0 + (job % nW)) {
+        const cf* dh = a.dhat + ((((long long)fam * a.S + s) * a.K + k) * a.R + rp) * F;
+        const int l = __lane_id();
+        cf v[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v[j] = herm_ext_conj(dh, l + 64 * j, F);
+        wfft::fft1024(v, L, a.tw);
+        float* dd = a.d + (((long long)fam * a.S + s) * a.K + k) * a.T;
+#pragma unroll
+        for (int c = 0; c < 16; ++c) {
+          const int n = wfft::out_index(c);
+          const int idx = end - N + n;
+          if (idx >= 0 && idx < a.T) dd[idx] += sc * a.hS[n] * v[c].re;
+        }
       }
-      __syncthreads();
-      cf* out = fft1024(b0, b1, a.tw);
-      float* dd = a.d + (((long long)fam * a.S + s) * a.K + k) * a.T;
-      const float sc = sqNs / (float)N;
-      for (int n = tid; n < N; n += blockDim.x) {
-        const int idx = end - N + n;
-        if (idx >= 0 && idx < a.T) dd[idx] += sc * a.hS[n] * out[n].re;
-      }
-      __syncthreads();
+      ++job;
     }
   }
-  if (!a.doBcast) return;
-
-  // ---- local analysis + fused spectrum
-  const int Mk = a.M[k];
-  const int bEnd = a.bcEnd[r * a.K + k];
-  const cf* wx = a.wExtHist + (long long)s * a.wExtStride + a.wExtNodeOff[k] +
-                 (a.wExtHistory ? (long long)r * F * Mk : 0);
-  for (int f = tid; f < F; f += blockDim.x) zacc[f] = cf{0.0f, 0.0f};
-  for (int m = 0; m < Mk; ++m) {
-    const int c = a.base[k] + m;
-    const float* x = a.y + ((long long)s * a.MT + c) * a.T;
-    load_frame(b0, x, bEnd, N, a.T, a.hA);
-    __syncthreads();
-    cf* out = fft1024(b0, b1, a.tw);
-    cf* Ys = a.Yspec + (((long long)(r & 1) * a.S + s) * a.MT + c) * F;
-    for (int f = tid; f < F; f += blockDim.x) {
-      const cf Y = invSqNs * out[f];
-      Ys[f] = Y;
-      zacc[f] = zacc[f] + cmul(wx[(long long)f * Mk + m], Y);
-    }
-    __syncthreads();
-    const bool needUp = (r == 0) || (a.upEnd[r * a.K + k] != a.bcEnd[(r - 1) * a.K + k]);
-    if (needUp) {
-      // update-local frame of round r (only when it is not the broadcast frame of r-1)
-      const int uEnd = a.upEnd[r * a.K + k];
-      load_frame(b0, x, uEnd, N, a.T, a.hA);
-      __syncthreads();
-      cf* o2 = fft1024(b0, b1, a.tw);
-      cf* Yu = a.Yspec + (((long long)((r + 1) & 1) * a.S + s) * a.MT + c) * F;
-      for (int f = tid; f < F; f += blockDim.x) Yu[f] = invSqNs * o2[f];
-      __syncthreads();
-    }
-  }
-  // ---- z synthesis: sqrt(Ns) * real(ifft(herm-ext(zhat))) * f
-  for (int n = tid; n < N; n += blockDim.x) {
-    cf X;
-    if (n < F) {
-      X = zacc[n];
-      if (n == 0 || n == F - 1) X.im = 0.0f;
-      X = conjg(X);
-    } else {
-      X = zacc[N - n];
-    }
-    b0[n] = X;
-  }
-  if (tid == 0) anyNZ = 0;
-  __syncthreads();
-  float* zp = a.zPrev + ((long long)s * a.K + k) * N;
-  {
-    int nz = 0;
-    for (int n = tid; n < N; n += blockDim.x) nz |= (zp[n] != 0.0f);
-    if (nz) atomicOr(&anyNZ, 1);
-  }
-  cf* out = fft1024(b0, b1, a.tw);
-  const float sc = sqNs / (float)N;
-  const bool prevNZ = anyNZ != 0;
-  for (int n = tid; n < N; n += blockDim.x) {
-    float zc = sc * out[n].re * a.hS[n];
-    if (prevNZ) {
-      float v = (n < N - Ns) ? zp[n + Ns] : 0.0f;
-      v += zc;
-      if (n < Ns) v = v / a.normVal[n];
-      zc = v;
-    }
-    zq[n] = zc;
-  }
-  __syncthreads();
-  float* zs = a.zStream + ((long long)s * a.K + k) * ((long long)a.R * Ns);
-  for (int n = tid; n < N; n += blockDim.x) {
-    zp[n] = zq[n];
-    if (n < Ns) zs[(long long)r * Ns + n] = zq[n];
-  }
-  // ---- z frame the receivers consume at round r: stream samples [(r+1)Ns - N, (r+1)Ns)
-  for (int n = tid; n < N; n += blockDim.x) {
-    const long long idx = (long long)(r + 1) * Ns - N + n;
-    float v;
-    if (idx < 0) v = 0.0f;
-    else if (idx >= (long long)r * Ns) v = zq[idx - (long long)r * Ns];
-    else v = zs[idx];
-    b0[n] = cf{v * a.hA[n], 0.0f};
-  }
-  __syncthreads();
-  out = fft1024(b0, b1, a.tw);
-  cf* Zs = a.Zspec + (((long long)(r & 1) * a.K + k) * a.S + s) * F;
-  for (int f = tid; f < F; f += blockDim.x) Zs[f] = invSqNs * out[f];
 }
 
 }  // namespace danse

@@ -1,23 +1,25 @@
-// Size classes of the update / filter kernels.  Every filter dimension
-// D in [1, 16] gets its own compile-time DMAX (= D, D = 1 padded to 2) so the
-// unrolled lane-group solver does no padded work; D <= 4 runs 16 bins per
-// wavefront (G = 4 lanes per bin), larger D 4 bins (G = 16).  Each class is a
-// separate translation unit (update_class.hip compiled with -DDANSE_DMAX=N)
-// so the build parallelises; the engine dispatches by DMAX at launch time.
+// Size classes of the update / filter kernels, one translation unit each
+// (update_class.hip compiled with -DDANSE_DMAX=N, so the build parallelises;
+// the engine dispatches by DMAX at launch time):
+//   D <= kLaneMaxD   one bin per LANE, packed-triangle SCMs (solver1.hpp)
+//   D in 13..16      lane groups of G = 16, one row per lane (solver.hpp)
+//   D in 17..64      one bin per wavefront, runtime pivot loops (solver64.hpp),
+//                    DMAX = D rounded up to a multiple of 8
 #pragma once
 #include "kernels.hpp"
 
 namespace danse {
 
 constexpr int kMaxDMax = 64;
-// D <= 16: exact classes (lane groups, solver.hpp); larger D rounds up to a
-// multiple of 8 and runs one bin per wavefront with runtime pivot loops over
-// the actual D (G = 64, solver64.hpp).
-constexpr int class_dmax(int D) { return D < 2 ? 2 : D <= 16 ? D : ((D + 7) / 8) * 8; }
-constexpr int class_group(int DMAX) { return DMAX <= 4 ? 4 : (DMAX <= 16 ? 16 : 64); }
+constexpr int kLaneMaxD = 12;
+constexpr int class_dmax(int D) { return D <= 16 ? D : ((D + 7) / 8) * 8; }
+constexpr int class_group(int DMAX) { return DMAX <= kLaneMaxD ? 1 : (DMAX <= 16 ? 16 : 64); }
+// SCM storage of a class: packed lower triangle, bin-minor ([D(D+1)/2][F])
+// for the lane kernels; full rows ([F][D][D]) otherwise.
+constexpr bool class_packed(int D) { return D <= kLaneMaxD; }
 
 #define DANSE_FOR_EACH_CLASS(X) \
-  X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16) X(24) X(32) X(40) \
+  X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16) X(24) X(32) X(40) \
   X(48) X(56) X(64)
 
 #define DANSE_DECLARE_CLASS(N)                                                                      \

@@ -91,6 +91,7 @@ static void pick_class(int D, int& G, int& DMAX) {
   DMAX = class_dmax(D);
   G = class_group(DMAX);
 }
+// (G = 1: lane kernels on packed SCMs; 16: lane groups; 64: one bin per wave)
 
 // Re-initialise filters (slot 0 of the histories) and SCMs of every
 // (scene, family-node): one block row per (scene, family-node).
@@ -101,10 +102,21 @@ __global__ void reset_fam_kernel(const FamNode* fns, int nFN, const long long* w
   const int i = blockIdx.y % nFN;
   const FamNode fn = fns[i];
   const int D = fn.D;
-  const long long nS = (long long)F * D * D;
+  const long long nS = fn.packed ? (long long)F * D * (D + 1) / 2 : (long long)F * D * D;
   const long long nW = (long long)F * D;
   for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < nS; e += (long long)gridDim.x * blockDim.x) {
-    const cf v = scm0[scmOff[i] + e % ((long long)D * D)];
+    long long src;
+    if (fn.packed) {
+      // packed entry t = i (i + 1) / 2 + j of bin e % F -> full slice element (i, j)
+      const int t = (int)(e / F);
+      int r = (int)((sqrtf(8.0f * (float)t + 1.0f) - 1.0f) * 0.5f);
+      while (r * (r + 1) / 2 > t) --r;
+      while ((r + 1) * (r + 2) / 2 <= t) ++r;
+      src = (long long)r * D + (t - r * (r + 1) / 2);
+    } else {
+      src = e % ((long long)D * D);
+    }
+    const cf v = scm0[scmOff[i] + src];
     Ryy[s * scmStride + fn.scmOff + e] = v;
     Rnn[s * scmStride + fn.scmOff + e] = v;
     if (e < nW) wHist[s * wStride + fn.wOff + e] = w0[w0Off[i] + e];
@@ -204,7 +216,8 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
       if (fn.D > kMaxDMax) return fail(eng, "filter dimension > 64 not supported");
       if (c->gevd && c->rank > fn.D) return fail(eng, "GEVD rank larger than a filter dimension");
       fn.scmOff = scmOff;
-      scmOff += (long long)F * fn.D * fn.D;
+      fn.packed = class_packed(fn.D) ? 1 : 0;
+      scmOff += fn.packed ? (long long)F * fn.D * (fn.D + 1) / 2 : (long long)F * fn.D * fn.D;
       fn.wOff = wOff;
       wOff += histW * F * fn.D;
       eng->fns.push_back(fn);

@@ -30,7 +30,7 @@ struct FamNode {
   int chanOff;        // offset into chanList
   int extMode;        // DANSE family only (else -1)
   int M;              // local mics of node k
-  int pad;
+  int packed;         // SCM layout: 1 packed lower triangle [D(D+1)/2][F], 0 rows [F][D][D]
   long long scmOff;   // complex-element offset within one scene's SCM block
   long long wOff;     // complex-element offset within one scene's w-history block
   long long wExtOff;  // DANSE only: offset within one scene's wExt-history block

@@ -2,9 +2,10 @@
 // once per DMAX with -DDANSE_DMAX=N.
 #include "classes.hpp"
 #include "kernels_big.hpp"
+#include "kernels_lane.hpp"
 
 #ifndef DANSE_DMAX
-#error "compile with -DDANSE_DMAX=<2..16>"
+#error "compile with -DDANSE_DMAX=<1..16, 24..64 step 8>"
 #endif
 
 namespace danse {
@@ -12,43 +13,58 @@ namespace danse {
 namespace {
 constexpr int kD = DANSE_DMAX;
 constexpr int kG = class_group(kD);
-constexpr int kNB = 64 / kG;
-static_assert(kD >= 2 && kD <= kMaxDMax, "class out of range");
+static_assert(kD >= 1 && kD <= kMaxDMax, "class out of range");
 }  // namespace
 
 #define DANSE_CAT2(a, b) a##b
 #define DANSE_CAT(a, b) DANSE_CAT2(a, b)
 
 void DANSE_CAT(launch_update_d, DANSE_DMAX)(const UpdateArgs& a, hipStream_t st) {
-  const int nBB = (a.F + kNB - 1) / kNB;
-  const unsigned grid = (unsigned)(a.S * a.nFN * nBB);
-  if constexpr (kG == 64) {
-    if (!a.gevd || a.rank == 1)
-      hipLaunchKernelGGL((update_kernel_big<kD, 1>), dim3(grid), dim3(64), 0, st, a);
-    else
-      hipLaunchKernelGGL((update_kernel_big<kD, kRMax>), dim3(grid), dim3(64), 0, st, a);
+  const bool r1 = !a.gevd || a.rank == 1;
+  if constexpr (kG == 1) {
+    const long long lanes = (long long)a.S * a.nFN * a.F;
+    const unsigned grid = (unsigned)((lanes + 63) / 64);
+    if (!a.gevd) hipLaunchKernelGGL((update_kernel_lane<kD, 1, false>), dim3(grid), dim3(64), 0, st, a);
+    else if (r1) hipLaunchKernelGGL((update_kernel_lane<kD, 1, true>), dim3(grid), dim3(64), 0, st, a);
+    else hipLaunchKernelGGL((update_kernel_lane<kD, kRMax, true>), dim3(grid), dim3(64), 0, st, a);
+  } else if constexpr (kG == 64) {
+    const unsigned grid = (unsigned)(a.S * a.nFN * a.F);
+    if (r1) hipLaunchKernelGGL((update_kernel_big<kD, 1>), dim3(grid), dim3(64), 0, st, a);
+    else hipLaunchKernelGGL((update_kernel_big<kD, kRMax>), dim3(grid), dim3(64), 0, st, a);
   } else {
-    if (!a.gevd || a.rank == 1)
-      hipLaunchKernelGGL((update_kernel<kG, kD, 1>), dim3(grid), dim3(64), 0, st, a);
-    else
-      hipLaunchKernelGGL((update_kernel<kG, kD, kRMax>), dim3(grid), dim3(64), 0, st, a);
+    constexpr int kNB = 64 / kG;
+    const int nBB = (a.F + kNB - 1) / kNB;
+    const unsigned grid = (unsigned)(a.S * a.nFN * nBB);
+    if (r1) hipLaunchKernelGGL((update_kernel<kG, kD, 1>), dim3(grid), dim3(64), 0, st, a);
+    else hipLaunchKernelGGL((update_kernel<kG, kD, kRMax>), dim3(grid), dim3(64), 0, st, a);
   }
 }
 
 void DANSE_CAT(launch_filter_update_d, DANSE_DMAX)(const cf* Ryy, const cf* Rnn, int B, int D, int gevd, int rank,
                                                    int ref, cf* w, int* diag, hipStream_t st) {
-  const unsigned grid = (unsigned)((B + kNB - 1) / kNB);
-  if constexpr (kG == 64) {
-    if (!gevd || rank == 1)
+  const bool r1 = !gevd || rank == 1;
+  if constexpr (kG == 1) {
+    const unsigned grid = (unsigned)((B + 63) / 64);
+    if (r1)
+      hipLaunchKernelGGL((filter_update_kernel_lane<kD, 1>), dim3(grid), dim3(64), 0, st, Ryy, Rnn, B, gevd, rank,
+                         ref, w, diag);
+    else
+      hipLaunchKernelGGL((filter_update_kernel_lane<kD, kRMax>), dim3(grid), dim3(64), 0, st, Ryy, Rnn, B, gevd,
+                         rank, ref, w, diag);
+  } else if constexpr (kG == 64) {
+    const unsigned grid = (unsigned)B;
+    if (r1)
       hipLaunchKernelGGL((filter_update_kernel_big<kD, 1>), dim3(grid), dim3(64), 0, st, Ryy, Rnn, B, D, gevd, rank,
                          ref, w, diag);
     else
       hipLaunchKernelGGL((filter_update_kernel_big<kD, kRMax>), dim3(grid), dim3(64), 0, st, Ryy, Rnn, B, D, gevd,
                          rank, ref, w, diag);
   } else {
-    if (!gevd || rank == 1)
-      hipLaunchKernelGGL((filter_update_kernel<kG, kD, 1>), dim3(grid), dim3(64), 0, st, Ryy, Rnn, B, D, gevd,
-                         rank, ref, w, diag);
+    constexpr int kNB = 64 / kG;
+    const unsigned grid = (unsigned)((B + kNB - 1) / kNB);
+    if (r1)
+      hipLaunchKernelGGL((filter_update_kernel<kG, kD, 1>), dim3(grid), dim3(64), 0, st, Ryy, Rnn, B, D, gevd, rank,
+                         ref, w, diag);
     else
       hipLaunchKernelGGL((filter_update_kernel<kG, kD, kRMax>), dim3(grid), dim3(64), 0, st, Ryy, Rnn, B, D, gevd,
                          rank, ref, w, diag);
