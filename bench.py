@@ -19,8 +19,10 @@ holds S scenes per GPU (weak scaling).  --shard scenes runs independent
 scene replicas (no collective).
 
 Also reported: the roofline of the dominant kernel (update_kernel) from live
-HIP-event timing, and the CPU oracle (a float64 NumPy restatement of the
-reference algorithm, "port") timed on this host on a bounded sample.
+HIP-event timing, its HBM traffic from two rocprofv3 PMC passes
+(FETCH_SIZE x2 + WRITE_SIZE, run as child processes), and the CPU oracle (a
+float64 NumPy restatement of the reference algorithm, "port") timed on this
+host on a bounded sample.
 """
 from __future__ import annotations
 
@@ -78,13 +80,17 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=3)
     ap.add_argument('--warmup', type=int, default=1)
-    ap.add_argument('--scenes', type=int, default=16, help='scenes per GPU')
+    ap.add_argument('--scenes', type=int, default=31,
+                    help='scenes per GPU (31 x 8 nodes x 513 bins = 1988 lane-kernel waves: ~2 full '
+                         'rounds of the 1024 wave slots the update kernel can hold)')
     ap.add_argument('--workload', default='B', choices=sorted(WORKLOADS))
     ap.add_argument('--shard', default='nodes', choices=['nodes', 'scenes'])
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
     ap.add_argument('--no-graph', action='store_true')
+    ap.add_argument('--no-traffic', action='store_true', help='skip the rocprofv3 PMC passes')
     ap.add_argument('--cpu-only', action='store_true', help=argparse.SUPPRESS)
+    ap.add_argument('--pmc-child', action='store_true', help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.cpu_only:
         wl = WORKLOADS[args.workload]
@@ -153,6 +159,13 @@ def main():
             L.check(eng.lib.danse_engine_reset(eng.eng, eng.stream_ptr()), eng.eng)
             eng.run(graph=not args.no_graph)
 
+    if args.pmc_child:
+        # one un-graphed pass for the PMC collector (every kernel its own dispatch)
+        L.check(eng.lib.danse_engine_reset(eng.eng, eng.stream_ptr()), eng.eng)
+        eng.run(graph=False)
+        torch.cuda.synchronize()
+        eng.close()
+        return
     for _ in range(args.warmup):
         one_pass()
     torch.cuda.synchronize()
@@ -204,6 +217,10 @@ def main():
     achieved = float(byts.mean() / (avg_ms * 1e-3) / 1e9)
     diag = eng.diagnostics()
 
+    traffic = None
+    if rank == 0 and world == 1 and not args.no_traffic:
+        traffic = pmc_traffic(args, 'update_kernel')
+
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
         import subprocess
@@ -235,7 +252,9 @@ def main():
             'config': {'workload': wl['desc'], 'scenes_per_gpu': S, 'K': K, 'M': M[0], 'D': D, 'bins': F,
                        'rounds': R, 'shard': shard, 'gevd_rank': 1, 'graph': not args.no_graph},
             'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                         'frac': achieved / HBM_PEAK_GBS, 'traffic': None,
+                         'frac': achieved / HBM_PEAK_GBS,
+                         'traffic': None if traffic is None else traffic['bytes_per_launch'],
+                         'traffic_detail': traffic,
                          'kernel': 'update_kernel', 'avg_launch_ms': avg_ms,
                          'alg_bytes_per_launch': float(byts.mean())},
             'cpu_baseline': cpu,
@@ -246,6 +265,44 @@ def main():
     eng.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def pmc_traffic(args, kernel_substr):
+    """HBM bytes per launch of the dominant kernel from two rocprofv3 PMC
+    passes over the same workload (MI355X_MICROARCH.md, HBM section):
+    FETCH_SIZE and WRITE_SIZE (KiB) in separate passes, FETCH_SIZE doubled
+    (gfx950 reports half the bytes of a wide streaming read)."""
+    import csv
+    import shutil
+    import subprocess
+    import tempfile
+    exe = shutil.which('rocprofv3')
+    if exe is None:
+        return None
+    out = {}
+    tmp = tempfile.mkdtemp(prefix='danse_pmc_')
+    env = dict(os.environ, TMPDIR=os.environ.get('TMPDIR', '/tmp'))
+    for counter in ('FETCH_SIZE', 'WRITE_SIZE'):
+        d = os.path.join(tmp, counter)
+        cmd = [exe, '--pmc', counter, '--kernel-trace', '-d', d, '-o', 'pmc', '--output-format', 'csv', '--',
+               sys.executable, str(ROOT / 'bench.py'), '--pmc-child', '--workload', args.workload,
+               '--scenes', str(args.scenes)]
+        try:
+            subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240, check=True)
+        except Exception as e:   # profiler unavailable or refused: report null, never fail the bench
+            return {'error': f'{counter}: {type(e).__name__}'}
+        files = [os.path.join(r, f) for r, _, fs in os.walk(d) for f in fs if f.endswith('counter_collection.csv')]
+        vals = [float(row['Counter_Value']) * 1024.0 for fn in files for row in csv.DictReader(open(fn))
+                if row['Counter_Name'] == counter and kernel_substr in row['Kernel_Name']]
+        if not vals:
+            return {'error': f'{counter}: no samples'}
+        out[counter] = float(np.mean(vals))
+        out['dispatches'] = len(vals)
+    shutil.rmtree(tmp, ignore_errors=True)
+    b = 2.0 * out['FETCH_SIZE'] + out['WRITE_SIZE']
+    return {'bytes_per_launch': b, 'fetch_bytes_raw': out['FETCH_SIZE'], 'write_bytes': out['WRITE_SIZE'],
+            'dispatches': out['dispatches'], 'method': 'rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, '
+            'FETCH_SIZE x2 (gfx950)'}
 
 
 def ctypes_void(p):

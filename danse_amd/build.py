@@ -33,15 +33,25 @@ def _units():
     return u
 
 
-def _headers():
-    return sorted(CSRC.glob('*.hpp')) + [INC / 'danse_mi355x.h']
+def _deps(src: Path, seen=None) -> set:
+    """The quoted #includes of a source, recursively (per-unit staleness, so a
+    broadcast-kernel edit does not recompile every solver class)."""
+    seen = set() if seen is None else seen
+    for line in src.read_text().splitlines():
+        line = line.strip()
+        if line.startswith('#include "'):
+            dep = (src.parent / line.split('"')[1]).resolve()
+            if dep.exists() and dep not in seen:
+                seen.add(dep)
+                _deps(dep, seen)
+    return seen
 
 
 def _stale(obj: Path, src: Path) -> bool:
     if not obj.exists():
         return True
     t = obj.stat().st_mtime
-    return any(p.stat().st_mtime > t for p in [src] + _headers())
+    return any(p.stat().st_mtime > t for p in [src, *_deps(src)])
 
 
 def up_to_date() -> bool:

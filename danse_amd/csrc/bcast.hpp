@@ -50,7 +50,8 @@ struct BcastArgs {
   const float* hA;         // analysis window [N]
   const float* hS;         // synthesis window [N]
   const float* normVal;    // [Ns] OLA normalisation h^2[n] + h^2[n+Ns]
-  const cf* tw;            // [N] twiddles
+  const cf* tw;            // wave-FFT twiddle table (wfft::kTwElems)
+  int dbg;                 // diagnostic ablation mask (DANSE_BCAST_ABLATE; 0 in production)
 };
 
 // y[(frame end - N) .. frame end) * win, zero before sample 0 -> buf (complex, imag 0)
@@ -99,7 +100,7 @@ __global__ void __launch_bounds__(256) bcast_kernel(const BcastArgs a) {
   cf* L = fftLds[wv];
 
   // ---- phase 1: analyses, per-wave partial fused spectra
-  if (a.doBcast) {
+  if (a.doBcast && !(a.dbg & 1)) {
     const int Mk = a.M[k];
     const int bEnd = a.bcEnd[r * a.K + k];
     const int uEnd = a.upEnd[r * a.K + k];
@@ -115,16 +116,20 @@ __global__ void __launch_bounds__(256) bcast_kernel(const BcastArgs a) {
       const int m = up ? j - Mk : j;
       const int ch = a.base[k] + m;
       cf v[16];
-      load_frame_wave(v, a.y + ((long long)s * a.MT + ch) * a.T, up ? uEnd : bEnd, a.T, a.hA);
-      wfft::fft1024(v, L, a.tw);
+      if (a.dbg & 8) {
+        for (int jj = 0; jj < 16; ++jj) v[jj] = cf{(float)(jj + threadIdx.x), 0.0f};
+      } else {
+        load_frame_wave(v, a.y + ((long long)s * a.MT + ch) * a.T, up ? uEnd : bEnd, a.T, a.hA);
+      }
+      if (!(a.dbg & 64)) wfft::fft1024(v, L, a.tw);
       cf* dst = a.Yspec + (((long long)((up ? r + 1 : r) & 1) * a.S + s) * a.MT + ch) * F;
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
         const int f = wfft::out_index(c);
         if (f < F) {
           const cf Y = invSqNs * v[c];
-          dst[f] = Y;
-          if (!up) zp[c] = zp[c] + cmul(wx[(long long)f * Mk + m], Y);
+          if (!(a.dbg & 32)) dst[f] = Y;
+          if (!up) zp[c] = zp[c] + ((a.dbg & 16) ? Y : cmul(wx[(long long)f * Mk + m], Y));
         }
       }
     }
@@ -136,7 +141,7 @@ __global__ void __launch_bounds__(256) bcast_kernel(const BcastArgs a) {
   }
   __syncthreads();
 
-  if (a.doBcast && wv == 0) {
+  if (a.doBcast && wv == 0 && !(a.dbg & 2)) {
     // ---- z synthesis: sqrt(Ns) * real(ifft(herm-ext(zhat))) * f, OLA with the previous frame
     const int l = __lane_id();
     cf v[16];
@@ -197,7 +202,7 @@ __global__ void __launch_bounds__(256) bcast_kernel(const BcastArgs a) {
   }
 
   // ---- synthesis of the estimates of round r-1, one family per wave
-  if (a.doSynth) {
+  if (a.doSynth && !(a.dbg & 4)) {
     const int rp = r - 1;
     const int end = a.upEnd[rp * a.K + k];
     const int w0 = a.doBcast ? 1 : 0;

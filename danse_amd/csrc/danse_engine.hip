@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -61,6 +62,7 @@ struct danse_engine {
   int graphR0 = -1, graphR1 = -1;
   void* graphStream = nullptr;
   bool ownZspec = true;
+  int bcastAblate = 0;   // DANSE_BCAST_ABLATE (diagnostics only; results are wrong when set)
   // initial-state copies for danse_engine_reset
   std::vector<long long> initW0Off, initScmOff, extSrcOff, tgtOff;
   cf *dW0 = nullptr, *dScm0 = nullptr, *dExt0 = nullptr, *dTgt0 = nullptr;
@@ -174,6 +176,7 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
   if (c->rank < 1 || c->rank > kRMax) return fail(nullptr, "GEVD rank out of range [1, 4]");
   eng = new danse_engine();
   eng->dev = device;
+  if (const char* ab = std::getenv("DANSE_BCAST_ABLATE")) eng->bcastAblate = std::atoi(ab);
   HIPCHK(hipSetDevice(device));
   eng->S = c->S; eng->K = c->K; eng->N = c->N; eng->Ns = c->Ns; eng->F = c->N / 2 + 1; eng->T = c->T;
   eng->R = c->R; eng->k0 = c->k0; eng->k1 = c->k1; eng->gevd = c->gevd; eng->rank = c->rank; eng->ref = c->ref;
@@ -261,7 +264,7 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
   HIPCHK(dalloc(&eng->dhA, (size_t)c->N));
   HIPCHK(dalloc(&eng->dhS, (size_t)c->N));
   HIPCHK(dalloc(&eng->dNorm, (size_t)c->Ns));
-  HIPCHK(dalloc(&eng->dTw, (size_t)c->N));
+  HIPCHK(dalloc(&eng->dTw, (size_t)c->N + wfft::kTwElems));
   HIPCHK(dalloc(&eng->dWExtNodeOff, (size_t)K));
   HIPCHK(hipMemcpy(eng->dM, eng->M.data(), K * sizeof(int), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(eng->dBase, eng->base.data(), K * sizeof(int), hipMemcpyHostToDevice));
@@ -296,7 +299,18 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
       const double ang = -2.0 * M_PI * (double)m / (double)c->N;
       tw[m] = cf{(float)std::cos(ang), (float)std::sin(ang)};
     }
-    HIPCHK(hipMemcpy(eng->dTw, tw.data(), c->N * sizeof(cf), hipMemcpyHostToDevice));
+    // [0, N): exp(-2 pi i m / N) (workgroup FFT); then the wave-FFT table
+    for (int k1 = 0; k1 < 16; ++k1)
+      for (int l = 0; l < 64; ++l) {
+        const double ang = -2.0 * M_PI * (double)(l * k1) / 1024.0;
+        tw.push_back(cf{(float)std::cos(ang), (float)std::sin(ang)});
+      }
+    for (int a4 = 0; a4 < 4; ++a4)
+      for (int cc = 0; cc < 16; ++cc) {
+        const double ang = -2.0 * M_PI * (double)(a4 * cc) / 64.0;
+        tw.push_back(cf{(float)std::cos(ang), (float)std::sin(ang)});
+      }
+    HIPCHK(hipMemcpy(eng->dTw, tw.data(), tw.size() * sizeof(cf), hipMemcpyHostToDevice));
   }
   for (auto& cl : eng->classes) {
     HIPCHK(dalloc(&cl.dev, cl.host.size()));
@@ -431,7 +445,8 @@ static BcastArgs make_bcast(danse_engine* e, int r, int synth, int bc) {
   a.Yspec = e->Yspec; a.Zspec = e->Zspec; a.zPrev = e->zPrev; a.zStream = e->zStream;
   a.wExtHist = e->wExtHist; a.wExtNodeOff = e->dWExtNodeOff; a.wExtStride = e->wExtStride;
   a.wExtHistory = e->keepHistory; a.dhat = e->dhat; a.d = e->d; a.hA = e->dhA; a.hS = e->dhS; a.normVal = e->dNorm;
-  a.tw = e->dTw;
+  a.tw = e->dTw + e->N;
+  a.dbg = e->bcastAblate;
   return a;
 }
 

@@ -88,14 +88,19 @@ DANSE_DEV void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Twiddle table of the wave FFT (kTwElems complex, built in double on the
+// host at engine creation): [k1][l] = W1024^(l k1) (16 x 64, so every load of
+// a wave is 512 contiguous bytes), then [a][c] = W64^(a c) (4 x 16).
+constexpr int kTwElems = 16 * 64 + 4 * 16;
+
 // Forward FFT of the wave's 1024 points (layout above).  lds: this wave's
-// kLdsElems-complex scratch.  tw: exp(-2 pi i m / 1024), m = 0..1023.
+// kLdsElems-complex scratch.  tw: the kTwElems table above.
 DANSE_DEV void fft1024(cf (&v)[16], cf* lds, const cf* __restrict__ tw) {
   const int l = __lane_id();
   // A: DFT over j, twiddle W1024^(l k1)
   dft16(v);
 #pragma unroll
-  for (int k1 = 1; k1 < 16; ++k1) v[k1] = v[k1] * tw[l * k1];
+  for (int k1 = 1; k1 < 16; ++k1) v[k1] = v[k1] * tw[k1 * 64 + l];
   wave_sync();   // the previous FFT's reads of lds are done
 #pragma unroll
   for (int k1 = 0; k1 < 16; ++k1) lds[k1 * kPitch + l] = v[k1];
@@ -106,7 +111,7 @@ DANSE_DEV void fft1024(cf (&v)[16], cf* lds, const cf* __restrict__ tw) {
   for (int b = 0; b < 16; ++b) v[b] = lds[k1 * kPitch + 4 * b + a];
   dft16(v);
 #pragma unroll
-  for (int c = 1; c < 16; ++c) v[c] = v[c] * tw[16 * a * c];
+  for (int c = 1; c < 16; ++c) v[c] = v[c] * tw[16 * 64 + a * 16 + c];
   // C: 4-point DFT over a across the quad.  Stage 1 pairs a, a ^ 2
   // (a1 = a >> 1 becomes e0, twiddle W4^(a0 e0)), stage 2 pairs a, a ^ 1
   // (a0 becomes e1).
