@@ -43,6 +43,22 @@ class DanseCfg(ctypes.Structure):
     ]
 
 
+class DanseBatchCfg(ctypes.Structure):
+    _fields_ = [
+        ('S', _c_i32), ('K', _c_i32), ('M', _p_i32),
+        ('N', _c_i32), ('Ns', _c_i32), ('T', _c_i32),
+        ('iters', _c_i32), ('nseg', _c_i32),
+        ('gevd', _c_i32), ('rank', _c_i32), ('ref', _c_i32),
+        ('alphaExt', ctypes.c_float),
+        ('extMode', _p_i32), ('betaExt', _p_f32), ('win', _p_f32),
+        ('vad', _p_u8), ('doSolve', _p_u8),
+        ('w0', _p_f32), ('wExt0', _p_f32),
+        ('costTrim', _c_i32),
+    ]
+
+
+BOUT_W, BOUT_WEXT, BOUT_D, BOUT_DHAT, BOUT_COST = 0, 1, 2, 3, 4
+
 # every symbol include/danse_mi355x.h declares, with its ctypes signature
 SIGNATURES = {
     'danse_engine_create': (_c_i32, [ctypes.POINTER(DanseCfg), _c_i32, ctypes.POINTER(ctypes.c_void_p)]),
@@ -67,6 +83,13 @@ SIGNATURES = {
                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     'danse_batch_covmats': (_c_i32, [ctypes.c_void_p, _c_i32, _c_i32, _c_i32, ctypes.c_void_p, ctypes.c_void_p,
                                      ctypes.c_void_p, ctypes.c_void_p]),
+    'danse_batch_create': (_c_i32, [ctypes.POINTER(DanseBatchCfg), _c_i32, ctypes.POINTER(ctypes.c_void_p)]),
+    'danse_batch_destroy': (None, [ctypes.c_void_p]),
+    'danse_batch_last_error': (ctypes.c_char_p, [ctypes.c_void_p]),
+    'danse_batch_set_inputs': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    'danse_batch_run': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p]),
+    'danse_batch_output_bytes': (_c_i32, [ctypes.c_void_p, _c_i32, _c_i32, ctypes.POINTER(ctypes.c_size_t)]),
+    'danse_batch_get': (_c_i32, [ctypes.c_void_p, _c_i32, _c_i32, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
 }
 
 _lib = None
@@ -98,4 +121,11 @@ def check(rc: int, eng=None):
     if rc != 0:
         lib = load_library()
         msg = lib.danse_last_error(eng)
+        raise DanseError((msg or b'').decode() or f'error {rc}')
+
+
+def check_batch(rc: int, eng=None):
+    if rc != 0:
+        lib = load_library()
+        msg = lib.danse_batch_last_error(eng)
         raise DanseError((msg or b'').decode() or f'error {rc}')

@@ -1,0 +1,186 @@
+"""Host driver of the device batch-mode engine (``danse_batch`` C-ABI,
+``csrc/batch.hip``).  Restates the parameter handling of the reference's
+``danse_batch`` (``danse_toolbox/d_core.py:251-352``) and
+``BatchDANSEvariables`` (``danse_toolbox/d_batch.py:3-205``): frame VAD,
+padded-STFT frame count, update schedule (seq: node ``i mod K`` at batch
+iteration i, asy / sim: every node), initial filters and external-filter
+modes.  Device path only; fully connected, DANSE estimates only
+(centralised / local batch estimates are not on the device path).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib as L
+from .engine import beta_from_t50p, init_complex_filter, _cf32, _ptr
+
+
+def stft_frames(T: int, N: int, Ns: int) -> int:
+    """Frames of ``scipy.signal.stft(..., boundary=None, padded=True)``: the
+    signal is zero-padded at the end to a whole number of hops."""
+    nadd = (-(T - N) % Ns) % N
+    return (T + nadd - N) // Ns + 1
+
+
+class BatchEngine:
+    """S same-shape scenes of one WASN shape, batch DANSE on one device."""
+
+    def __init__(self, scenes, p, device=0, costTrim=1000):
+        import torch
+        self.torch = torch
+        self.lib = L.load_library()
+        self.p = p
+        self.scenes = list(scenes)
+        sc0 = self.scenes[0]
+        self.S = S = len(self.scenes)
+        self.K = K = sc0.nNodes
+        self.M = [n.nSensors for n in sc0.wasn]
+        self.Mtot = int(sum(self.M))
+        self.N, self.Ns = p.DFTsize, p.Ns
+        self.F = F = self.N // 2 + 1
+        self.T = T = sc0.wasn[0].data.shape[0]
+        if p.simType != 'batch':
+            raise ValueError('BatchEngine runs simType batch')
+        if p.computeCentralised or p.computeLocal or p.computeSingleSensorBroadcast:
+            raise NotImplementedError('centralised / local / single-sensor batch estimates are not on the device path')
+        for sc in self.scenes:
+            if sc.nNodes != K or [n.nSensors for n in sc.wasn] != self.M or sc.wasn[0].data.shape[0] != T:
+                raise ValueError('all scenes of one engine must share the WASN shape')
+        for k in range(K):
+            if sorted(sc0.wasn[k].neighborsIdx) != [q for q in range(K) if q != k]:
+                raise NotImplementedError('device path covers fully connected WASNs')
+        self.device = device
+        self.iters = int(p.maxBatchUpdates)
+        self.nIter = int((T - self.N) / self.Ns) + 1
+        self.nseg = nseg = stft_frames(T, self.N, self.Ns)
+        if nseg - 1 != self.nIter:
+            # the reference's batch_estimate fails with a shape mismatch here (quirk Q9)
+            raise ValueError('batch DANSE needs a signal length with (T - N) not a multiple of Ns (quirk Q9)')
+        self.D = [self.M[k] + K - 1 for k in range(K)]
+        # frame VAD, truncated to the STFT frames (update_covmats_batch)
+        vad = np.zeros((S, K, nseg), dtype=np.uint8)
+        for s, sc in enumerate(self.scenes):
+            for k, nd in enumerate(sc.wasn):
+                v = np.asarray(nd.vadPerFrame, dtype=bool)[:nseg]
+                if len(v) < nseg:
+                    raise ValueError('vadPerFrame shorter than the STFT frame count')
+                vad[s, k] = v
+        self._vad = np.ascontiguousarray(vad)
+        doSolve = np.zeros((self.iters, K), dtype=np.uint8)
+        if 'seq' in p.nodeUpdating:
+            for it in range(self.iters):
+                doSolve[it, it % K] = 1
+        else:
+            doSolve[:] = 1
+        self._doSolve = doSolve
+        fi = dict(initType=p.filterInitType, fixedValue=p.filterInitFixedValue)
+        self._w0 = _cf32(np.concatenate([init_complex_filter((F, self.D[k]), p.referenceSensor, **fi).ravel()
+                                         for k in range(K)]))
+        self._wExt0 = _cf32(np.concatenate([init_complex_filter((F, self.M[k]), p.referenceSensor, **fi).ravel()
+                                            for k in range(K)]))
+        extMode = []
+        for k in range(K):
+            if p.onlyBroadcastRefSensorSigs:
+                extMode.append(L.EXT_REFONLY)
+            elif self.M[k] == 1 and p.noFusionAtSingleSensorNodes:
+                extMode.append(L.EXT_KEEP)
+            elif p.noExternalFilterRelaxation or 'seq' in p.nodeUpdating:
+                extMode.append(L.EXT_COPY)
+            else:
+                extMode.append(L.EXT_RELAX)
+        self._extMode = np.array(extMode, dtype=np.int32)
+        betaE = np.zeros((S, K), dtype=np.float32)
+        for s, sc in enumerate(self.scenes):
+            for k, nd in enumerate(sc.wasn):
+                betaE[s, k] = (p.forcedBetaExternalFilters if p.forcedBetaExternalFilters is not None
+                               else beta_from_t50p(p.t_expAvg50pExternalFilters, nd.fs, self.Ns))
+        self._betaE = betaE
+        self._M = np.array(self.M, dtype=np.int32)
+        self._win = np.asarray(p.winWOLAanalysis, dtype=np.float32)
+        c = L.DanseBatchCfg()
+        c.S, c.K, c.M = S, K, _ptr(self._M, ctypes.c_int32)
+        c.N, c.Ns, c.T = self.N, self.Ns, T
+        c.iters, c.nseg = self.iters, nseg
+        c.gevd, c.rank, c.ref = int(bool(p.performGEVD)), int(p.GEVDrank) if p.performGEVD else 1, int(p.referenceSensor)
+        c.alphaExt = float(p.alphaExternalFilters)
+        c.extMode = _ptr(self._extMode, ctypes.c_int32)
+        c.betaExt = _ptr(self._betaE, ctypes.c_float)
+        c.win = _ptr(self._win, ctypes.c_float)
+        c.vad = _ptr(self._vad, ctypes.c_uint8)
+        c.doSolve = _ptr(self._doSolve, ctypes.c_uint8)
+        c.w0, c.wExt0 = _ptr(self._w0, ctypes.c_float), _ptr(self._wExt0, ctypes.c_float)
+        c.costTrim = int(costTrim)
+        self._cfg = c
+        eng = ctypes.c_void_p()
+        L.check_batch(self.lib.danse_batch_create(ctypes.byref(c), int(device), ctypes.byref(eng)))
+        self.eng = eng
+        y = np.empty((S, self.Mtot, T), dtype=np.float32)
+        cl = np.empty((S, K, T), dtype=np.float32)
+        base = np.concatenate(([0], np.cumsum(self.M)[:-1])).astype(int)
+        for s, sc in enumerate(self.scenes):
+            for k, nd in enumerate(sc.wasn):
+                y[s, base[k]:base[k] + self.M[k], :] = nd.data.T
+                cl[s, k] = nd.cleanspeech[:, p.referenceSensor]
+        self.y = torch.from_numpy(y).to(f'cuda:{device}')
+        self.clean = torch.from_numpy(cl).to(f'cuda:{device}')
+        L.check_batch(self.lib.danse_batch_set_inputs(self.eng, ctypes.c_void_p(self.y.data_ptr()),
+                                                      ctypes.c_void_p(self.clean.data_ptr())), self.eng)
+
+    def stream_ptr(self, stream=None):
+        st = stream if stream is not None else self.torch.cuda.current_stream(self.device)
+        return ctypes.c_void_p(st.cuda_stream)
+
+    def run(self, stream=None):
+        L.check_batch(self.lib.danse_batch_run(self.eng, self.stream_ptr(stream)), self.eng)
+        return self
+
+    def _get(self, which, node=0, dtype=np.complex64, shape=None):
+        nb = ctypes.c_size_t()
+        L.check_batch(self.lib.danse_batch_output_bytes(self.eng, which, node, ctypes.byref(nb)), self.eng)
+        out = np.empty(nb.value // np.dtype(dtype).itemsize, dtype=dtype)
+        L.check_batch(self.lib.danse_batch_get(self.eng, which, node, out.ctypes.data_as(ctypes.c_void_p), out.nbytes,
+                                               None), self.eng)
+        return out.reshape(shape) if shape is not None else out
+
+    def outputs(self):
+        """Per scene, the batch outputs in the reference layout: ``wTilde[k]``
+        (F, iters+1, D_k), ``wTildeExt[k]``, ``d`` (T, K), ``dhat``
+        (F, nIter, K), ``mmseCost`` (iters, K)."""
+        S, K, F, H = self.S, self.K, self.F, self.iters + 1
+        res = [BatchOutputs() for _ in range(S)]
+        d = self._get(L.BOUT_D, dtype=np.float32, shape=(S, K, self.T))
+        dh = self._get(L.BOUT_DHAT, shape=(S, K, self.nseg - 1, F))
+        cost = self._get(L.BOUT_COST, dtype=np.float64, shape=(self.iters, S, K))
+        for s in range(S):
+            res[s].d = d[s].T.astype(np.float64)
+            res[s].TDdesiredSignals_est = res[s].d
+            res[s].dhat = np.transpose(dh[s], (2, 1, 0)).astype(np.complex128)
+            res[s].mmseCost = cost[:, s, :].copy()
+            res[s].wTilde, res[s].wTildeExt = [], []
+        for k in range(K):
+            w = self._get(L.BOUT_W, k, shape=(S, H, F, self.D[k]))
+            e = self._get(L.BOUT_WEXT, k, shape=(S, H, F, self.M[k]))
+            for s in range(S):
+                res[s].wTilde.append(np.transpose(w[s], (1, 0, 2)).astype(np.complex128))
+                res[s].wTildeExt.append(np.transpose(e[s], (1, 0, 2)).astype(np.complex128))
+        for s in range(S):
+            res[s].filters = res[s].wTilde
+        return res
+
+    def close(self):
+        if getattr(self, 'eng', None):
+            self.lib.danse_batch_destroy(self.eng)
+            self.eng = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class BatchOutputs:
+    """Container with the reference's batch output field names."""
+    pass

@@ -55,6 +55,28 @@ def danse(wasnObj, p, device=0, graph=True):
     return dv, wasnObj
 
 
+def danse_batch_multi(scenes, p, device=0):
+    """Batch DANSE on S same-shape scenes at once (device batch engine)."""
+    from .batch import BatchEngine
+    eng = BatchEngine(scenes, p, device=device)
+    try:
+        eng.run()
+        return eng.outputs()
+    finally:
+        eng.close()
+
+
+def danse_batch(wasnObj, p, device=0):
+    """``d_core.danse_batch`` (``d_core.py:251-352``): batch-mode fully
+    connected DANSE of one WASN; returns ``(out, wasnObj)`` with the
+    reference's output names (``filters``, ``TDdesiredSignals_est``,
+    ``mmseCost``, ``wTilde``, ``wTildeExt``, ``d``, ``dhat``)."""
+    t0 = time.perf_counter()
+    out = danse_batch_multi([wasnObj], p, device=device)[0]
+    out.wallSeconds = time.perf_counter() - t0
+    return out, wasnObj
+
+
 def generate_signals_for_snr_computation(pD, dv, wasnObj, danse_function=danse):
     """``d_core.generate_signals_for_snr_computation`` (``d_core.py:550-599``):
     noise-only and speech-only replays with the recorded filters."""

@@ -1,0 +1,718 @@
+// Batch-mode DANSE on the device (d_batch.py:3-205, d_core.py:251-352,
+// d_classes.py:3272-3304, d_base.py:2284-2364,2473-2542): the whole signal's
+// STFT once, then per batch iteration
+//   z_q = wExt_q^H Y_q                         (batch_z_kernel)
+//   Ryy, Rnn = mean over VAD / non-VAD frames  (herk_kernel: MFMA f32 16x16x4)
+//   w = MWF / GEVD(Ryy, Rnn)                   (the filter-update size classes)
+//   external filters                           (batch_ext_kernel)
+//   dhat = w^H ytilde, d = ISTFT(dhat)         (batch_est_kernel + batch_ola_kernel)
+//   MMSE cost                                  (batch_cost_kernel)
+// The STFT is scipy.signal.stft(boundary=None, padded=True) times sum(win)
+// (a raw windowed DFT of frames t Ns .. t Ns + N, the signal zero-padded at
+// the end); the ISTFT is scipy.signal.istft(boundary=None) divided by
+// sum(win): x = sum_t irfft(dhat_t) win / sum_t win^2 where that is > 1e-10.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <string>
+#include <vector>
+
+#include "classes.hpp"
+#include "wfft.hpp"
+
+using namespace danse;
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <typename T>
+hipError_t balloc(T** p, size_t n) {
+  if (n == 0) n = 1;
+  return hipMalloc((void**)p, n * sizeof(T));
+}
+
+// ---------------------------------------------------------------------------
+// Kernels
+// ---------------------------------------------------------------------------
+
+// STFT: one wave per (scene, channel, frame).  Y[s][f][t][c] (channel-minor,
+// so a node's channels of one (bin, frame) are contiguous for the HERK loads).
+__global__ void __launch_bounds__(256) batch_stft_kernel(const float* __restrict__ y, int S, int MT, int T, int Ns,
+                                                         int nseg, const float* __restrict__ win,
+                                                         const cf* __restrict__ tw, cf* __restrict__ Y) {
+  __shared__ cf lds[4][wfft::kLdsElems];
+  const int wv = threadIdx.x >> 6;
+  const long long job = (long long)blockIdx.x * 4 + wv;
+  const long long nJobs = (long long)S * MT * nseg;
+  if (job >= nJobs) return;   // whole wave exits together
+  const int t = (int)(job % nseg);
+  const int c = (int)((job / nseg) % MT);
+  const int s = (int)(job / ((long long)nseg * MT));
+  const float* x = y + ((long long)s * MT + c) * T;
+  const int l = __lane_id();
+  cf v[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int n = l + 64 * j;
+    const int idx = t * Ns + n;
+    v[j] = cf{(idx < T ? x[idx] : 0.0f) * win[n], 0.0f};
+  }
+  wfft::fft1024(v, lds[wv], tw);
+  constexpr int F = 513;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int f = wfft::out_index(q);
+    if (f < F) Y[(((long long)s * F + f) * nseg + t) * MT + c] = v[q];
+  }
+}
+
+// z_q[s][f][t] = sum_m conj(wExt_q[f][m]) Y[s][f][t][base_q + m]   -> Z[s][f][t][q]
+__global__ void batch_z_kernel(const cf* __restrict__ Y, int S, int K, int MT, int nseg, const int* __restrict__ M,
+                               const int* __restrict__ base, const cf* __restrict__ wExtHist,
+                               const long long* __restrict__ wExtOff, long long wExtStride, int slot,
+                               cf* __restrict__ Z) {
+  constexpr int F = 513;
+  const long long n = (long long)S * F * nseg * K;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+    const int q = (int)(e % K);
+    const long long sft = e / K;            // (s, f, t)
+    const int f = (int)((sft / nseg) % F);
+    const int s = (int)(sft / ((long long)nseg * F));
+    const int Mq = M[q];
+    const cf* wx = wExtHist + (long long)s * wExtStride + wExtOff[q] + ((long long)slot * F + f) * Mq;
+    const cf* yy = Y + sft * MT + base[q];
+    cf acc = cf{0.0f, 0.0f};
+    for (int m = 0; m < Mq; ++m) acc = acc + cmul(wx[m], yy[m]);
+    Z[e] = acc;
+  }
+}
+
+struct HerkNode {
+  int k, D, M;
+  int pad;
+  long long scmOff;   // complex offset of this node's [S][F][D][D] block
+};
+
+// Ryy / Rnn of every (scene, node, bin): one wave per problem, the D x D
+// Hermitian product of the observation matrix over the VAD (pass 0) and
+// non-VAD (pass 1) frame lists, on v_mfma_f32_16x16x4_f32 (exact f32 FMA
+// chains).  C = sum_t y_t y_t^H:  Re C = Yr^T Yr + Yi^T Yi,
+// Im C = Yi^T Yr - Yr^T Yi; tile pairs (I >= J) of 16 x 16, the upper
+// triangle by symmetry.
+template <int NT>
+__global__ void __launch_bounds__(64) herk_kernel(const cf* __restrict__ Y, const cf* __restrict__ Z, int S, int K,
+                                                  int MT, int nseg, const int* __restrict__ base,
+                                                  const HerkNode* __restrict__ nodes, int nNodes,
+                                                  const int* __restrict__ frames, const int* __restrict__ nvad,
+                                                  cf* __restrict__ Ryy, cf* __restrict__ Rnn) {
+  constexpr int F = 513;
+  constexpr int NP = NT * (NT + 1) / 2;
+  const int l = threadIdx.x;
+  const int f = blockIdx.x % F;
+  const int ni = (blockIdx.x / F) % nNodes;
+  const int s = blockIdx.x / (F * nNodes);
+  const HerkNode nd = nodes[ni];
+  const int k = nd.k, D = nd.D, Mk = nd.M;
+  const int il = l & 15, tt = l >> 4;
+  const int* fl = frames + ((long long)s * K + k) * nseg;   // VAD frames first, then the others
+  const int nv = nvad[s * K + k];
+  // per tile: source pointer of channel 16 I + il (local mic or a neighbour's z)
+  const cf* src[NT];
+  int stride[NT];
+  bool act[NT];
+#pragma unroll
+  for (int I = 0; I < NT; ++I) {
+    const int i = 16 * I + il;
+    act[I] = i < D;
+    if (i < Mk) {
+      src[I] = Y + ((long long)s * F + f) * nseg * MT + base[k] + i;
+      stride[I] = MT;
+    } else {
+      const int j = i - Mk;
+      const int q = (j < k) ? j : j + 1;
+      src[I] = act[I] ? Z + ((long long)s * F + f) * nseg * K + q : Y;   // inactive: never read
+      stride[I] = K;
+    }
+  }
+  for (int pass = 0; pass < 2; ++pass) {
+    const int t0 = pass ? nv : 0;
+    const int cnt = pass ? nseg - nv : nv;
+    f32x4 are[NP], aim[NP];
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      are[p] = f32x4(0.0f);
+      aim[p] = f32x4(0.0f);
+    }
+    for (int b = 0; b < cnt; b += 4) {
+      const int ti = b + tt;
+      const bool ok = ti < cnt;
+      const int t = ok ? fl[t0 + ti] : 0;
+      cf v[NT];
+#pragma unroll
+      for (int I = 0; I < NT; ++I) v[I] = (ok && act[I]) ? src[I][(long long)t * stride[I]] : cf{0.0f, 0.0f};
+      int p = 0;
+#pragma unroll
+      for (int I = 0; I < NT; ++I) {
+#pragma unroll
+        for (int J = 0; J <= I; ++J) {
+          are[p] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[I].re, v[J].re, are[p], 0, 0, 0);
+          are[p] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[I].im, v[J].im, are[p], 0, 0, 0);
+          aim[p] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[I].im, v[J].re, aim[p], 0, 0, 0);
+          aim[p] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[I].re, -v[J].im, aim[p], 0, 0, 0);
+          ++p;
+        }
+      }
+    }
+    // mean over the frames (np.mean of an empty set is NaN, as in the reference)
+    const float sc = (cnt > 0) ? 1.0f / (float)cnt : __builtin_nanf("");
+    cf* out = (pass ? Rnn : Ryy) + nd.scmOff + ((long long)s * F + f) * D * D;
+    int p = 0;
+#pragma unroll
+    for (int I = 0; I < NT; ++I) {
+#pragma unroll
+      for (int J = 0; J <= I; ++J) {
+#pragma unroll
+        for (int rg = 0; rg < 4; ++rg) {
+          const int row = 16 * I + 4 * tt + rg;   // C/D map: col = lane & 15, row = 4 (lane >> 4) + reg
+          const int col = 16 * J + il;
+          if (row < D && col < D && (I != J || col <= row)) {
+            cf c = cf{sc * are[p][rg], sc * aim[p][rg]};
+            if (row == col) c.im = 0.0f;
+            out[(long long)row * D + col] = c;
+            if (row != col) out[(long long)col * D + row] = conjg(c);
+          }
+        }
+        ++p;
+      }
+    }
+  }
+}
+
+// External filters after the update of iteration it (update_external_filters,
+// d_classes.py:1627-1694, batch call with t = None): per (scene, node, bin, mic).
+__global__ void batch_ext_kernel(int S, int K, int it, const int* __restrict__ M, const int* __restrict__ Dk,
+                                 const int* __restrict__ extMode, int ref, const float* __restrict__ betaExt,
+                                 float alphaExt, const cf* __restrict__ wHist, const long long* __restrict__ wOff,
+                                 long long wStride, int hist, cf* __restrict__ wExtHist,
+                                 const long long* __restrict__ wExtOff, long long wExtStride,
+                                 cf* __restrict__ tgt, const long long* __restrict__ tgtOff, long long tgtStride,
+                                 int Mmax) {
+  constexpr int F = 513;
+  const long long n = (long long)S * K * F * Mmax;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+    const int m = (int)(e % Mmax);
+    const int f = (int)((e / Mmax) % F);
+    const int k = (int)((e / ((long long)Mmax * F)) % K);
+    const int s = (int)(e / ((long long)Mmax * F * K));
+    const int Mq = M[k];
+    if (m >= Mq) continue;
+    const cf* w = wHist + (long long)s * wStride + wOff[k] + ((long long)(it + 1) * F + f) * Dk[k];
+    cf* eprev = wExtHist + (long long)s * wExtStride + wExtOff[k] + ((long long)it * F + f) * Mq;
+    cf* enext = eprev + (long long)F * Mq;
+    cf* tg = tgt + (long long)s * tgtStride + tgtOff[k] + (long long)f * Mq;
+    cf ne;
+    const int mode = extMode[k];
+    if (mode == DANSE_EXT_REFONLY) ne = cf{(m == ref) ? 1.0f : 0.0f, 0.0f};
+    else if (mode == DANSE_EXT_KEEP) ne = eprev[m];
+    else if (mode == DANSE_EXT_COPY) ne = w[m];
+    else {
+      const float be = betaExt[s * K + k];
+      const cf t0 = tg[m];
+      ne = be * eprev[m] + (1.0f - be) * t0;
+      tg[m] = (1.0f - alphaExt) * t0 + alphaExt * w[m];
+    }
+    enext[m] = ne;
+    (void)hist;
+  }
+}
+
+// dhat_k[f][t] = sum_i conj(w_k[f][i]) ytilde_k[f][t][i] for t < nseg - 1, and
+// the frame's irfft times the window: one wave per (scene, node, frame).
+__global__ void __launch_bounds__(256) batch_est_kernel(const cf* __restrict__ Y, const cf* __restrict__ Z, int S,
+                                                        int K, int MT, int nseg, const int* __restrict__ M,
+                                                        const int* __restrict__ base, const int* __restrict__ Dk,
+                                                        const cf* __restrict__ wHist, const long long* __restrict__ wOff,
+                                                        long long wStride, int slot, const float* __restrict__ win,
+                                                        const cf* __restrict__ tw, cf* __restrict__ dhat,
+                                                        float* __restrict__ frames) {
+  __shared__ cf lds[4][wfft::kLdsElems];
+  constexpr int F = 513;
+  const int nfr = nseg - 1;
+  const int wv = threadIdx.x >> 6;
+  const long long job = (long long)blockIdx.x * 4 + wv;
+  if (job >= (long long)S * K * nfr) return;
+  const int t = (int)(job % nfr);
+  const int k = (int)((job / nfr) % K);
+  const int s = (int)(job / ((long long)nfr * K));
+  const int Mk = M[k], D = Dk[k];
+  const cf* w = wHist + (long long)s * wStride + wOff[k] + (long long)slot * F * D;
+  const int l = __lane_id();
+  auto dh = [&](int f) {
+    const cf* yl = Y + (((long long)s * F + f) * nseg + t) * MT + base[k];
+    const cf* zl = Z + (((long long)s * F + f) * nseg + t) * K;
+    const cf* wf = w + (long long)f * D;
+    cf acc = cf{0.0f, 0.0f};
+    for (int i = 0; i < Mk; ++i) acc = acc + cmul(wf[i], yl[i]);
+    for (int j = 0; j < D - Mk; ++j) acc = acc + cmul(wf[Mk + j], zl[(j < k) ? j : j + 1]);
+    return acc;
+  };
+  cf v[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int n = l + 64 * j;
+    if (n < F) {
+      const cf d = dh(n);
+      dhat[(((long long)s * K + k) * nfr + t) * F + n] = d;
+      cf x = conjg(d);
+      if (n == 0 || n == F - 1) x.im = 0.0f;   // irfft ignores the imaginary DC / Nyquist parts
+      v[j] = x;
+    } else {
+      v[j] = dh(1024 - n);
+    }
+  }
+  wfft::fft1024(v, lds[wv], tw);
+  float* out = frames + (((long long)s * K + k) * nfr + t) * 1024;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int n = wfft::out_index(q);
+    out[n] = v[q].re * (1.0f / 1024.0f) * win[n];
+  }
+}
+
+// Overlap-add of the windowed frames, normalised by the overlap-add of win^2
+// where that exceeds 1e-10 (scipy istft); zero beyond the last frame.
+__global__ void batch_ola_kernel(const float* __restrict__ frames, int S, int K, int T, int Ns, int nseg,
+                                 const float* __restrict__ win, float* __restrict__ d) {
+  const int nfr = nseg - 1;
+  const long long n = (long long)S * K * T;
+  const int outLen = 1024 + (nfr - 1) * Ns;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+    const int x = (int)(e % T);
+    const long long sk = e / T;
+    float acc = 0.0f, nrm = 0.0f;
+    if (x < outLen) {
+      int tLo = (x - 1024) / Ns + 1;
+      if (x - 1024 < 0) tLo = 0;
+      const int tHi = min(x / Ns, nfr - 1);
+      for (int t = max(tLo, 0); t <= tHi; ++t) {
+        const int o = x - t * Ns;
+        if (o < 0 || o >= 1024) continue;
+        acc += frames[(sk * nfr + t) * 1024 + o];
+        nrm += win[o] * win[o];
+      }
+      if (nrm > 1e-10f) acc /= nrm;
+    }
+    d[e] = acc;
+  }
+}
+
+// MMSE cost of iteration it: mean over [trim, T - trim) of |clean - d|^2
+// (get_mmse_cost, d_batch.py), fixed-order tree reduction in double.
+__global__ void __launch_bounds__(256) batch_cost_kernel(const float* __restrict__ clean, const float* __restrict__ d,
+                                                         int T, int trim, double* __restrict__ cost) {
+  __shared__ double red[256];
+  const long long sk = blockIdx.x;
+  double acc = 0.0;
+  for (int x = trim + threadIdx.x; x < T - trim; x += blockDim.x) {
+    const double e = (double)clean[sk * T + x] - (double)d[sk * T + x];
+    acc += e * e;
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) cost[sk] = red[0] / (double)max(T - 2 * trim, 1);
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// Engine
+// ---------------------------------------------------------------------------
+
+struct danse_batch {
+  int dev = 0;
+  std::string err;
+  int S, K, MT, N, Ns, T, F, iters, nseg, gevd, rank, ref, trim;
+  float alphaExt;
+  std::vector<int> M, base, D, extMode;
+  std::vector<long long> scmOff, wOff, wExtOff, tgtOff;
+  long long scmStride = 0, wStride = 0, wExtStride = 0, tgtStride = 0;
+  std::vector<uint8_t> doSolve;   // [iters][K]
+  std::vector<int> nvadHost;
+  // device
+  int *dM = nullptr, *dBase = nullptr, *dD = nullptr, *dExtMode = nullptr, *dFrames = nullptr, *dNvad = nullptr;
+  long long *dWOff = nullptr, *dWExtOff = nullptr, *dTgtOff = nullptr;
+  HerkNode* dNodes = nullptr;
+  std::vector<HerkNode> nodes;
+  float *dWin = nullptr, *dBetaExt = nullptr, *dFramesTD = nullptr, *dD_ = nullptr;
+  cf *dTw = nullptr, *Y = nullptr, *Z = nullptr, *Ryy = nullptr, *Rnn = nullptr, *wHist = nullptr, *wExtHist = nullptr,
+     *tgt = nullptr, *dhat = nullptr, *wTmp = nullptr;
+  double* dCost = nullptr;
+  int* dDiag = nullptr;
+  const float* y = nullptr;
+  const float* clean = nullptr;
+  std::vector<cf> w0, wExt0;   // host initial filters (per node, concatenated)
+};
+
+static thread_local std::string g_berr;
+
+#define BCHK(expr)                                                                  \
+  do {                                                                              \
+    hipError_t _e = (expr);                                                         \
+    if (_e != hipSuccess) {                                                         \
+      std::string m = std::string(#expr) + ": " + hipGetErrorString(_e);            \
+      if (eng) eng->err = m;                                                        \
+      g_berr = m;                                                                   \
+      return -2;                                                                    \
+    }                                                                               \
+  } while (0)
+
+static int bfail(danse_batch* eng, const std::string& m) {
+  if (eng) eng->err = m;
+  g_berr = m;
+  return -1;
+}
+
+extern "C" {
+
+const char* danse_batch_last_error(const danse_batch* eng) {
+  if (eng && !eng->err.empty()) return eng->err.c_str();
+  return g_berr.c_str();
+}
+
+int danse_batch_create(const danse_batch_cfg* c, int device, danse_batch** out) {
+  danse_batch* eng = nullptr;
+  if (!c || !out) return bfail(nullptr, "null argument");
+  if (c->N != 1024) return bfail(nullptr, "only DFTsize 1024 is supported");
+  if (c->K < 2 || c->S < 1 || c->iters < 1 || c->nseg < 2) return bfail(nullptr, "bad sizes");
+  if (c->rank < 1 || c->rank > kRMax) return bfail(nullptr, "GEVD rank out of range [1, 4]");
+  eng = new danse_batch();
+  eng->dev = device;
+  BCHK(hipSetDevice(device));
+  eng->S = c->S; eng->K = c->K; eng->N = c->N; eng->Ns = c->Ns; eng->T = c->T; eng->F = c->N / 2 + 1;
+  eng->iters = c->iters; eng->nseg = c->nseg; eng->gevd = c->gevd; eng->rank = c->rank; eng->ref = c->ref;
+  eng->alphaExt = c->alphaExt; eng->trim = c->costTrim;
+  const int S = c->S, K = c->K, F = eng->F, nseg = c->nseg, H = c->iters + 1;
+  eng->M.assign(c->M, c->M + K);
+  eng->extMode.assign(c->extMode, c->extMode + K);
+  eng->base.resize(K);
+  eng->D.resize(K);
+  int mt = 0, Mmax = 0;
+  for (int k = 0; k < K; ++k) {
+    eng->base[k] = mt;
+    mt += eng->M[k];
+    Mmax = std::max(Mmax, eng->M[k]);
+    eng->D[k] = eng->M[k] + K - 1;
+    if (eng->D[k] > kMaxDMax) return bfail(eng, "filter dimension > 64 not supported");
+    if (c->ref >= eng->M[k]) return bfail(eng, "referenceSensor must be < M_k for every node");
+    if (c->gevd && c->rank > eng->D[k]) return bfail(eng, "GEVD rank larger than a filter dimension");
+  }
+  eng->MT = mt;
+  long long so = 0, wo = 0, eo = 0, to = 0;
+  eng->scmOff.resize(K); eng->wOff.resize(K); eng->wExtOff.resize(K); eng->tgtOff.resize(K);
+  for (int k = 0; k < K; ++k) {
+    eng->scmOff[k] = so; so += (long long)S * F * eng->D[k] * eng->D[k];
+    eng->wOff[k] = wo; wo += (long long)H * F * eng->D[k];
+    eng->wExtOff[k] = eo; eo += (long long)H * F * eng->M[k];
+    eng->tgtOff[k] = to; to += (long long)F * eng->M[k];
+    eng->nodes.push_back(HerkNode{k, eng->D[k], eng->M[k], 0, eng->scmOff[k]});
+  }
+  eng->scmStride = so;   // Ryy / Rnn are node-major [k][S][F][D][D] (not per scene)
+  eng->wStride = wo; eng->wExtStride = eo; eng->tgtStride = to;
+  eng->doSolve.assign(c->doSolve, c->doSolve + (size_t)c->iters * K);
+  // frame lists: VAD frames first, then the rest, per (scene, node)
+  std::vector<int> frames((size_t)S * K * nseg), nv((size_t)S * K);
+  for (int s = 0; s < S; ++s)
+    for (int k = 0; k < K; ++k) {
+      const uint8_t* v = c->vad + ((size_t)s * K + k) * nseg;
+      int* fl = frames.data() + ((size_t)s * K + k) * nseg;
+      int n = 0;
+      for (int t = 0; t < nseg; ++t)
+        if (v[t]) fl[n++] = t;
+      nv[(size_t)s * K + k] = n;
+      for (int t = 0; t < nseg; ++t)
+        if (!v[t]) fl[n++] = t;
+    }
+  eng->nvadHost = nv;
+  // initial filters
+  {
+    long long a = 0, b = 0;
+    for (int k = 0; k < K; ++k) { a += (long long)F * eng->D[k]; b += (long long)F * eng->M[k]; }
+    eng->w0.resize(a);
+    eng->wExt0.resize(b);
+    for (long long i = 0; i < a; ++i)
+      eng->w0[i] = c->w0 ? cf{c->w0[2 * i], c->w0[2 * i + 1]} : cf{0.0f, 0.0f};
+    for (long long i = 0; i < b; ++i)
+      eng->wExt0[i] = c->wExt0 ? cf{c->wExt0[2 * i], c->wExt0[2 * i + 1]} : cf{0.0f, 0.0f};
+  }
+  // device buffers
+  BCHK(balloc(&eng->dM, K)); BCHK(balloc(&eng->dBase, K)); BCHK(balloc(&eng->dD, K)); BCHK(balloc(&eng->dExtMode, K));
+  BCHK(balloc(&eng->dFrames, frames.size())); BCHK(balloc(&eng->dNvad, nv.size()));
+  BCHK(balloc(&eng->dWOff, K)); BCHK(balloc(&eng->dWExtOff, K)); BCHK(balloc(&eng->dTgtOff, K));
+  BCHK(balloc(&eng->dNodes, K));
+  BCHK(balloc(&eng->dWin, c->N)); BCHK(balloc(&eng->dBetaExt, (size_t)S * K));
+  BCHK(balloc(&eng->dTw, wfft::kTwElems));
+  BCHK(hipMemcpy(eng->dM, eng->M.data(), K * sizeof(int), hipMemcpyHostToDevice));
+  BCHK(hipMemcpy(eng->dBase, eng->base.data(), K * sizeof(int), hipMemcpyHostToDevice));
+  BCHK(hipMemcpy(eng->dD, eng->D.data(), K * sizeof(int), hipMemcpyHostToDevice));
+  BCHK(hipMemcpy(eng->dExtMode, eng->extMode.data(), K * sizeof(int), hipMemcpyHostToDevice));
+  BCHK(hipMemcpy(eng->dFrames, frames.data(), frames.size() * sizeof(int), hipMemcpyHostToDevice));
+  BCHK(hipMemcpy(eng->dNvad, nv.data(), nv.size() * sizeof(int), hipMemcpyHostToDevice));
+  BCHK(hipMemcpy(eng->dWOff, eng->wOff.data(), K * sizeof(long long), hipMemcpyHostToDevice));
+  BCHK(hipMemcpy(eng->dWExtOff, eng->wExtOff.data(), K * sizeof(long long), hipMemcpyHostToDevice));
+  BCHK(hipMemcpy(eng->dTgtOff, eng->tgtOff.data(), K * sizeof(long long), hipMemcpyHostToDevice));
+  BCHK(hipMemcpy(eng->dNodes, eng->nodes.data(), K * sizeof(HerkNode), hipMemcpyHostToDevice));
+  BCHK(hipMemcpy(eng->dWin, c->win, c->N * sizeof(float), hipMemcpyHostToDevice));
+  BCHK(hipMemcpy(eng->dBetaExt, c->betaExt, (size_t)S * K * sizeof(float), hipMemcpyHostToDevice));
+  {
+    std::vector<cf> tw;
+    for (int k1 = 0; k1 < 16; ++k1)
+      for (int l = 0; l < 64; ++l) {
+        const double ang = -2.0 * M_PI * (double)(l * k1) / 1024.0;
+        tw.push_back(cf{(float)std::cos(ang), (float)std::sin(ang)});
+      }
+    for (int a4 = 0; a4 < 4; ++a4)
+      for (int cc = 0; cc < 16; ++cc) {
+        const double ang = -2.0 * M_PI * (double)(a4 * cc) / 64.0;
+        tw.push_back(cf{(float)std::cos(ang), (float)std::sin(ang)});
+      }
+    BCHK(hipMemcpy(eng->dTw, tw.data(), tw.size() * sizeof(cf), hipMemcpyHostToDevice));
+  }
+  BCHK(balloc(&eng->Y, (size_t)S * F * nseg * mt));
+  BCHK(balloc(&eng->Z, (size_t)S * F * nseg * K));
+  BCHK(balloc(&eng->Ryy, (size_t)so));
+  BCHK(balloc(&eng->Rnn, (size_t)so));
+  BCHK(balloc(&eng->wHist, (size_t)S * wo));
+  BCHK(balloc(&eng->wExtHist, (size_t)S * eo));
+  BCHK(balloc(&eng->tgt, (size_t)S * to));
+  BCHK(balloc(&eng->dhat, (size_t)S * K * (nseg - 1) * F));
+  BCHK(balloc(&eng->dFramesTD, (size_t)S * K * (nseg - 1) * 1024));
+  BCHK(balloc(&eng->dD_, (size_t)S * K * c->T));
+  BCHK(balloc(&eng->dCost, (size_t)c->iters * S * K));
+  int Dmax = 0;
+  for (int k = 0; k < K; ++k) Dmax = std::max(Dmax, eng->D[k]);
+  BCHK(balloc(&eng->wTmp, (size_t)S * F * Dmax));
+  BCHK(balloc(&eng->dDiag, (size_t)S * F));
+  (void)Mmax;
+  *out = eng;
+  return 0;
+}
+
+void danse_batch_destroy(danse_batch* eng) {
+  if (!eng) return;
+  (void)hipSetDevice(eng->dev);
+  void* ptrs[] = {eng->dM, eng->dBase, eng->dD, eng->dExtMode, eng->dFrames, eng->dNvad, eng->dWOff, eng->dWExtOff,
+                  eng->dTgtOff, eng->dNodes, eng->dWin, eng->dBetaExt, eng->dTw, eng->Y, eng->Z, eng->Ryy, eng->Rnn,
+                  eng->wHist, eng->wExtHist, eng->tgt, eng->dhat, eng->dFramesTD, eng->dD_, eng->dCost, eng->wTmp,
+                  eng->dDiag};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  delete eng;
+}
+
+int danse_batch_set_inputs(danse_batch* eng, const float* y, const float* clean) {
+  if (!eng || !y) return bfail(eng, "null argument");
+  eng->y = y;
+  eng->clean = clean;
+  return 0;
+}
+
+static void launch_herk(danse_batch* e, hipStream_t st) {
+  // one launch per tile count (nodes grouped by ceil(D / 16))
+  for (int nt = 1; nt <= 4; ++nt) {
+    std::vector<HerkNode> grp;
+    for (auto& n : e->nodes)
+      if ((n.D + 15) / 16 == nt) grp.push_back(n);
+    if (grp.empty()) continue;
+    // contiguous groups only when all nodes share nt (the common case); else per node
+    const bool all = (int)grp.size() == e->K;
+    for (size_t g = 0; g < (all ? 1 : grp.size()); ++g) {
+      const HerkNode* dn = e->dNodes + (all ? 0 : grp[g].k);
+      const int nN = all ? e->K : 1;
+      const unsigned grid = (unsigned)(e->S * nN * e->F);
+#define DANSE_HERK(NTV)                                                                                             \
+  hipLaunchKernelGGL(herk_kernel<NTV>, dim3(grid), dim3(64), 0, st, e->Y, e->Z, e->S, e->K, e->MT, e->nseg, e->dBase, \
+                     dn, nN, e->dFrames, e->dNvad, e->Ryy, e->Rnn)
+      if (nt == 1) DANSE_HERK(1);
+      else if (nt == 2) DANSE_HERK(2);
+      else if (nt == 3) DANSE_HERK(3);
+      else DANSE_HERK(4);
+#undef DANSE_HERK
+    }
+  }
+}
+
+int danse_batch_run(danse_batch* eng, void* stream) {
+  if (!eng || !eng->y) return bfail(eng, "inputs not set");
+  BCHK(hipSetDevice(eng->dev));
+  hipStream_t st = (hipStream_t)stream;
+  const int S = eng->S, K = eng->K, F = eng->F, nseg = eng->nseg, H = eng->iters + 1;
+  // initial state: w / wExt slot 0 and the external-filter targets
+  for (int s = 0; s < S; ++s) {
+    long long a = 0, b = 0;
+    for (int k = 0; k < K; ++k) {
+      BCHK(hipMemcpyAsync(eng->wHist + (long long)s * eng->wStride + eng->wOff[k], eng->w0.data() + a,
+                          (size_t)F * eng->D[k] * sizeof(cf), hipMemcpyHostToDevice, st));
+      BCHK(hipMemcpyAsync(eng->wExtHist + (long long)s * eng->wExtStride + eng->wExtOff[k], eng->wExt0.data() + b,
+                          (size_t)F * eng->M[k] * sizeof(cf), hipMemcpyHostToDevice, st));
+      BCHK(hipMemcpyAsync(eng->tgt + (long long)s * eng->tgtStride + eng->tgtOff[k], eng->wExt0.data() + b,
+                          (size_t)F * eng->M[k] * sizeof(cf), hipMemcpyHostToDevice, st));
+      a += (long long)F * eng->D[k];
+      b += (long long)F * eng->M[k];
+    }
+  }
+  {
+    const long long jobs = (long long)S * eng->MT * nseg;
+    hipLaunchKernelGGL(batch_stft_kernel, dim3((unsigned)((jobs + 3) / 4)), dim3(256), 0, st, eng->y, S, eng->MT,
+                       eng->T, eng->Ns, nseg, eng->dWin, eng->dTw, eng->Y);
+    BCHK(hipGetLastError());
+  }
+  int Mmax = 0;
+  for (int k = 0; k < K; ++k) Mmax = std::max(Mmax, eng->M[k]);
+  for (int it = 0; it < eng->iters; ++it) {
+    hipLaunchKernelGGL(batch_z_kernel, dim3(2048), dim3(256), 0, st, eng->Y, S, K, eng->MT, nseg, eng->dM, eng->dBase,
+                       eng->wExtHist, eng->dWExtOff, eng->wExtStride, it, eng->Z);
+    BCHK(hipGetLastError());
+    launch_herk(eng, st);
+    BCHK(hipGetLastError());
+    for (int k = 0; k < K; ++k) {
+      const int D = eng->D[k];
+      cf* wNext = eng->wHist + eng->wOff[k] + (long long)(it + 1) * F * D;
+      const size_t rowB = (size_t)F * D * sizeof(cf);
+      const size_t pitch = (size_t)eng->wStride * sizeof(cf);
+      if (eng->doSolve[(size_t)it * K + k]) {
+        const cf* Ry = eng->Ryy + eng->scmOff[k];
+        const cf* Rn = eng->Rnn + eng->scmOff[k];
+        if (!launch_filter_update_class(class_dmax(D), Ry, Rn, S * F, D, eng->gevd, eng->rank, eng->ref, eng->wTmp,
+                                        eng->dDiag, st))
+          return bfail(eng, "no solver class for this filter dimension");
+        BCHK(hipMemcpy2DAsync(wNext, pitch, eng->wTmp, rowB, rowB, S, hipMemcpyDeviceToDevice, st));
+      } else {
+        BCHK(hipMemcpy2DAsync(wNext, pitch, wNext - (long long)F * D, pitch, rowB, S, hipMemcpyDeviceToDevice, st));
+      }
+    }
+    hipLaunchKernelGGL(batch_ext_kernel, dim3(512), dim3(256), 0, st, S, K, it, eng->dM, eng->dD, eng->dExtMode,
+                       eng->ref, eng->dBetaExt, eng->alphaExt, eng->wHist, eng->dWOff, eng->wStride, H, eng->wExtHist,
+                       eng->dWExtOff, eng->wExtStride, eng->tgt, eng->dTgtOff, eng->tgtStride, Mmax);
+    BCHK(hipGetLastError());
+    const long long jobs = (long long)S * K * (nseg - 1);
+    hipLaunchKernelGGL(batch_est_kernel, dim3((unsigned)((jobs + 3) / 4)), dim3(256), 0, st, eng->Y, eng->Z, S, K,
+                       eng->MT, nseg, eng->dM, eng->dBase, eng->dD, eng->wHist, eng->dWOff, eng->wStride, it + 1,
+                       eng->dWin, eng->dTw, eng->dhat, eng->dFramesTD);
+    BCHK(hipGetLastError());
+    hipLaunchKernelGGL(batch_ola_kernel, dim3(2048), dim3(256), 0, st, eng->dFramesTD, S, K, eng->T, eng->Ns, nseg,
+                       eng->dWin, eng->dD_);
+    BCHK(hipGetLastError());
+    if (eng->clean) {
+      hipLaunchKernelGGL(batch_cost_kernel, dim3(S * K), dim3(256), 0, st, eng->clean, eng->dD_, eng->T, eng->trim,
+                         eng->dCost + (size_t)it * S * K);
+      BCHK(hipGetLastError());
+    }
+  }
+  return 0;
+}
+
+int danse_batch_output_bytes(danse_batch* eng, int32_t which, int32_t node, size_t* bytes) {
+  if (!eng || !bytes) return bfail(eng, "null argument");
+  const int S = eng->S, K = eng->K, F = eng->F, H = eng->iters + 1;
+  if ((which == DANSE_BATCH_OUT_W || which == DANSE_BATCH_OUT_WEXT) && (node < 0 || node >= K))
+    return bfail(eng, "node out of range");
+  switch (which) {
+    case DANSE_BATCH_OUT_W: *bytes = (size_t)S * H * F * eng->D[node] * sizeof(cf); break;
+    case DANSE_BATCH_OUT_WEXT: *bytes = (size_t)S * H * F * eng->M[node] * sizeof(cf); break;
+    case DANSE_BATCH_OUT_D: *bytes = (size_t)S * K * eng->T * sizeof(float); break;
+    case DANSE_BATCH_OUT_DHAT: *bytes = (size_t)S * K * (eng->nseg - 1) * F * sizeof(cf); break;
+    case DANSE_BATCH_OUT_COST: *bytes = (size_t)eng->iters * S * K * sizeof(double); break;
+    default: return bfail(eng, "unknown output");
+  }
+  return 0;
+}
+
+int danse_batch_get(danse_batch* eng, int32_t which, int32_t node, void* dst, size_t bytes, void* stream) {
+  size_t need;
+  int rc = danse_batch_output_bytes(eng, which, node, &need);
+  if (rc) return rc;
+  if (bytes < need) return bfail(eng, "destination too small");
+  BCHK(hipSetDevice(eng->dev));
+  hipStream_t st = (hipStream_t)stream;
+  const int F = eng->F, H = eng->iters + 1;
+  if (which == DANSE_BATCH_OUT_W || which == DANSE_BATCH_OUT_WEXT) {
+    const bool w = which == DANSE_BATCH_OUT_W;
+    const size_t chunk = (size_t)H * F * (w ? eng->D[node] : eng->M[node]) * sizeof(cf);
+    const char* src = (const char*)(w ? eng->wHist + eng->wOff[node] : eng->wExtHist + eng->wExtOff[node]);
+    const size_t pitch = (size_t)(w ? eng->wStride : eng->wExtStride) * sizeof(cf);
+    BCHK(hipMemcpy2DAsync(dst, chunk, src, pitch, chunk, eng->S, hipMemcpyDefault, st));
+  } else {
+    const void* src = which == DANSE_BATCH_OUT_D ? (const void*)eng->dD_
+                      : which == DANSE_BATCH_OUT_DHAT ? (const void*)eng->dhat
+                                                      : (const void*)eng->dCost;
+    BCHK(hipMemcpyAsync(dst, src, need, hipMemcpyDefault, st));
+  }
+  BCHK(hipStreamSynchronize(st));
+  return 0;
+}
+
+// Stand-alone Y.Y^H operator (include/danse_mi355x.h): B independent
+// [Tf][D] observation matrices, shared frame VAD.  Runs the MFMA HERK kernel
+// with one "node" of dimension D and no z channels.
+int danse_batch_covmats(const float* Y, int32_t B, int32_t Tf, int32_t D, const uint8_t* vad, float* Ryy, float* Rnn,
+                        void* stream) {
+  danse_batch* eng = nullptr;
+  if (!Y || !vad || !Ryy || !Rnn || B < 1 || Tf < 1 || D < 1 || D > kMaxDMax) return bfail(nullptr, "bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  // frame list from the (device) VAD: copy to the host once
+  std::vector<uint8_t> v(Tf);
+  BCHK(hipMemcpy(v.data(), vad, Tf, hipMemcpyDeviceToHost));
+  std::vector<int> fl(Tf);
+  int n = 0;
+  for (int t = 0; t < Tf; ++t)
+    if (v[t]) fl[n++] = t;
+  const int nv = n;
+  for (int t = 0; t < Tf; ++t)
+    if (!v[t]) fl[n++] = t;
+  // treat item b as scene b, bin 0 .. : map to the kernel's (s, f) with F = 513 by
+  // running bins in chunks of 513 items
+  int *dFl = nullptr, *dNv = nullptr, *dBase = nullptr;
+  HerkNode* dNode = nullptr;
+  BCHK(balloc(&dFl, Tf));
+  BCHK(balloc(&dNv, 1));
+  BCHK(balloc(&dBase, 1));
+  BCHK(balloc(&dNode, 1));
+  const int zero = 0;
+  HerkNode hn{0, D, D, 0, 0};
+  BCHK(hipMemcpy(dFl, fl.data(), Tf * sizeof(int), hipMemcpyHostToDevice));
+  BCHK(hipMemcpy(dNv, &nv, sizeof(int), hipMemcpyHostToDevice));
+  BCHK(hipMemcpy(dBase, &zero, sizeof(int), hipMemcpyHostToDevice));
+  BCHK(hipMemcpy(dNode, &hn, sizeof(HerkNode), hipMemcpyHostToDevice));
+  // the kernel indexes Y[s][f][t][c] with F = 513 bins per scene; feed items
+  // in blocks of 513 (the last block padded by re-reading item B - 1 into a
+  // scratch copy is avoided by launching with exact grids per block)
+  const cf* Yc = (const cf*)Y;
+  cf* Ry = (cf*)Ryy;
+  cf* Rn = (cf*)Rnn;
+  for (int b0 = 0; b0 < B; b0 += 513) {
+    const int nb = std::min(513, B - b0);
+    const int nt = (D + 15) / 16;
+#define DANSE_HERK1(NTV)                                                                                       \
+  hipLaunchKernelGGL(herk_kernel<NTV>, dim3(nb), dim3(64), 0, st, Yc + (size_t)b0 * Tf * D, (const cf*)nullptr, 1, 1, \
+                     D, Tf, dBase, dNode, 1, dFl, dNv, Ry + (size_t)b0 * D * D, Rn + (size_t)b0 * D * D)
+    if (nt == 1) DANSE_HERK1(1);
+    else if (nt == 2) DANSE_HERK1(2);
+    else if (nt == 3) DANSE_HERK1(3);
+    else DANSE_HERK1(4);
+#undef DANSE_HERK1
+  }
+  BCHK(hipGetLastError());
+  BCHK(hipStreamSynchronize(st));
+  (void)hipFree(dFl);
+  (void)hipFree(dNv);
+  (void)hipFree(dBase);
+  (void)hipFree(dNode);
+  return 0;
+}
+
+}  // extern "C"

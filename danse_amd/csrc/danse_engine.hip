@@ -674,26 +674,6 @@ __global__ void __launch_bounds__(256) wola_analysis_kernel(const float* x, int 
   for (int f = threadIdx.x; f < F; f += blockDim.x) out[(long long)c * F + f] = inv * o[f];
 }
 
-// Batch SCMs: Ryy = mean over VAD frames of y y^H, Rnn over the others.
-// One workgroup per batch item b; thread (i, j) accumulates over frames.
-__global__ void batch_covmats_kernel(const cf* Y, int B, int Tf, int D, const uint8_t* vad, cf* Ryy, cf* Rnn) {
-  const int b = blockIdx.x;
-  const cf* Yb = Y + (long long)b * Tf * D;
-  int nv = 0, nn = 0;
-  for (int t = 0; t < Tf; ++t) (vad[t] ? nv : nn)++;
-  for (int e = threadIdx.x; e < D * D; e += blockDim.x) {
-    const int i = e / D, j = e % D;
-    cf sy = cf{0.0f, 0.0f}, sn = cf{0.0f, 0.0f};
-    for (int t = 0; t < Tf; ++t) {
-      const cf p = mulc(Yb[(long long)t * D + i], Yb[(long long)t * D + j]);
-      if (vad[t]) sy = sy + p;
-      else sn = sn + p;
-    }
-    Ryy[((long long)b * D + i) * D + j] = (nv > 0) ? (1.0f / nv) * sy : cf{NAN, NAN};
-    Rnn[((long long)b * D + i) * D + j] = (nn > 0) ? (1.0f / nn) * sn : cf{NAN, NAN};
-  }
-}
-
 int danse_wola_analysis(const float* x, int32_t C, int32_t T, const int32_t* ends, const float* win, int32_t N,
                         int32_t Ns, float* out, void* stream) {
   danse_engine* eng = nullptr;
@@ -727,15 +707,6 @@ int danse_filter_update(const float* Ryy, const float* Rnn, int32_t B, int32_t D
   const cf* n = (const cf*)Rnn;
   cf* o = (cf*)w;
   launch_filter_update_class(DM, a, n, B, D, gevd, rank, ref, o, diag, st);
-  HIPCHK(hipGetLastError());
-  return 0;
-}
-
-int danse_batch_covmats(const float* Y, int32_t B, int32_t Tf, int32_t D, const uint8_t* vad, float* Ryy, float* Rnn,
-                        void* stream) {
-  danse_engine* eng = nullptr;
-  hipLaunchKernelGGL(batch_covmats_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, (const cf*)Y, B, Tf, D, vad,
-                     (cf*)Ryy, (cf*)Rnn);
   HIPCHK(hipGetLastError());
   return 0;
 }

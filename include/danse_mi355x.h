@@ -189,10 +189,59 @@ int danse_filter_update(const float* Ryy, const float* Rnn, int32_t B, int32_t D
                         int32_t rank, int32_t ref, float* w, int32_t* diag, void* stream);
 
 /* Batch-mode SCM contraction (update_covmats_batch, d_classes.py:3272-3304):
- * Y: [B][Tf][D] complex, vad: [Tf] uint8 -> Ryy, Rnn: [B][D][D] complex
- * (means over VAD / non-VAD frames). */
+ * Y: [B][Tf][D] complex, vad: [Tf] uint8 (device) -> Ryy, Rnn: [B][D][D]
+ * complex (means over VAD / non-VAD frames; MFMA f32 HERK). */
 int danse_batch_covmats(const float* Y, int32_t B, int32_t Tf, int32_t D, const uint8_t* vad,
                         float* Ryy, float* Rnn, void* stream);
+
+/* ---- batch-mode engine (danse_batch, d_core.py:251-352; d_batch.py) ----
+ * Replaces the reference's danse_batch(wasnObj, p): STFT of the whole
+ * signal, then maxBatchUpdates iterations of z = wExt^H y, Y.Y^H SCMs over
+ * VAD / non-VAD frames, MWF / GEVD filter update (seq: one node per
+ * iteration, asy/sim: all), external filters, dhat = w^H ytilde, ISTFT and
+ * the MMSE cost.  Fully connected, DANSE estimates only. */
+typedef struct danse_batch_cfg {
+  int32_t S;               /* scenes (same shape)                                 */
+  int32_t K;               /* nodes                                               */
+  const int32_t* M;        /* [K] sensors per node                                */
+  int32_t N, Ns, T;        /* DFT size (1024), hop, samples per channel           */
+  int32_t iters;           /* maxBatchUpdates                                     */
+  int32_t nseg;            /* STFT frames of the end-padded signal (scipy padded=True) */
+  int32_t gevd, rank, ref;
+  float alphaExt;          /* alphaExternalFilters                                */
+  const int32_t* extMode;  /* [K] enum danse_ext_mode                             */
+  const float* betaExt;    /* [S*K] external-filter forgetting factors            */
+  const float* win;        /* [N] STFT window (winWOLAanalysis)                   */
+  const uint8_t* vad;      /* [S][K][nseg] frame VAD (WASN.get_vad_per_frame)     */
+  const uint8_t* doSolve;  /* [iters][K] 1: node updates its filters this iteration */
+  const float* w0;         /* initial filters, node blocks [F][D_k] complex        */
+  const float* wExt0;      /* initial external filters (and targets), [F][M_k]     */
+  int32_t costTrim;        /* samples trimmed at both ends in the MMSE cost (1000) */
+} danse_batch_cfg;
+
+typedef struct danse_batch danse_batch;
+
+/* Outputs of danse_batch_get:
+ *   W     node k: [S][iters+1][F][D_k] complex     WEXT node k: [S][iters+1][F][M_k]
+ *   D     [S][K][T] float (last iteration)          DHAT [S][K][nseg-1][F] complex
+ *   COST  [iters][S][K] double (NaN-free only when clean signals were given) */
+enum danse_batch_output {
+  DANSE_BATCH_OUT_W = 0,
+  DANSE_BATCH_OUT_WEXT = 1,
+  DANSE_BATCH_OUT_D = 2,
+  DANSE_BATCH_OUT_DHAT = 3,
+  DANSE_BATCH_OUT_COST = 4
+};
+
+int danse_batch_create(const danse_batch_cfg* cfg, int device, danse_batch** out);
+void danse_batch_destroy(danse_batch* eng);
+const char* danse_batch_last_error(const danse_batch* eng);
+/* y: [S][sum_k M_k][T] float (device); clean: [S][K][T] float (device, the
+ * clean speech at each node's reference sensor) or NULL (no MMSE cost). */
+int danse_batch_set_inputs(danse_batch* eng, const float* y, const float* clean);
+int danse_batch_run(danse_batch* eng, void* stream);
+int danse_batch_output_bytes(danse_batch* eng, int32_t which, int32_t node, size_t* bytes);
+int danse_batch_get(danse_batch* eng, int32_t which, int32_t node, void* dst, size_t bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -15,7 +15,7 @@ import ctypes
 import numpy as np
 import pytest
 
-from golden_cases import ONLINE_CASES, KAT_CASES, kat_inputs
+from golden_cases import ONLINE_CASES, BATCH_CASES, KAT_CASES, kat_inputs
 from _util import make_case_params, make_case_scene, rel_err
 
 pytestmark = pytest.mark.gpu
@@ -183,6 +183,49 @@ def test_online_engine_large_D(case):
     st, de = _compare_online(case, dv, ov)
     assert st['median'] <= 1e-4 and st['p99'] <= 1e-3, st
     assert de <= 1e-4
+
+
+@pytest.mark.parametrize('case', BATCH_CASES, ids=lambda c: c['name'])
+def test_batch_engine_vs_oracle(case, golden_dir):
+    """Device batch DANSE (MFMA Y.Y^H, STFT / ISTFT, MMSE cost) against the
+    float64 oracle and the reference's own fixture."""
+    from danse_amd.core import danse_batch
+    from oracle import danse_ref_cpu as O
+    sc = make_case_scene(case)
+    dp, wp = make_case_params(case)
+    sc.get_vad_per_frame(dp.DFTsize, dp.Ns, wp.vadMinProportionActive)
+    out, _ = danse_batch(sc, dp)
+    ov = O.danse_batch(sc, dp, vadMinProp=wp.vadMinProportionActive)
+    nb = case['danse']['maxBatchUpdates'] + 1
+    errs = [_bin_rel(out.wTilde[k][:, 1:nb, :], ov.wTilde[k][:, 1:nb, :]).ravel() for k in range(len(case['M']))]
+    st = _stats(np.concatenate(errs))
+    de = rel_err(out.d, ov.d)
+    ce = float(np.max(np.abs(out.mmseCost - np.array(ov.mmseCost, dtype=float)) / np.abs(np.array(ov.mmseCost, dtype=float))))
+    g = np.load(golden_dir / f"{case['name']}.npz")
+    print(case['name'], 'w', st, 'd', de, 'cost', ce, 'd vs golden', rel_err(out.d, g['d']))
+    assert st['median'] <= 1e-5 and st['p99'] <= 1e-4, st
+    assert de <= 1e-4 and ce <= 1e-4
+
+
+def test_batch_covmats_op():
+    """danse_batch_covmats (MFMA HERK) on random observations vs numpy."""
+    L, lib = _lib()
+    rng = np.random.default_rng(5)
+    for (B, Tf, D) in [(7, 37, 5), (600, 50, 11), (3, 21, 39)]:
+        Y = rng.standard_normal((B, Tf, D)) + 1j * rng.standard_normal((B, Tf, D))
+        vad = (rng.random(Tf) > 0.4).astype(np.uint8)
+        yd, vd = _dev_cf(Y), torch.from_numpy(vad).cuda()
+        ry = torch.empty((B, D, D, 2), dtype=torch.float32, device='cuda')
+        rn = torch.empty_like(ry)
+        L.check(lib.danse_batch_covmats(ctypes.c_void_p(yd.data_ptr()), B, Tf, D, ctypes.c_void_p(vd.data_ptr()),
+                                        ctypes.c_void_p(ry.data_ptr()), ctypes.c_void_p(rn.data_ptr()), None))
+        torch.cuda.synchronize()
+        v = vad.astype(bool)
+        refy = np.mean(np.einsum('btj,btl->btjl', Y[:, v], Y[:, v].conj()), axis=1)
+        refn = np.mean(np.einsum('btj,btl->btjl', Y[:, ~v], Y[:, ~v].conj()), axis=1)
+        gy = ry.cpu().numpy().view(np.complex64)[..., 0]
+        gn = rn.cpu().numpy().view(np.complex64)[..., 0]
+        assert rel_err(gy, refy) < 2e-6 and rel_err(gn, refn) < 2e-6, (B, Tf, D, rel_err(gy, refy), rel_err(gn, refn))
 
 
 def test_batched_scenes_are_independent():
