@@ -93,3 +93,33 @@ def kat_inputs(case):
         yy = 1 / D * np.einsum('ij,ik->ijk', n2 + s, (n2 + s).conj())
         Ryy = beta * Ryy + (1 - beta) * yy
     return Ryy, Rnn
+
+
+# DXCP-PhaT sampling-rate-offset estimator (dxcpphat/sro_estimation.py,
+# DXCPPhaT with default parameters): two channels of one band-limited
+# multi-sine source, channel 2 sampled at (1 + sro 1e-6) fs with a delay.
+DXCP_CASES = [
+    dict(name='dxcp_sro100', dur=14.0, sro=100.0, delay=3.5, seed=31),
+    dict(name='dxcp_sro_m60', dur=12.0, sro=-60.0, delay=-7.25, seed=32),
+    dict(name='dxcp_sro200', dur=10.0, sro=200.0, delay=0.0, seed=33),
+]
+
+
+def dxcp_inputs(case, fs=16000.0):
+    """Exact evaluation of a random multi-sine at each channel's sample
+    instants (no resampler needed), plus independent sensor noise."""
+    rng = np.random.default_rng(case['seed'])
+    n = int(case['dur'] * fs)
+    f = rng.uniform(100.0, 7000.0, 120)
+    a = rng.uniform(0.2, 1.0, 120)
+    ph = rng.uniform(0.0, 2 * np.pi, 120)
+    t1 = np.arange(n) / fs
+    t2 = (np.arange(n) * (1.0 + case['sro'] * 1e-6) + case['delay']) / fs
+    x1 = np.zeros(n)
+    x2 = np.zeros(n)
+    for i in range(120):
+        x1 += a[i] * np.cos(2 * np.pi * f[i] * t1 + ph[i])
+        x2 += a[i] * np.cos(2 * np.pi * f[i] * t2 + ph[i])
+    x1 += 0.05 * rng.standard_normal(n)
+    x2 += 0.05 * rng.standard_normal(n)
+    return x1.astype(np.float32).astype(np.float64), x2.astype(np.float32).astype(np.float64)

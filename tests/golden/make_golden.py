@@ -23,6 +23,7 @@ sys.path.insert(0, str(HERE))
 import _refharness as H  # noqa: E402
 from danse_amd.scene import make_scene, scene_digest  # noqa: E402
 from golden_cases import ONLINE_CASES, BATCH_CASES, SRO_EVENT_CASES, KAT_CASES, kat_inputs  # noqa: E402
+from golden_cases import DXCP_CASES, dxcp_inputs  # noqa: E402
 
 
 def _run_online(ns, case):
@@ -102,13 +103,29 @@ def _run_kat(ns, case):
     return {'w': w}
 
 
+def _run_dxcp(ns, case):
+    import sro_estimation   # dxcpphat/, on sys.path once the reference is loaded (d_sros.py:12)
+    x1, x2 = dxcp_inputs(case)
+    est = sro_estimation.DXCPPhaT()
+    n = len(x1) // 2048
+    sro = np.zeros(n)
+    sto = np.zeros(n)
+    for i in range(n):
+        fr = np.stack((x1[i * 2048:(i + 1) * 2048], x2[i * 2048:(i + 1) * 2048]), axis=1)
+        out = est.process_data(fr)
+        sro[i] = out['SROppm_est_out']
+        sto[i] = out['STOsmp_est_out']
+    return {'sro': sro, 'sto': sto}
+
+
 def main():
     ns = H.load()
     only = sys.argv[1:]
     jobs = [('online', c, _run_online) for c in ONLINE_CASES] + \
            [('batch', c, _run_batch) for c in BATCH_CASES] + \
            [('events', c, _run_sro_events) for c in SRO_EVENT_CASES] + \
-           [('kat', c, _run_kat) for c in KAT_CASES]
+           [('kat', c, _run_kat) for c in KAT_CASES] + \
+           [('dxcp', c, _run_dxcp) for c in DXCP_CASES]
     for kind, case, fn in jobs:
         name = case['name']
         if only and name not in only:

@@ -3,7 +3,7 @@ the reference itself (tests/golden/make_golden.py).  CPU only."""
 import numpy as np
 import pytest
 
-from golden_cases import ONLINE_CASES, BATCH_CASES, SRO_EVENT_CASES, KAT_CASES, kat_inputs
+from golden_cases import ONLINE_CASES, BATCH_CASES, SRO_EVENT_CASES, KAT_CASES, DXCP_CASES, kat_inputs
 from danse_amd.scene import scene_digest
 from danse_amd.scheduler import initialize_events
 from oracle import danse_ref_cpu as O
@@ -88,3 +88,21 @@ def test_filter_update_kat(case, golden_dir):
     fn = O.update_w_gevd if case['gevd'] else O.update_w
     w = fn(Ryy, Rnn, refSensorIdx=case['ref'], rank=case['rank'])
     assert rel_err(w, g['w']) < 1e-12
+
+
+@pytest.mark.parametrize('case', DXCP_CASES, ids=[c['name'] for c in DXCP_CASES])
+def test_dxcp_oracle_matches_reference(case, golden_dir):
+    """DXCP-PhaT restatement (oracle/dxcp_ref.py) against the reference's
+    DXCPPhaT run on the same two-channel input: identical per-frame SRO and
+    STO estimates."""
+    import warnings
+    from golden_cases import dxcp_inputs
+    from oracle import dxcp_ref as D
+    g = _load(golden_dir, case['name'])
+    x1, x2 = dxcp_inputs(case)
+    with warnings.catch_warnings():
+        warnings.simplefilter('ignore', DeprecationWarning)
+        sro, sto = D.run(x1, x2)
+    assert np.max(np.abs(sro - g['sro'])) <= 1e-9
+    assert np.max(np.abs(sto - g['sto'])) <= 1e-9
+    assert abs(sro[-1] - case['sro']) < 1.0     # converged estimate
