@@ -90,6 +90,10 @@ SIGNATURES = {
     'danse_batch_run': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p]),
     'danse_batch_output_bytes': (_c_i32, [ctypes.c_void_p, _c_i32, _c_i32, ctypes.POINTER(ctypes.c_size_t)]),
     'danse_batch_get': (_c_i32, [ctypes.c_void_p, _c_i32, _c_i32, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    'danse_dxcp_create': (_c_i32, [_c_i32, _c_i32, ctypes.POINTER(ctypes.c_void_p)]),
+    'danse_dxcp_destroy': (None, [ctypes.c_void_p]),
+    'danse_dxcp_last_error': (ctypes.c_char_p, [ctypes.c_void_p]),
+    'danse_dxcp_process': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
 }
 
 _lib = None

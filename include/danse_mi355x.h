@@ -243,6 +243,18 @@ int danse_batch_run(danse_batch* eng, void* stream);
 int danse_batch_output_bytes(danse_batch* eng, int32_t which, int32_t node, size_t* bytes);
 int danse_batch_get(danse_batch* eng, int32_t which, int32_t node, void* dst, size_t bytes, void* stream);
 
+/* ---- DXCP-PhaT sampling-rate-offset estimator (dxcpphat/sro_estimation.py:
+ * 130-345, class DXCPPhaT with its default parameters: fs 16 kHz, 2048-sample
+ * frames, 8192-point FFT, 5 s accumulation), batched over P node pairs.
+ * danse_dxcp_process() is one process_data() call of every pair:
+ *   x:   [P][2][2048] float (device): the two channels' next frame
+ *   out: [P][2] double (device): SROppm_est_out, STOsmp_est_out after it. */
+typedef struct danse_dxcp danse_dxcp;
+int danse_dxcp_create(int32_t P, int device, danse_dxcp** out);
+void danse_dxcp_destroy(danse_dxcp* eng);
+const char* danse_dxcp_last_error(const danse_dxcp* eng);
+int danse_dxcp_process(danse_dxcp* eng, const float* x, double* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

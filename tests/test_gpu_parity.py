@@ -228,6 +228,34 @@ def test_batch_covmats_op():
         assert rel_err(gy, refy) < 2e-6 and rel_err(gn, refn) < 2e-6, (B, Tf, D, rel_err(gy, refy), rel_err(gn, refn))
 
 
+def test_dxcp_vs_oracle():
+    """Device DXCP-PhaT (batched pairs) against the float64 oracle, itself
+    pinned bit-exactly to the reference's DXCPPhaT: per-frame SRO within
+    0.05 ppm and STO within 0.05 samples, all three golden cases in one batch."""
+    import warnings
+    from golden_cases import DXCP_CASES, dxcp_inputs
+    from danse_amd.dxcp import DXCPPhaTBatch
+    from oracle import dxcp_ref as D
+    ins = [dxcp_inputs(c) for c in DXCP_CASES]
+    n = min(len(a) for a, _ in ins) // 2048
+    est = DXCPPhaTBatch(len(DXCP_CASES))
+    got = np.zeros((n, len(DXCP_CASES), 2))
+    for i in range(n):
+        fr = np.stack([np.stack((a[i * 2048:(i + 1) * 2048], b[i * 2048:(i + 1) * 2048])) for a, b in ins])
+        sro, sto = est.process_frames(fr)
+        got[i, :, 0] = sro.cpu().numpy()
+        got[i, :, 1] = sto.cpu().numpy()
+    est.close()
+    for c, (a, b) in zip(DXCP_CASES, ins):
+        j = DXCP_CASES.index(c)
+        with warnings.catch_warnings():
+            warnings.simplefilter('ignore', DeprecationWarning)
+            sro_o, sto_o = D.run(a[:n * 2048], b[:n * 2048])
+        es, et = np.max(np.abs(got[:, j, 0] - sro_o)), np.max(np.abs(got[:, j, 1] - sto_o))
+        print(c['name'], 'max |dSRO| ppm', es, 'max |dSTO|', et, 'final', got[-1, j])
+        assert es <= 0.05 and et <= 0.05, (c['name'], es, et)
+
+
 def test_batched_scenes_are_independent():
     """S scenes in one engine give the same results as one scene alone."""
     from danse_amd.core import danse_multi
