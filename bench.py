@@ -253,7 +253,7 @@ def main():
                        'rounds': R, 'shard': shard, 'gevd_rank': 1, 'graph': not args.no_graph},
             'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': achieved / HBM_PEAK_GBS,
-                         'traffic': None if traffic is None else traffic['bytes_per_launch'],
+                         'traffic': (traffic or {}).get('bytes_per_launch'),
                          'traffic_detail': traffic,
                          'kernel': 'update_kernel', 'avg_launch_ms': avg_ms,
                          'alg_bytes_per_launch': float(byts.mean())},

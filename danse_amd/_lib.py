@@ -94,6 +94,13 @@ SIGNATURES = {
     'danse_dxcp_destroy': (None, [ctypes.c_void_p]),
     'danse_dxcp_last_error': (ctypes.c_char_p, [ctypes.c_void_p]),
     'danse_dxcp_process': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    'danse_tz_create': (_c_i32, [_c_i32, ctypes.c_void_p, ctypes.c_void_p, _c_i32, _c_i32,
+                                 ctypes.POINTER(ctypes.c_void_p)]),
+    'danse_tz_destroy': (None, [ctypes.c_void_p]),
+    'danse_tz_last_error': (ctypes.c_char_p, [ctypes.c_void_p]),
+    'danse_tz_ir': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p, _c_i32, _c_i32, ctypes.c_void_p, ctypes.c_void_p]),
+    'danse_tz_compress': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, _c_i32, _c_i32, _c_i32,
+                                   ctypes.c_void_p, ctypes.c_void_p]),
 }
 
 _lib = None

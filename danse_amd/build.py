@@ -1,8 +1,8 @@
 """In-tree build of the HIP extension (gfx950): ``libdanse_mi355x.so``.
 
 ``hipcc -c -fPIC`` of ``csrc/danse_engine.hip`` (online engine, C-ABI, bcast /
-operator kernels), ``csrc/batch.hip`` (batch-mode engine), ``csrc/dxcp.hip``
-(DXCP-PhaT SRO estimator) and of
+operator kernels), ``csrc/batch.hip`` (batch-mode engine), ``csrc/dxcp.hip`` (DXCP-PhaT SRO
+estimator), ``csrc/tz.hip`` (T(z) few-samples compression) and of
 ``csrc/update_class.hip`` once per filter-size class
 (``-DDANSE_DMAX=N``, N = 1..16 and 24..64 in steps of 8, see
 ``csrc/classes.hpp``), in parallel, then one
@@ -30,7 +30,7 @@ FLAGS = ['--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC']
 def _units():
     """(object name, source, extra flags) of every translation unit."""
     u = [('danse_engine.o', CSRC / 'danse_engine.hip', []), ('batch.o', CSRC / 'batch.hip', []),
-         ('dxcp.o', CSRC / 'dxcp.hip', [])]
+         ('dxcp.o', CSRC / 'dxcp.hip', []), ('tz.o', CSRC / 'tz.hip', [])]
     for n in CLASSES:
         u.append((f'update_d{n}.o', CSRC / 'update_class.hip', [f'-DDANSE_DMAX={n}']))
     return u

@@ -255,6 +255,27 @@ void danse_dxcp_destroy(danse_dxcp* eng);
 const char* danse_dxcp_last_error(const danse_dxcp* eng);
 int danse_dxcp_process(danse_dxcp* eng, const float* x, double* out, void* stream);
 
+/* ---- T(z) few-samples compression (broadcastType 'fewSamples').
+ * danse_tz_create: analysis window h, synthesis window f (N floats, host), the
+ *   WOLA shift R (= Ns); N = 1024.
+ * danse_tz_ir replaces dist_fct_approx(wHat, h, f, R) (danse_toolbox/
+ *   d_base.py:1941-1991) for B filters at once:
+ *     wHat: [B][N/2+1][M] complex float (device; the reference's wqqHat layout)
+ *     wIR:  [B][2N-1][M] float (device; the reference's wIR layout).
+ * danse_tz_compress replaces the convolution of danse_compression_few_samples
+ *   (d_base.py:1871-1938, extract_few_samples_from_convolution 1538-1566):
+ *     yq:   [B][N][M] float (device; each node's local frame ykFrame)
+ *     wIR:  [B][2N-1][M] float (device)
+ *     z:    [B][L] float (device): the last L samples of the T(z)-filtered
+ *           frame summed over the node's sensors (zq), 1 <= L <= N. */
+typedef struct danse_tz danse_tz;
+int danse_tz_create(int32_t N, const float* h, const float* f, int32_t R, int device, danse_tz** out);
+void danse_tz_destroy(danse_tz* eng);
+const char* danse_tz_last_error(const danse_tz* eng);
+int danse_tz_ir(danse_tz* eng, const float* wHat, int32_t B, int32_t M, float* wIR, void* stream);
+int danse_tz_compress(danse_tz* eng, const float* yq, const float* wIR, int32_t B, int32_t M, int32_t L, float* z,
+                      void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -12,8 +12,8 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -v -s --timeout 120 --time
 tail -3 gpurun_out/pytest_gpu_$TAG.log
 timeout -k 10 600 python bench.py $BENCH_ARGS > gpurun_out/bench_$TAG.log 2>&1 || { echo "bench failed"; tail -30 gpurun_out/bench_$TAG.log; exit 1; }
 tail -2 gpurun_out/bench_$TAG.log
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o kt --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/prof_$TAG.log 2>&1 || { echo "rocprof kt failed"; tail -30 gpurun_out/prof_$TAG.log; exit 1; }
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch_$TAG -o pmc --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-graph > gpurun_out/pmc_fetch_$TAG.log 2>&1 || { echo "pmc fetch failed"; tail -30 gpurun_out/pmc_fetch_$TAG.log; exit 1; }
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write_$TAG -o pmc --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-graph > gpurun_out/pmc_write_$TAG.log 2>&1 || { echo "pmc write failed"; tail -30 gpurun_out/pmc_write_$TAG.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o kt --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-traffic > gpurun_out/prof_$TAG.log 2>&1 || { echo "rocprof kt failed"; tail -30 gpurun_out/prof_$TAG.log; exit 1; }
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch_$TAG -o pmc --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-graph --no-traffic > gpurun_out/pmc_fetch_$TAG.log 2>&1 || { echo "pmc fetch failed"; tail -30 gpurun_out/pmc_fetch_$TAG.log; exit 1; }
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write_$TAG -o pmc --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-graph --no-traffic > gpurun_out/pmc_write_$TAG.log 2>&1 || { echo "pmc write failed"; tail -30 gpurun_out/pmc_write_$TAG.log; exit 1; }
 find gpurun_out -name "*.csv" | head -50
 echo done

@@ -123,3 +123,35 @@ def dxcp_inputs(case, fs=16000.0):
     x1 += 0.05 * rng.standard_normal(n)
     x2 += 0.05 * rng.standard_normal(n)
     return x1.astype(np.float32).astype(np.float64), x2.astype(np.float32).astype(np.float64)
+
+
+# T(z) few-samples compression KATs: dist_fct_approx +
+# danse_compression_few_samples on seeded filters / frames.  'win' picks the
+# analysis / synthesis windows: 'sqrthann' (the default DANSE windows) or
+# 'rand' (independent positive random windows: exercises the asymmetric
+# window correlation).  'update' False feeds the Dirac initial IR of
+# d_classes.py:660-663 as wIRprevious.
+TZ_CASES = [
+    dict(name='tz_m2_L64', M=2, L=64, N=1024, Ns=512, win='sqrthann', update=True, seed=41),
+    dict(name='tz_m3_L512', M=3, L=512, N=1024, Ns=512, win='sqrthann', update=True, seed=42),
+    dict(name='tz_m1_L1', M=1, L=1, N=1024, Ns=512, win='rand', update=True, seed=43),
+    dict(name='tz_m4_L128_dirac', M=4, L=128, N=1024, Ns=512, win='sqrthann', update=False, seed=44),
+]
+
+
+def tz_inputs(case):
+    """(wHat [N/2+1, M] complex, yq [N, M], h, f, wIRprevious [2N-1, M])."""
+    rng = np.random.default_rng(case['seed'])
+    N, M = case['N'], case['M']
+    F = N // 2 + 1
+    wHat = rng.standard_normal((F, M)) + 1j * rng.standard_normal((F, M))
+    yq = rng.standard_normal((N, M))
+    if case['win'] == 'sqrthann':
+        h = np.sqrt(np.hanning(N))
+        f = h.copy()
+    else:
+        h = rng.uniform(0.1, 1.0, N)
+        f = rng.uniform(0.1, 1.0, N)
+    wPrev = np.zeros((2 * N - 1, M))
+    wPrev[N, 0] = 1.0
+    return wHat, yq, h, f, wPrev

@@ -23,7 +23,7 @@ sys.path.insert(0, str(HERE))
 import _refharness as H  # noqa: E402
 from danse_amd.scene import make_scene, scene_digest  # noqa: E402
 from golden_cases import ONLINE_CASES, BATCH_CASES, SRO_EVENT_CASES, KAT_CASES, kat_inputs  # noqa: E402
-from golden_cases import DXCP_CASES, dxcp_inputs  # noqa: E402
+from golden_cases import DXCP_CASES, dxcp_inputs, TZ_CASES, tz_inputs  # noqa: E402
 
 
 def _run_online(ns, case):
@@ -118,6 +118,13 @@ def _run_dxcp(ns, case):
     return {'sro': sro, 'sto': sto}
 
 
+def _run_tz(ns, case):
+    wHat, yq, h, f, wPrev = tz_inputs(case)
+    z, wIR = ns.base.danse_compression_few_samples(yq, wHat, case['L'], wPrev, h, f, case['Ns'],
+                                                   updateBroadcastFilter=case['update'])
+    return {'z': z, 'wIR': wIR}
+
+
 def main():
     ns = H.load()
     only = sys.argv[1:]
@@ -125,7 +132,8 @@ def main():
            [('batch', c, _run_batch) for c in BATCH_CASES] + \
            [('events', c, _run_sro_events) for c in SRO_EVENT_CASES] + \
            [('kat', c, _run_kat) for c in KAT_CASES] + \
-           [('dxcp', c, _run_dxcp) for c in DXCP_CASES]
+           [('dxcp', c, _run_dxcp) for c in DXCP_CASES] + \
+           [('tz', c, _run_tz) for c in TZ_CASES]
     for kind, case, fn in jobs:
         name = case['name']
         if only and name not in only:

@@ -256,6 +256,55 @@ def test_dxcp_vs_oracle():
         assert es <= 0.05 and et <= 0.05, (c['name'], es, et)
 
 
+def test_tz_few_samples_vs_reference_fixtures():
+    """T(z) few-samples compression through the reference-shaped drop-ins
+    (danse_amd.tz.dist_fct_approx / danse_compression_few_samples) against the
+    reference's own outputs (tz_* fixtures): relative error <= 1e-5 on the
+    IR and on the broadcast samples."""
+    from golden_cases import TZ_CASES, tz_inputs
+    from danse_amd import tz
+    from pathlib import Path
+    gdir = Path(__file__).resolve().parent / 'golden'
+    for c in TZ_CASES:
+        g = dict(np.load(gdir / f"{c['name']}.npz", allow_pickle=False))
+        wHat, yq, h, f, wPrev = tz_inputs(c)
+        z, wIR = tz.danse_compression_few_samples(yq, wHat, c['L'], wPrev, h, f, c['Ns'],
+                                                  updateBroadcastFilter=c['update'])
+        ew, ez = rel_err(wIR, g['wIR']), rel_err(z, g['z'])
+        print(c['name'], 'wIR', ew, 'z', ez)
+        assert ew < 1e-5 and ez < 1e-5, (c['name'], ew, ez)
+
+
+@pytest.mark.parametrize('M,L', [(1, 1), (2, 7), (3, 100), (4, 512), (5, 1024), (9, 333)])
+def test_tz_batched_vs_oracle(M, L):
+    """B = 37 nodes per launch (TZCompressor) against the float64 oracle
+    (closed-form IR, itself pinned to the reference's dist_fct_approx), ragged
+    L (not a multiple of the 8-output tile) and M above the 4-sensor LDS pass."""
+    from danse_amd.tz import TZCompressor
+    from oracle import tz_ref as T
+    rng = np.random.default_rng(1000 + 10 * M + L)
+    N, B = 1024, 37
+    h = np.sqrt(np.hanning(N))
+    f = rng.uniform(0.2, 1.0, N)
+    wHat = rng.standard_normal((B, N // 2 + 1, M)) + 1j * rng.standard_normal((B, N // 2 + 1, M))
+    yq = rng.standard_normal((B, N, M))
+    c = TZCompressor(h, f, 512)
+    wIR = c.ir(wHat)
+    z = c.compress(yq, wIR, L).cpu().numpy()
+    wIRh = wIR.cpu().numpy()
+    c.close()
+    for b in range(B):
+        ref_ir = T.dist_fct_approx_closed(wHat[b], h.astype(np.float32).astype(np.float64),
+                                          f.astype(np.float32).astype(np.float64), 512)
+        assert rel_err(wIRh[b], ref_ir) < 1e-5, (b, rel_err(wIRh[b], ref_ir))
+        # the convolution on the device's own IR: isolates the compress kernel
+        zr = np.zeros(L)
+        for m in range(M):
+            zr += T.extract_few_samples_from_convolution(np.arange(2 * N - 1 - L + 1, 2 * N), wIRh[b, :, m].astype(np.float64),
+                                                         yq[b, :, m].astype(np.float32).astype(np.float64))
+        assert rel_err(z[b], zr) < 1e-5, (b, rel_err(z[b], zr))
+
+
 def test_batched_scenes_are_independent():
     """S scenes in one engine give the same results as one scene alone."""
     from danse_amd.core import danse_multi

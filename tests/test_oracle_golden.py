@@ -3,7 +3,7 @@ the reference itself (tests/golden/make_golden.py).  CPU only."""
 import numpy as np
 import pytest
 
-from golden_cases import ONLINE_CASES, BATCH_CASES, SRO_EVENT_CASES, KAT_CASES, DXCP_CASES, kat_inputs
+from golden_cases import ONLINE_CASES, BATCH_CASES, SRO_EVENT_CASES, KAT_CASES, DXCP_CASES, TZ_CASES, kat_inputs
 from danse_amd.scene import scene_digest
 from danse_amd.scheduler import initialize_events
 from oracle import danse_ref_cpu as O
@@ -106,3 +106,20 @@ def test_dxcp_oracle_matches_reference(case, golden_dir):
     assert np.max(np.abs(sro - g['sro'])) <= 1e-9
     assert np.max(np.abs(sto - g['sto'])) <= 1e-9
     assert abs(sro[-1] - case['sro']) < 1.0     # converged estimate
+
+
+@pytest.mark.parametrize('case', TZ_CASES, ids=[c['name'] for c in TZ_CASES])
+def test_tz_oracle_matches_reference(case, golden_dir):
+    """T(z) few-samples restatement (oracle/tz_ref.py) against the
+    reference's dist_fct_approx + danse_compression_few_samples; the closed
+    form IR (the one the device computes) against the literal restatement."""
+    from golden_cases import tz_inputs
+    from oracle import tz_ref as T
+    g = _load(golden_dir, case['name'])
+    wHat, yq, h, f, wPrev = tz_inputs(case)
+    z, wIR = T.danse_compression_few_samples(yq, wHat, case['L'], wPrev, h, f, case['Ns'],
+                                             updateBroadcastFilter=case['update'])
+    assert rel_err(wIR, g['wIR']) < TOL
+    assert rel_err(z, g['z']) < TOL
+    if case['update']:
+        assert rel_err(T.dist_fct_approx_closed(wHat, h, f, case['Ns']), g['wIR']) < TOL
