@@ -389,6 +389,16 @@ class OnlineDANSE:
         self.lastExtFiltUp = np.zeros(K)
         self.nSensorsNeighborsCentr = [[self.M[q] for q in range(K) if q != k] for k in range(K)]
         self.startRound = np.full(K, -1)
+        # fewSamples broadcasting state (d_classes.py:522, 658-663, 828-831):
+        # T(z) IR initialised as a Dirac at tap N (not N - 1) on the reference sensor
+        self.lastBroadcastInstant = np.zeros(K)
+        self.lastTDfilterUp = np.zeros(K)
+        self.timeInstants = np.stack([nd.timeStamps for nd in self.scene.wasn], axis=1)
+        self.wIR = []
+        for k in range(K):
+            wt = np.zeros((2 * self.N - 1, self.M[k]))
+            wt[self.N, p.referenceSensor] = 1
+            self.wIR.append(wt)
 
     # ---- driver (d_core.py:66-90) ----
     def run(self):
@@ -422,23 +432,61 @@ class OnlineDANSE:
         idxEnd = int(np.floor(tCurr * fs))
         ykFrame, _, _ = local_chunk(self.yin[k], idxEnd, self.N)
         if p.computeCentralised:
-            self.yLocalCentr[k] = ykFrame
-        if p.broadcastType != 'wholeChunk':
-            raise NotImplementedError('fewSamples broadcast in the oracle')
-        _, self.zLocal[k] = compression_whole_chunk(
-            ykFrame, self.wExt[k][:, self.i[k], :], self.h, self.f, self.zLocal[k], self.Ns)
-        self.zFullTD[k] = np.concatenate((self.zFullTD[k], self.zLocal[k][:self.Ns]))
-        n = self.Ns
-        chunk = self.zLocal[k][:n]
+            # pre_fill_buffers_centralised (d_classes.py:1162-1183)
+            if p.broadcastType == 'wholeChunk':
+                self.yLocalCentr[k] = ykFrame
+            elif p.efficientSpSBC:
+                self.yLocalCentr[k] = ykFrame[-self._bc_size(k, tCurr):, :]
+            else:
+                raise NotImplementedError('centralised fewSamples without efficientSpSBC (reference raises too)')
+        if p.broadcastType == 'wholeChunk':
+            _, self.zLocal[k] = compression_whole_chunk(
+                ykFrame, self.wExt[k][:, self.i[k], :], self.h, self.f, self.zLocal[k], self.Ns)
+            self.zFullTD[k] = np.concatenate((self.zFullTD[k], self.zLocal[k][:self.Ns]))
+            chunk = self.zLocal[k][:self.Ns]
+            n = self.Ns
+        elif p.broadcastType == 'fewSamples':
+            # d_classes.py:1090-1125: IR refresh every upTDfilterEvery seconds,
+            # currL = L floor(samples since last broadcast / L) (efficientSpSBC)
+            from . import tz_ref
+            upd = False
+            if np.abs(tCurr - self.lastTDfilterUp[k]) >= p.upTDfilterEvery:
+                if not (p.noFusionAtSingleSensorNodes and self.M[k] == 1):
+                    upd = True
+                self.lastTDfilterUp[k] = tCurr
+            if p.efficientSpSBC:
+                currL = self._bc_size(k, tCurr)
+                self.lastBroadcastInstant[k] = tCurr
+            else:
+                currL = int(p.broadcastLength)
+            self.zLocal[k], self.wIR[k] = tz_ref.danse_compression_few_samples(
+                ykFrame, self.wExt[k][:, self.i[k], :], currL, self.wIR[k], self.h, self.f, self.Ns,
+                updateBroadcastFilter=upd)
+            n = -currL
+            chunk = self.zLocal[k][n:] if currL > 0 else np.array([])
+        else:
+            raise ValueError(p.broadcastType)
+        # fill_buffers / fill_buffers_centr (d_classes.py:1185-1250)
         for q in self.neighbors[k]:
             idx = self.neighbors[q].index(k)
             self.zBuffer[q][idx] = np.concatenate((self.zBuffer[q][idx], chunk), axis=0)
         if p.computeCentralised:
-            ych = self.yLocalCentr[k][:n, :]
+            if n > 0:
+                ych = self.yLocalCentr[k][:n, :]
+            elif n < 0:
+                ych = self.yLocalCentr[k][n:, :]
+            else:
+                ych = np.empty((0, self.M[k]))
             for q in range(self.K):
                 if q != k:
                     idx = k if k < q else k - 1
                     self.yBufferCentr[q][idx] = np.concatenate((self.yBufferCentr[q][idx], ych), axis=0)
+
+    def _bc_size(self, k, tCurr):
+        """``get_buffer_size_for_efficient_bc`` (d_classes.py:1130-1160)."""
+        L_ = int(self.p.broadcastLength)
+        n = np.sum((self.timeInstants[:, k] > self.lastBroadcastInstant[k]) & (self.timeInstants[:, k] <= tCurr))
+        return int(L_ * np.floor(n / L_))
 
     # ---- process_incoming_signals_buffers (d_classes.py:1701-1807) ----
     def _process_buffers(self, k):
@@ -522,7 +570,8 @@ class OnlineDANSE:
         if k == p.referenceSensor and self.nInternalFilterUps[k] == 0:
             self.firstDANSEupdateRefSensor = tCurr
         self._process_buffers(k)
-        idxEnd = int(np.floor(tCurr * fs)) - (N - Ns)
+        # local_chunk_for_update (d_base.py:1427-1479): WOLA lag N - Ns for wholeChunk only
+        idxEnd = int(np.floor(tCurr * fs)) - ((N - Ns) if p.broadcastType == 'wholeChunk' else 0)
         yLoc, self.idxBeg, self.idxEnd = local_chunk(self.yin[k], idxEnd, N)
         # build_ytilde (1893-1934)
         yT = np.concatenate((yLoc, self.z[k]), axis=1)

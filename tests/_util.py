@@ -29,5 +29,8 @@ def make_case_scene(case, **kw):
 def rel_err(a, b):
     a = np.asarray(a)
     b = np.asarray(b)
+    assert a.shape == b.shape, (a.shape, b.shape)
+    if b.size == 0:
+        return 0.0
     den = np.max(np.abs(b))
     return float(np.max(np.abs(a - b)) / (den if den > 0 else 1.0))

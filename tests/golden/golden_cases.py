@@ -48,6 +48,18 @@ ONLINE_CASES = [
                   computeLocal=True)),
     dict(name='online_C_sro_noflags_seq', M=[2, 2, 2, 2], dur=3.0, seed=9, sros=[50, 0, 200, 120],
          danse=_d(BATTERY, nodeUpdating='seq', compensateSROs=True, includeFSDflags=False, estimateSROs='Oracle')),
+    # config E shape (tests/battery20230919_perf_asfctofL.py:14-110): MK = [2, 3],
+    # broadcastType 'fewSamples' with efficientSpSBC (T(z) compression, L-sample
+    # broadcasts, IR refresh every upTDfilterEvery = 1 s; d_classes.py:1090-1160,
+    # d_base.py:837-863, 1871-1991); 2.5 s so the IR is refreshed twice
+    dict(name='online_E_fs_L64_asy', M=[2, 3], dur=2.5, seed=10,
+         danse=_d(BATTERY, nodeUpdating='asy', broadcastType='fewSamples', broadcastLength=64,
+                  computeLocal=True, computeCentralised=True)),
+    dict(name='online_E_fs_L128_sro_comp', M=[2, 3], dur=2.5, seed=11, sros=[0, 200],
+         danse=_d(BATTERY, nodeUpdating='asy', broadcastType='fewSamples', broadcastLength=128,
+                  compensateSROs=True, includeFSDflags=True, estimateSROs='Oracle', computeLocal=True)),
+    dict(name='online_E_fs_L1_seq', M=[2, 3, 1], dur=2.5, seed=12,
+         danse=_d(BATTERY, nodeUpdating='seq', broadcastType='fewSamples', broadcastLength=1)),
 ]
 
 BATCH_CASES = [
