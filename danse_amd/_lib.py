@@ -40,6 +40,7 @@ class DanseCfg(ctypes.Structure):
         ('w0', _p_f32), ('wExt0', _p_f32), ('wExtTarget0', _p_f32), ('scmInit', _p_f32),
         ('keepHistory', _c_i32),
         ('zLag', _p_u8), ('zPhase', ctypes.POINTER(ctypes.c_double)),
+        ('fsTab', _p_i32), ('zStreamLen', _c_i32),
     ]
 
 

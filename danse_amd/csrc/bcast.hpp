@@ -40,7 +40,9 @@ struct BcastArgs {
   cf* Yspec;               // [2][S][MT][F]
   cf* Zspec;               // [2][K][S][F] (slot r & 1)
   float* zPrev;            // [S][K][N]
-  float* zStream;          // [S][K][R*Ns]
+  float* zStream;          // [S][K][zLen]
+  int zLen;                // samples per node stream (R*Ns for wholeChunk)
+  const int* fsTab;        // fewSamples: [R][K][DANSE_FS_FIELDS] (null: wholeChunk)
   const cf* wExtHist;      // per scene block (stride wExtStride) : node offsets wExtNodeOff
   const long long* wExtNodeOff;  // [K]
   long long wExtStride;
@@ -141,7 +143,28 @@ __global__ void __launch_bounds__(256) bcast_kernel(const BcastArgs a) {
   }
   __syncthreads();
 
-  if (a.doBcast && wv == 0 && !(a.dbg & 2)) {
+  if (a.doBcast && wv == 0 && a.fsTab) {
+    // ---- fewSamples: the chunks are already in the stream (fs_chunk_kernel);
+    // the receivers' z frame is stream[ZEND - N, ZEND) (process_incoming_
+    // signals_buffers, d_classes.py:1701-1807: the last N received samples)
+    const int l = __lane_id();
+    const float* zs = a.zStream + ((long long)s * a.K + k) * a.zLen;
+    const int zEnd = a.fsTab[((long long)r * a.K + k) * DANSE_FS_FIELDS + DANSE_FS_ZEND];
+    cf v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int n = l + 64 * j;
+      const int idx = zEnd - N + n;
+      v[j] = cf{(idx >= 0) ? zs[idx] * a.hA[n] : 0.0f, 0.0f};
+    }
+    wfft::fft1024(v, L, a.tw);
+    cf* Zs = a.Zspec + (((long long)(r & 1) * a.K + k) * a.S + s) * F;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      const int f = wfft::out_index(c);
+      if (f < F) Zs[f] = invSqNs * v[c];
+    }
+  } else if (a.doBcast && wv == 0 && !(a.dbg & 2)) {
     // ---- z synthesis: sqrt(Ns) * real(ifft(herm-ext(zhat))) * f, OLA with the previous frame
     const int l = __lane_id();
     cf v[16];
@@ -174,7 +197,7 @@ __global__ void __launch_bounds__(256) bcast_kernel(const BcastArgs a) {
       zq[n] = zc;
     }
     wfft::wave_sync();
-    float* zs = a.zStream + ((long long)s * a.K + k) * ((long long)a.R * Ns);
+    float* zs = a.zStream + ((long long)s * a.K + k) * a.zLen;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       const int n = l + 64 * j;

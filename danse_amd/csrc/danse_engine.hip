@@ -2,6 +2,7 @@
 // sequencing, hipGraph capture, and the fine-grained operators.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -10,6 +11,7 @@
 
 #include "bcast.hpp"
 #include "classes.hpp"
+#include "tzconv.hpp"
 
 using namespace danse;
 
@@ -68,6 +70,11 @@ struct danse_engine {
   cf *dW0 = nullptr, *dScm0 = nullptr, *dExt0 = nullptr, *dTgt0 = nullptr;
   FamNode* dFnAll = nullptr;
   long long *dInitW0Off = nullptr, *dInitScmOff = nullptr, *dExtSrcOff = nullptr, *dTgtOff = nullptr;
+  // fewSamples broadcasts (cfg.fsTab): T(z) IRs [S][K][Mmax][2N-1], schedule
+  int zLen = 0, Mmax = 0;
+  std::vector<int> fsTab;          // host copy [R][K][DANSE_FS_FIELDS]
+  int* dFsTab = nullptr;
+  float *wIR = nullptr, *dSn = nullptr;
 };
 
 static thread_local std::string g_lastErr;
@@ -138,6 +145,77 @@ __global__ void reset_ext_kernel(const int* M, int k0, int k1, const long long* 
   }
 }
 
+// ---- fewSamples broadcasts (tzconv.hpp) -------------
+struct FsArgs {
+  int S, K, MT, T, N, F, r, k0, k1, Mmax, ref, keepHistory, zLen;
+  const int* M;
+  const int* base;
+  const int* fsTab;          // [R][K][DANSE_FS_FIELDS]
+  const float* y;            // [S][MT][T]
+  const cf* wExtHist;
+  const long long* wExtNodeOff;
+  long long wExtStride;
+  const cf* tw;              // wave-FFT twiddles
+  const float* sn;           // window correlation / (N Ns), [2N-1]
+  float* wIR;                // [S][K][Mmax][2N-1]
+  float* zStream;            // [S][K][zLen]
+};
+
+DANSE_DEV const int* fs_entry(const FsArgs& a, int k) { return a.fsTab + ((long long)a.r * a.K + k) * DANSE_FS_FIELDS; }
+
+// T(z) IR refresh (dist_fct_approx of wExt[i], d_classes.py:1093-1106): one
+// wave per (scene, owned node, sensor); nodes without a refresh this round
+// exit as whole waves.
+__global__ void __launch_bounds__(256) fs_ir_kernel(const FsArgs a) {
+  __shared__ cf lds[4][wfft::kLdsElems];
+  const int wv = threadIdx.x >> 6;
+  const int nOwn = a.k1 - a.k0;
+  const int item = blockIdx.x * 4 + wv;
+  if (item >= a.S * nOwn * a.Mmax) return;
+  const int m = item % a.Mmax;
+  const int s = item / (nOwn * a.Mmax);
+  const int k = a.k0 + (item / a.Mmax) % nOwn;
+  const int Mk = a.M[k];
+  const int src = fs_entry(a, k)[DANSE_FS_IRSRC];
+  if (m >= Mk || src < 0) return;
+  const int slot = a.keepHistory ? src : (src & 1);
+  const cf* w = a.wExtHist + (long long)s * a.wExtStride + a.wExtNodeOff[k] + (long long)slot * a.F * Mk + m;
+  float* o = a.wIR + (((long long)s * a.K + k) * a.Mmax + m) * tzc::kA;
+  tzc::ir_wave(lds[wv], a.tw, a.sn, [&](int f) { return w[(long long)f * Mk]; }, [&](int t, float v) { o[t] = v; });
+}
+
+// The currL samples node k broadcasts (danse_compression_few_samples,
+// d_base.py:1871-1938) appended to its stream at POS (fill_buffers,
+// d_classes.py:1185-1224): one workgroup per (scene, owned node).
+__global__ void __launch_bounds__(tzc::kThr) fs_chunk_kernel(const FsArgs a) {
+  __shared__ tzc::ConvLds sm;
+  const int nOwn = a.k1 - a.k0;
+  const int s = blockIdx.x / nOwn;
+  const int k = a.k0 + blockIdx.x % nOwn;
+  const int* e = fs_entry(a, k);
+  const int L = e[DANSE_FS_LEN];
+  if (L <= 0) return;   // uniform per workgroup
+  const int end = e[DANSE_FS_BCEND];
+  const int Mk = a.M[k];
+  const float* y = a.y + ((long long)s * a.MT + a.base[k]) * a.T;
+  const float* ir = a.wIR + ((long long)s * a.K + k) * a.Mmax * tzc::kA;
+  float* z = a.zStream + ((long long)s * a.K + k) * a.zLen + e[DANSE_FS_POS];
+  const int T = a.T, N = a.N;
+  tzc::conv_block(
+      sm, Mk, L,
+      [&](int q, int m) {   // local_chunk_for_broadcast: y[end - N + q], zero before sample 0
+        const int idx = end - N + q;
+        return (idx >= 0 && idx < T) ? y[(long long)m * T + idx] : 0.0f;
+      },
+      [&](int i, int m) { return ir[(long long)m * tzc::kA + i]; }, [&](int i, float v) { z[i] = v; });
+}
+
+// Initial IR: a Dirac at tap N on the reference sensor (d_classes.py:660-663).
+__global__ void fs_ir_init_kernel(float* wIR, int K, int Mmax, int ref, int N) {
+  const int sk = blockIdx.x;
+  if (threadIdx.x == 0) wIR[((long long)sk * Mmax + ref) * tzc::kA + N] = 1.0f;
+}
+
 int danse_engine_reset(danse_engine* eng, void* stream) {
   if (!eng) return fail(eng, "null engine");
   HIPCHK(hipSetDevice(eng->dev));
@@ -145,7 +223,12 @@ int danse_engine_reset(danse_engine* eng, void* stream) {
   const int S = eng->S, K = eng->K, F = eng->F, R = eng->R;
   HIPCHK(hipMemsetAsync(eng->zPrev, 0, (size_t)S * K * eng->N * sizeof(float), st));
   HIPCHK(hipMemsetAsync(eng->Zspec, 0, (size_t)2 * K * S * F * sizeof(cf), st));
-  HIPCHK(hipMemsetAsync(eng->zStream, 0, (size_t)S * K * R * eng->Ns * sizeof(float), st));
+  HIPCHK(hipMemsetAsync(eng->zStream, 0, (size_t)S * K * eng->zLen * sizeof(float), st));
+  if (eng->wIR) {
+    HIPCHK(hipMemsetAsync(eng->wIR, 0, (size_t)S * K * eng->Mmax * tzc::kA * sizeof(float), st));
+    hipLaunchKernelGGL(fs_ir_init_kernel, dim3(S * K), dim3(64), 0, st, eng->wIR, K, eng->Mmax, eng->ref, eng->N);
+    HIPCHK(hipGetLastError());
+  }
   HIPCHK(hipMemsetAsync(eng->dhat, 0, (size_t)kMaxFam * S * K * R * F * sizeof(cf), st));
   HIPCHK(hipMemsetAsync(eng->d, 0, (size_t)kMaxFam * S * K * eng->T * sizeof(float), st));
   HIPCHK(hipMemsetAsync(eng->diag, 0, (size_t)S * K * kMaxFam * sizeof(int), st));
@@ -183,6 +266,23 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
   eng->families = c->families | 1; eng->keepHistory = c->keepHistory; eng->alphaExt = c->alphaExt;
   const int K = c->K, S = c->S, F = eng->F, R = c->R;
   eng->M.assign(c->M, c->M + K);
+  for (int k = 0; k < K; ++k) eng->Mmax = std::max(eng->Mmax, eng->M[k]);
+  eng->zLen = c->fsTab ? c->zStreamLen : R * c->Ns;
+  if (eng->zLen < 1) return fail(eng, "zStreamLen must be positive with fsTab");
+  if (c->fsTab) {
+    eng->fsTab.assign(c->fsTab, c->fsTab + (size_t)R * K * DANSE_FS_FIELDS);
+    for (int r = 0; r < R; ++r)
+      for (int k = 0; k < K; ++k) {
+        const int* e = &eng->fsTab[((size_t)r * K + k) * DANSE_FS_FIELDS];
+        if (e[DANSE_FS_LEN] < 0 || e[DANSE_FS_LEN] > c->N) return fail(eng, "fewSamples chunk length outside [0, N]");
+        if (e[DANSE_FS_POS] < 0 || e[DANSE_FS_POS] + e[DANSE_FS_LEN] > eng->zLen)
+          return fail(eng, "fewSamples chunk outside the stream");
+        if (e[DANSE_FS_ZEND] < 0 || e[DANSE_FS_ZEND] > eng->zLen) return fail(eng, "fewSamples z frame end outside the stream");
+        if (e[DANSE_FS_IRSRC] > r || e[DANSE_FS_IRSRC] < -1) return fail(eng, "IR refresh from a future wExt iteration");
+        if (!c->keepHistory && e[DANSE_FS_IRSRC] >= 0 && e[DANSE_FS_IRSRC] != r)
+          return fail(eng, "IR refresh from an old wExt iteration needs keepHistory");
+      }
+  }
   eng->extMode.assign(c->extMode, c->extMode + K);
   eng->base.resize(K);
   int mt = 0;
@@ -322,7 +422,23 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
   HIPCHK(dalloc(&eng->Yspec, 2 * S * MT * F));
   HIPCHK(dalloc(&eng->Zspec, (size_t)2 * K * S * F));
   HIPCHK(dalloc(&eng->zPrev, (size_t)S * K * c->N));
-  HIPCHK(dalloc(&eng->zStream, (size_t)S * K * R * c->Ns));
+  HIPCHK(dalloc(&eng->zStream, (size_t)S * K * eng->zLen));
+  if (c->fsTab) {
+    HIPCHK(dalloc(&eng->dFsTab, eng->fsTab.size()));
+    HIPCHK(hipMemcpy(eng->dFsTab, eng->fsTab.data(), eng->fsTab.size() * sizeof(int), hipMemcpyHostToDevice));
+    HIPCHK(dalloc(&eng->wIR, (size_t)S * K * eng->Mmax * tzc::kA));
+    // sn[i] = sum_n f[n] h[n + i - N + 1] / (N Ns)  (dist_fct_approx with R = Ns)
+    std::vector<float> sn(tzc::kA);
+    for (int i = 0; i < tzc::kA; ++i) {
+      const int tau = i - (c->N - 1);
+      double acc = 0.0;
+      for (int n = std::max(0, -tau); n < std::min(c->N, c->N - tau); ++n)
+        acc += (double)c->winSynthesis[n] * (double)c->winAnalysis[n + tau];
+      sn[i] = (float)(acc / ((double)c->N * (double)c->Ns));
+    }
+    HIPCHK(dalloc(&eng->dSn, (size_t)tzc::kA));
+    HIPCHK(hipMemcpy(eng->dSn, sn.data(), sn.size() * sizeof(float), hipMemcpyHostToDevice));
+  }
   HIPCHK(dalloc(&eng->Ryy, (size_t)S * eng->scmStride));
   HIPCHK(dalloc(&eng->Rnn, (size_t)S * eng->scmStride));
   HIPCHK(dalloc(&eng->wHist, (size_t)S * eng->wStride));
@@ -334,7 +450,7 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
   HIPCHK(hipMemset(eng->Yspec, 0, 2 * S * MT * F * sizeof(cf)));
   HIPCHK(hipMemset(eng->Zspec, 0, (size_t)2 * K * S * F * sizeof(cf)));
   HIPCHK(hipMemset(eng->zPrev, 0, (size_t)S * K * c->N * sizeof(float)));
-  HIPCHK(hipMemset(eng->zStream, 0, (size_t)S * K * R * c->Ns * sizeof(float)));
+  HIPCHK(hipMemset(eng->zStream, 0, (size_t)S * K * eng->zLen * sizeof(float)));
   HIPCHK(hipMemset(eng->dhat, 0, (size_t)kMaxFam * S * K * R * F * sizeof(cf)));
   HIPCHK(hipMemset(eng->d, 0, (size_t)kMaxFam * S * K * c->T * sizeof(float)));
   HIPCHK(hipMemset(eng->diag, 0, (size_t)S * K * kMaxFam * sizeof(int)));
@@ -421,7 +537,7 @@ void danse_engine_destroy(danse_engine* eng) {
                   eng->ownZspec ? eng->Zspec : nullptr, eng->Ryy,
                   eng->Rnn, eng->wHist, eng->wExtHist, eng->wExtTarget, eng->dhat, eng->zPrev, eng->zStream, eng->d,
                   eng->diag, eng->dW0, eng->dScm0, eng->dExt0, eng->dTgt0, eng->dFnAll, eng->dInitW0Off,
-                  eng->dInitScmOff, eng->dExtSrcOff, eng->dTgtOff};
+                  eng->dInitScmOff, eng->dExtSrcOff, eng->dTgtOff, eng->dFsTab, eng->wIR, eng->dSn};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (auto& cl : eng->classes) {
@@ -447,6 +563,8 @@ static BcastArgs make_bcast(danse_engine* e, int r, int synth, int bc) {
   a.wExtHistory = e->keepHistory; a.dhat = e->dhat; a.d = e->d; a.hA = e->dhA; a.hS = e->dhS; a.normVal = e->dNorm;
   a.tw = e->dTw + e->N;
   a.dbg = e->bcastAblate;
+  a.zLen = e->zLen;
+  a.fsTab = e->dFsTab;
   return a;
 }
 
@@ -472,7 +590,29 @@ static void launch_update(danse_engine* e, int r, hipStream_t st) {
   }
 }
 
+static void launch_fs(danse_engine* e, int r, hipStream_t st) {
+  FsArgs a{};
+  a.S = e->S; a.K = e->K; a.MT = e->MT; a.T = e->T; a.N = e->N; a.F = e->F; a.r = r; a.k0 = e->k0; a.k1 = e->k1;
+  a.Mmax = e->Mmax; a.ref = e->ref; a.keepHistory = e->keepHistory; a.zLen = e->zLen;
+  a.M = e->dM; a.base = e->dBase; a.fsTab = e->dFsTab; a.y = e->y;
+  a.wExtHist = e->wExtHist; a.wExtNodeOff = e->dWExtNodeOff; a.wExtStride = e->wExtStride;
+  a.tw = e->dTw + e->N; a.sn = e->dSn; a.wIR = e->wIR; a.zStream = e->zStream;
+  const int nOwn = e->k1 - e->k0;
+  bool refresh = false, chunk = false;
+  for (int k = e->k0; k < e->k1; ++k) {
+    const int* t = &e->fsTab[((size_t)r * e->K + k) * DANSE_FS_FIELDS];
+    refresh = refresh || t[DANSE_FS_IRSRC] >= 0;
+    chunk = chunk || t[DANSE_FS_LEN] > 0;
+  }
+  if (refresh) {
+    const unsigned items = (unsigned)(e->S * nOwn * e->Mmax);
+    hipLaunchKernelGGL(fs_ir_kernel, dim3((items + 3) / 4), dim3(256), 0, st, a);
+  }
+  if (chunk) hipLaunchKernelGGL(fs_chunk_kernel, dim3(e->S * nOwn), dim3(tzc::kThr), 0, st, a);
+}
+
 static void launch_bcast(danse_engine* e, int r, int synth, int bc, hipStream_t st) {
+  if (bc && e->dFsTab) launch_fs(e, r, st);
   BcastArgs a = make_bcast(e, r, synth, bc);
   const unsigned grid = (unsigned)(e->S * (e->k1 - e->k0));
   hipLaunchKernelGGL(bcast_kernel, dim3(grid), dim3(256), 0, st, a);
@@ -603,7 +743,7 @@ static int out_region(danse_engine* e, int which, int family, int node, char** p
     *chunk = (size_t)S * K * e->R * F * sizeof(cf);
   } else if (which == DANSE_OUT_Z) {
     *ptr = (char*)e->zStream;
-    *chunk = (size_t)S * K * e->R * e->Ns * sizeof(float);
+    *chunk = (size_t)S * K * e->zLen * sizeof(float);
   } else if (which == DANSE_OUT_DIAG) {
     *ptr = (char*)e->diag;
     *chunk = (size_t)S * K * kMaxFam * sizeof(int);

@@ -1,0 +1,147 @@
+// T(z) few-samples compression building blocks, shared by the stand-alone
+// operators (tz.hip: danse_tz_ir / danse_tz_compress) and the online engine's
+// fewSamples broadcasts (danse_engine.hip).  SURVEY §8a row a14.
+//
+// dist_fct_approx (d_base.py:1941-1991) sums the offset diagonals of
+// diag(f) C diag(h), C the circulant of flip(w_td), w_td = real(IFFT(
+// Hermitian-extended conj(wHat))).  The tau-th diagonal has the constant
+// circulant entry c[(-tau) mod N], so
+//     wIR[i] = w_td[i mod N] * S[i] / R,   i = tau + N - 1 in [0, 2N - 2],
+//     S[i]   = sum_n f[n] h[n + i - N + 1]       (window cross-correlation)
+// and, w_td being real, w_td = Re(FFT(Y)) / N with Y the Hermitian extension
+// of wHat itself: one wave FFT (wfft.hpp), then 2N - 1 scaled stores.
+// sn = S / (N R) is a host-built table (windows only).
+//
+// The convolution (extract_few_samples_from_convolution, d_base.py:1538-1566)
+// keeps only the L samples the node broadcasts:
+//     z[ii] = sum_m sum_q yq[q][m] wIR[id_ii - q][m],  id_ii = 2N - 1 - L + 1 + ii
+// (taps outside [0, 2N - 2] are the reference's zero padding).  One 256-thread
+// workgroup per filter; the frame and the IR of up to kMC sensors sit in LDS.
+// A thread owns kR = 8 consecutive outputs over a contiguous range of q and
+// slides a 15-tap window through the IR, so every LDS read feeds 4 FMAs; the
+// IR is stored with one pad slot per 8 taps so the 64 lanes of a wave (output
+// blocks 8 apart) hit 64 distinct banks.  Partial sums over the q ranges are
+// reduced through LDS.
+#pragma once
+#include "wfft.hpp"
+
+namespace danse {
+namespace tzc {
+
+constexpr int kN = 1024;
+constexpr int kA = 2 * kN - 1;          // IR length
+constexpr int kR = 8;                   // outputs per thread
+constexpr int kMC = 4;                  // sensors per LDS pass
+constexpr int kThr = 256;
+constexpr int kIrPad = 16;              // zero taps past the IR end (tile overhang)
+constexpr int kIrSlots = kA + kIrPad;
+DANSE_DEV int phys(int x) { return x + (x >> 3); }
+constexpr int kIrPhys = kIrSlots + kIrSlots / 8 + 1;
+
+struct ConvLds {
+  float ys[kMC][kN];
+  float as[kMC][kIrPhys];
+  float red[kThr * kR];
+};
+
+// One wave: IR of one (filter, sensor).  wAt(k) = wHat[k] for k in [0, N/2];
+// out(t, v) stores tap t in [0, 2N - 2].
+template <class WF, class OF>
+DANSE_DEV void ir_wave(cf* lds, const cf* __restrict__ tw, const float* __restrict__ sn, WF wAt, OF out) {
+  const int l = __lane_id();
+  cf v[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int k = l + 64 * j;
+    cf y;
+    if (k == 0 || k == kN / 2) {
+      y = cf{wAt(k).re, 0.f};            // DC / Nyquist forced real (d_base.py:1522-1523)
+    } else if (k < kN / 2) {
+      y = wAt(k);
+    } else {
+      y = conjg(wAt(kN - k));
+    }
+    v[j] = y;
+  }
+  wfft::fft1024(v, lds, tw);
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    const int t = wfft::out_index(c);
+    const float wt = v[c].re;
+    out(t, wt * sn[t]);
+    if (t < kN - 1) out(t + kN, wt * sn[t + kN]);
+  }
+}
+
+// One workgroup (kThr threads): the last L (1 <= L <= N) outputs of the
+// M-sensor convolution.  yAt(q, m): frame sample q of sensor m; aAt(i, m): IR
+// tap i < kA of sensor m; out(e, v): output e in [0, L).
+// nTiles = ceil(L / kR) output tiles, G = kThr / nTiles q ranges (G >= 1).
+template <class YF, class AF, class OF>
+DANSE_DEV void conv_block(ConvLds& sm, int M, int L, YF yAt, AF aAt, OF out) {
+  const int t = threadIdx.x;
+  const int nTiles = (L + kR - 1) / kR;
+  const int G = kThr / nTiles;
+  const int tile = t % nTiles, g = t / nTiles;
+  const bool active = g < G;
+  const int qc = (kN + G - 1) / G;
+  const int q0 = min(kN, g * qc), q1 = min(kN, q0 + qc);
+  const int d0 = kA - L + 1 + tile * kR;   // convolution index of this thread's first output
+  float acc[kR];
+#pragma unroll
+  for (int r = 0; r < kR; ++r) acc[r] = 0.f;
+  for (int m0 = 0; m0 < M; m0 += kMC) {
+    const int mc = min(kMC, M - m0);
+    __syncthreads();   // previous pass's reads are done
+    for (int e = t; e < kN * mc; e += kThr) {
+      const int q = e / mc, mm = e - q * mc;
+      sm.ys[mm][q] = yAt(q, m0 + mm);
+    }
+    for (int e = t; e < kIrSlots * mc; e += kThr) {
+      const int i = e / mc, mm = e - i * mc;
+      sm.as[mm][phys(i)] = i < kA ? aAt(i, m0 + mm) : 0.f;
+    }
+    __syncthreads();
+    if (active) {
+      for (int mm = 0; mm < mc; ++mm) {
+        const float* ym = sm.ys[mm];
+        const float* am = sm.as[mm];
+        // win[s] = a[d0 - q - 7 + s], s = 0..14, for the block q .. q + 7:
+        // a[d0 + r - (q + u)] = win[r - u + 7]
+        int q = q0;
+        for (; q + 8 <= q1; q += 8) {
+          float win[15];
+#pragma unroll
+          for (int s = 0; s < 15; ++s) {
+            const int x = d0 - q - 7 + s;   // >= 1 always: d0 >= N, q <= N - 8
+            win[s] = am[phys(x)];
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const float yv = ym[q + u];
+#pragma unroll
+            for (int r = 0; r < kR; ++r) acc[r] = fmaf(yv, win[r - u + 7], acc[r]);
+          }
+        }
+        for (; q < q1; ++q) {
+          const float yv = ym[q];
+#pragma unroll
+          for (int r = 0; r < kR; ++r) acc[r] = fmaf(yv, am[phys(d0 + r - q)], acc[r]);
+        }
+      }
+    }
+  }
+  // reduce over the G q ranges
+#pragma unroll
+  for (int r = 0; r < kR; ++r) sm.red[t * kR + r] = acc[r];
+  __syncthreads();
+  for (int e = t; e < L; e += kThr) {
+    const int tl = e / kR, r = e - tl * kR;
+    float s = 0.f;
+    for (int gg = 0; gg < G; ++gg) s += sm.red[(gg * nTiles + tl) * kR + r];
+    out(e, s);
+  }
+}
+
+}  // namespace tzc
+}  // namespace danse

@@ -27,7 +27,7 @@ from dataclasses import dataclass
 import numpy as np
 
 from . import _lib as L
-from .scheduler import initialize_events, compile_rounds
+from .scheduler import initialize_events, compile_rounds, compile_rounds_fs
 
 
 def beta_from_t50p(t50p, fs, Ns):
@@ -129,7 +129,11 @@ class DanseEngine:
                 raise NotImplementedError('device path covers fully connected WASNs')
         events, fs = initialize_events([n.timeStamps for n in sc0.wasn], [n.fs for n in sc0.wasn], p, neighbors)
         self.events, self.fsEv = events, fs
-        self.rt = compile_rounds(events, fs, p, K)
+        self.fewSamples = p.broadcastType == 'fewSamples'
+        if self.fewSamples:
+            self.rt = compile_rounds_fs(events, fs, p, K, [n.timeStamps for n in sc0.wasn], self.M)
+        else:
+            self.rt = compile_rounds(events, fs, p, K)
         self.R = R = self.rt.nRounds
         if not self.rt.synchronous and (p.computeCentralised or p.computeSingleSensorBroadcast):
             raise NotImplementedError('centralised / single-sensor-broadcast estimates with asynchronous (SRO) '
@@ -189,7 +193,9 @@ class DanseEngine:
         ``includeFSDflags``), the frame is compensated with phi, then
         phi -= eps_q Ns."""
         p, K, R = self.p, self.K, self.R
-        self._zLag = None if self.rt.synchronous else np.ascontiguousarray(self.rt.zLag[:R], dtype=np.uint8)
+        # fewSamples: the stream offsets of fsTab already select the frame
+        self._zLag = (None if self.rt.synchronous or self.fewSamples
+                      else np.ascontiguousarray(self.rt.zLag[:R], dtype=np.uint8))
         self._zPhase = None
         if not p.compensateSROs:
             return
@@ -333,6 +339,10 @@ class DanseEngine:
         c.keepHistory = int(bool(self.keepHistory))
         c.zLag = _ptr(self._zLag, ctypes.c_uint8)
         c.zPhase = _ptr(self._zPhase, ctypes.c_double)
+        self._fsTab = np.ascontiguousarray(self.rt.fsTab, dtype=np.int32) if self.fewSamples else None
+        c.fsTab = _ptr(self._fsTab, ctypes.c_int32)
+        c.zStreamLen = int(self.rt.zStreamLen) if self.fewSamples else 0
+        self.zLen = c.zStreamLen if self.fewSamples else self.R * self.Ns
         self._cfg = c
         eng = ctypes.c_void_p()
         L.check(self.lib.danse_engine_create(ctypes.byref(c), int(self.device), ctypes.byref(eng)))
@@ -430,8 +440,9 @@ class DanseEngine:
                     if self.keepHistory:
                         full[:, :R + 1, :] = np.transpose(w[s], (1, 0, 2))
                     getattr(res[s], wn)[k] = full
-        z = self._get(L.OUT_Z, dtype=np.float32, shape=(S, K, R * self.Ns))
+        z = self._get(L.OUT_Z, dtype=np.float32, shape=(S, K, self.zLen))
         for s in range(S):
+            # fewSamples: the broadcast streams (the reference leaves zFullTD empty)
             res[s].zFullTD = [z[s, k].astype(np.float64) for k in range(K)]
             res[s].wTildeExt = [None] * K
         for k in range(self.k0, self.k1):

@@ -216,6 +216,8 @@ class RoundTables:
     zLag: np.ndarray = None
     flags: np.ndarray = None
     synchronous: bool = True
+    fsTab: np.ndarray = None      # fewSamples: [R][K][FS_FIELDS] (compile_rounds_fs)
+    zStreamLen: int = 0
 
 
 def compile_rounds(events, fs, p, nNodes: int) -> RoundTables:
@@ -292,3 +294,131 @@ def compile_rounds(events, fs, p, nNodes: int) -> RoundTables:
     flags = np.stack([np.stack(f[:R]) for f in flg], axis=1)                   # [R][K][K]
     t = np.array([x[:R] for x in tUp], dtype=np.float64).T
     return RoundTables(bcEnd, upEnd, doSolve, R, t, zLag, flags, sync)
+
+
+FS_FIELDS = 5   # enum danse_fs_field (include/danse_mi355x.h)
+FS_BCEND, FS_LEN, FS_POS, FS_IRSRC, FS_ZEND = range(FS_FIELDS)
+
+
+def compile_rounds_fs(events, fs, p, nNodes: int, timeStamps, M) -> RoundTables:
+    """Integer round tables for fewSamples broadcasts with ``efficientSpSBC``.
+
+    Replays the reference events (``d_core.py:66-90``) with the state of
+    ``broadcast`` (``d_classes.py:1043-1128``): the chunk size
+    ``get_buffer_size_for_efficient_bc`` (``d_classes.py:1130-1160``: L times
+    the whole number of L-blocks of node samples since the last broadcast),
+    the T(z) IR refresh timer (``upTDfilterEvery``, ``d_classes.py:1090-1106``;
+    no refresh at single-sensor nodes with ``noFusionAtSingleSensorNodes``) and
+    the buffer flags of ``process_incoming_signals_buffers``
+    (``d_classes.py:1701-1807``).  Every node stream is append-only, so the z
+    frame an update consumes is the sender's stream[ZEND - N, ZEND) with ZEND
+    the samples received so far (zero before 0, the reference's front
+    padding).
+
+    Device round r runs the broadcasts of every node at its own iteration r
+    (wExt index r), then the updates r.  A schedule is accepted when
+    (i) each node broadcasts at most once per own iteration, (ii) every
+    update consumes only chunks broadcast in its round or earlier, and
+    (iii) in round r all receivers of a sender consume the same stream length
+    (always true at K = 2 and on synchronous clocks).  Returns RoundTables with
+    ``fsTab [R][K][FS_FIELDS]`` and ``zStreamLen``."""
+    if p.broadcastType != 'fewSamples':
+        raise ValueError('compile_rounds_fs is for fewSamples broadcasts')
+    if not p.efficientSpSBC:
+        raise NotImplementedError('fewSamples without efficientSpSBC (one broadcast per L samples) on the device path')
+    K, N, Ns = nNodes, p.DFTsize, p.Ns
+    Lb = int(p.broadcastLength)
+    ts = [np.asarray(t, dtype=np.float64) for t in timeStamps]
+    it = np.zeros(K, dtype=np.int64)              # iterations done per node
+    lastBc = np.zeros(K)
+    lastTD = np.zeros(K)
+    streamLen = np.zeros(K, dtype=np.int64)
+    lastBcRound = np.full(K, -1, dtype=np.int64)  # device round of each node's last broadcast
+    buf = np.zeros((K, K), dtype=np.int64)
+    bcRec = {}                                    # (r, k) -> [bcEnd, len, pos, irSrc]
+    zEnd = {}                                     # (r, q) -> stream length consumed
+    up = [[] for _ in range(K)]
+    solve = [[] for _ in range(K)]
+    tUp = [[] for _ in range(K)]
+    flg = [[] for _ in range(K)]
+    sync = True
+    for ev in events:
+        ks = list(ev.nodes)
+        if ev.type != ['bc'] * K + ['up'] * K or ks != list(range(K)) * 2:
+            sync = False
+        for ii, (k, typ) in enumerate(zip(ks, ev.type)):
+            k = int(k)
+            if typ == 'bc':
+                r = int(it[k])
+                if (r, k) in bcRec:
+                    raise NotImplementedError(f'node {k} broadcasts twice in iteration {r}')
+                irSrc = -1
+                if np.abs(ev.t - lastTD[k]) >= p.upTDfilterEvery:
+                    if not (p.noFusionAtSingleSensorNodes and M[k] == 1):
+                        irSrc = r
+                    lastTD[k] = ev.t
+                # sum((ts > last) & (ts <= t)) on the sorted clock
+                n = int(np.searchsorted(ts[k], ev.t, 'right') - np.searchsorted(ts[k], lastBc[k], 'right'))
+                currL = int(Lb * np.floor(n / Lb))
+                lastBc[k] = ev.t
+                if currL > N:
+                    raise NotImplementedError(f'broadcast chunk of {currL} > N samples')
+                bcRec[(r, k)] = [int(np.floor(ev.t * fs[k])), currL, int(streamLen[k]), irSrc]
+                streamLen[k] += currL
+                lastBcRound[k] = r
+                for q in range(K):
+                    if q != k:
+                        buf[q, k] += currL
+            else:
+                r = int(it[k])
+                up[k].append(int(np.floor(ev.t * fs[k])))
+                solve[k].append(0 if ev.bypassUpdate[ii] else 1)
+                tUp[k].append(ev.t)
+                fr = np.zeros(K, dtype=np.int64)
+                for q in range(K):
+                    if q == k:
+                        continue
+                    Bq = buf[k, q]
+                    if r == 0:
+                        fr[q] = 0 if Bq == N else (-(N - Bq) if Bq < N else (Bq - N))
+                    else:
+                        if Bq > N:
+                            raise NotImplementedError('more than N samples received between two updates')
+                        fr[q] = 0 if Bq == Ns else (-(Ns - Bq) if Bq < Ns else (Bq - Ns))
+                    if lastBcRound[q] > r:
+                        raise NotImplementedError(f'node {k} update {r} consumes a broadcast of a later round')
+                    if (r, q) in zEnd and zEnd[(r, q)] != streamLen[q]:
+                        raise NotImplementedError('receivers of one sender consume different stream lengths')
+                    zEnd[(r, q)] = int(streamLen[q])
+                    buf[k, q] = 0
+                flg[k].append(fr)
+                it[k] += 1
+    R = min(len(u) for u in up)
+    if R < 1:
+        raise ValueError('signal too short for one DANSE round')
+    tab = np.zeros((R, K, FS_FIELDS), dtype=np.int32)
+    tab[:, :, FS_IRSRC] = -1
+    for (r, k), (e, ln, pos, src) in bcRec.items():
+        if r < R:
+            tab[r, k, FS_BCEND], tab[r, k, FS_LEN], tab[r, k, FS_POS], tab[r, k, FS_IRSRC] = e, ln, pos, src
+    for (r, q), z in zEnd.items():
+        if r < R:
+            tab[r, q, FS_ZEND] = z
+    # senders nobody consumed in a round keep the previous frame end
+    for r in range(R):
+        for q in range(K):
+            if (r, q) not in zEnd:
+                tab[r, q, FS_ZEND] = tab[r - 1, q, FS_ZEND] if r > 0 else 0
+    upEnd = np.array([u[:R] for u in up], dtype=np.int64).T
+    # the broadcast kernel's phase 1 analyses "bcEnd" into the spectrum slot of
+    # the next round's local frame: point it at upEnd[r + 1]
+    bcEnd = np.empty_like(upEnd)
+    bcEnd[:-1] = upEnd[1:]
+    bcEnd[-1] = upEnd[-1]
+    doSolve = np.array([x[:R] for x in solve], dtype=np.int32).T
+    flags = np.stack([np.stack(f[:R]) for f in flg], axis=1)
+    t = np.array([x[:R] for x in tUp], dtype=np.float64).T
+    rt = RoundTables(bcEnd, upEnd, doSolve, R, t, np.zeros((R, K, K), np.uint8), flags, sync)
+    rt.fsTab = tab
+    rt.zStreamLen = int(max(1, streamLen.max()))
+    return rt

@@ -109,7 +109,27 @@ typedef struct danse_cfg {
                                of sender q's channel at node k's update r:
                                yhat *= exp(-j 2 pi f phi / N) (compensate_sros,
                                d_classes.py:1936-2046); NULL = no compensation  */
+  /* fewSamples broadcasts (broadcastType 'fewSamples' + efficientSpSBC: T(z)
+   * compression of the last currL samples, d_classes.py:1090-1160,
+   * d_base.py:1871-1991) instead of the wholeChunk WOLA compression.
+   * NULL = wholeChunk.  Host-compiled by replaying the reference event order
+   * (danse_amd/scheduler.py compile_rounds_fs); per (round r, node k):     */
+  const int32_t* fsTab;     /* [R*K*DANSE_FS_FIELDS]: DANSE_FS_BCEND, _LEN, _POS,
+                               _IRSRC, _ZEND (see enum danse_fs_field)          */
+  int32_t zStreamLen;       /* samples per node stream with fsTab (else R*Ns)  */
 } danse_cfg;
+
+/* Fields of one fsTab entry (round r, node k). */
+enum danse_fs_field {
+  DANSE_FS_BCEND = 0,   /* broadcast frame end floor(t fs) of node k's broadcast in round r */
+  DANSE_FS_LEN = 1,     /* currL: samples appended to node k's stream (0: none)             */
+  DANSE_FS_POS = 2,     /* stream position of that chunk                                    */
+  DANSE_FS_IRSRC = 3,   /* >= 0: refresh the T(z) IR from wExt iteration IRSRC first
+                           (upTDfilterEvery timer); -1: keep the current IR                 */
+  DANSE_FS_ZEND = 4,    /* node k's stream length the receivers' round-r z frame ends at
+                           (their frame = stream[ZEND - N, ZEND), zero before 0)            */
+  DANSE_FS_FIELDS = 5
+};
 
 typedef struct danse_engine danse_engine;
 

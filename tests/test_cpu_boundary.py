@@ -95,6 +95,7 @@ def test_round_tables_sro_schedule():
 
 
 def test_compile_rounds_rejects_few_samples():
+    """The wholeChunk compiler refuses fewSamples; compile_rounds_fs takes it."""
     from danse_amd.scene import make_scene
     from danse_amd.scheduler import initialize_events, compile_rounds
     from _util import make_case_params
@@ -106,6 +107,45 @@ def test_compile_rounds_rejects_few_samples():
                                [n.neighborsIdx for n in sc.wasn])
     with pytest.raises(NotImplementedError):
         compile_rounds(ev, fs, dp, 2)
+
+
+@pytest.mark.parametrize('sros', [None, [0, 200]])
+def test_round_tables_few_samples(sros):
+    """fewSamples + efficientSpSBC (config E shape): the first broadcast sends
+    L floor(N / L) samples, later ones Ns; streams are append-only (POS is
+    the running sum of LEN); each round's z frame ends at the sender's stream
+    length; the T(z) IR is refreshed from the node's current wExt iteration
+    once per upTDfilterEvery = 1 s, never at single-sensor nodes."""
+    from danse_amd.scene import make_scene
+    from danse_amd.scheduler import initialize_events, compile_rounds_fs, FS_BCEND, FS_LEN, FS_POS, FS_IRSRC, FS_ZEND
+    from _util import make_case_params
+    M = [2, 3] if sros else [2, 3, 1]
+    case = dict(M=M, danse=dict(simType='online', nodeUpdating='asy', broadcastType='fewSamples',
+                                broadcastLength=128, noFusionAtSingleSensorNodes=True))
+    kw = dict(SROperNode=sros) if sros else {}
+    dp, wp = make_case_params(case, **kw)
+    sc = make_scene(M, sigDur=2.5, seed=0, **kw)
+    ev, fs = initialize_events([n.timeStamps for n in sc.wasn], [n.fs for n in sc.wasn], dp,
+                               [n.neighborsIdx for n in sc.wasn])
+    rt = compile_rounds_fs(ev, fs, dp, len(M), [n.timeStamps for n in sc.wasn], M)
+    t = rt.fsTab
+    assert rt.synchronous == (sros is None)
+    for k in range(len(M)):
+        assert np.array_equal(t[1:, k, FS_POS], np.cumsum(t[:-1, k, FS_LEN]))
+        assert np.all(t[1:, k, FS_LEN] == 512)
+        assert np.all(t[:, k, FS_ZEND] == t[:, k, FS_POS] + t[:, k, FS_LEN])
+        src = t[:, k, FS_IRSRC]
+        rr = np.nonzero(src >= 0)[0]
+        assert np.array_equal(src[rr], rr)
+        assert len(rr) == (0 if M[k] == 1 else 2)
+    if sros is None:
+        assert np.all(t[0, :, FS_LEN] == 1024) and not np.any(rt.flags)
+        assert np.array_equal(t[:, :, FS_BCEND], rt.upEnd)
+    else:
+        # node 0 (slow clock) broadcasts at node 1's earlier update instant,
+        # snapped to its own 128-sample grid: 896 samples, flag -128 at node 1
+        assert t[0, 0, FS_LEN] == 896 and rt.flags[0, 1, 0] == -128
+    assert np.array_equal(rt.bcEnd[:-1], rt.upEnd[1:])
 
 
 def test_yaml_config_loads():
