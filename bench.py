@@ -41,9 +41,9 @@ sys.path.insert(0, str(ROOT))
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md, chip-level parameters
 
 
-def _battery_params(M, nodeUpdating='asy'):
+def _battery_params(M, nodeUpdating='asy', **extra):
     from danse_amd import params as P
-    dp = P.DANSEparameters(simType='online', nodeUpdating=nodeUpdating, performGEVD=True, GEVDrank=1,
+    dp = P.DANSEparameters(simType='online', nodeUpdating=nodeUpdating, performGEVD=True, GEVDrank=1, **extra,
                            use1stFrameAsBasis=True, filterInitType='selectFirstSensor',
                            forcedBetaExternalFilters=0.7, t_expAvg50p=1, t_expAvg50pExternalFilters=1,
                            noFusionAtSingleSensorNodes=True, startComputeMetricsAt='after_5s')
@@ -62,7 +62,15 @@ WORKLOADS = {
     'B': dict(M=[4] * 8, dur=10.0, nodeUpdating='asy', desc='B: GEVD-DANSE r1, K=8 x 4 mics, N=1024, asy, 10 s'),
     'B_seq': dict(M=[4] * 8, dur=10.0, nodeUpdating='seq', desc='B (seq): GEVD-DANSE r1, K=8 x 4 mics, seq, 10 s'),
     'small': dict(M=[2] * 4, dur=3.0, nodeUpdating='asy', desc='small smoke workload K=4 x 2, 3 s'),
+    # BASELINE.json configs[4] scene shape (tests/battery20230919_perf_asfctofL.py:14-88):
+    # K=2, MK=[2,3], fewSamples + efficientSpSBC (T(z) compression), L=64; run with --scenes 512
+    'E_L64': dict(M=[2, 3], dur=10.0, nodeUpdating='asy', extra=dict(broadcastType='fewSamples', broadcastLength=64),
+                  desc='E: GEVD-DANSE r1, K=2, MK=[2,3], fewSamples L=64 (T(z)), asy, 10 s'),
 }
+
+
+def _wl_params(wl):
+    return _battery_params(wl['M'], wl['nodeUpdating'], **wl.get('extra', {}))
 
 
 def alg_bytes_update(D, solve):
@@ -94,7 +102,7 @@ def main():
     args = ap.parse_args()
     if args.cpu_only:
         wl = WORKLOADS[args.workload]
-        dp, wp = _battery_params(wl['M'], wl['nodeUpdating'])
+        dp, wp = _wl_params(wl)
         print(json.dumps(cpu_baseline(wl['M'], wl, dp, wp, args.cpu_seconds)))
         return
 
@@ -119,7 +127,7 @@ def main():
     wl = WORKLOADS[args.workload]
     M = wl['M']
     K = len(M)
-    dp, wp = _battery_params(M, wl['nodeUpdating'])
+    dp, wp = _wl_params(wl)
     S = args.scenes
     shard = args.shard if world > 1 else 'scenes'
     if shard == 'nodes':
@@ -203,15 +211,17 @@ def main():
     eng.finish()
     torch.cuda.synchronize()
     upd_ms = np.array([a.elapsed_time(b) for a, b in evs])
-    D = M[0] + K - 1
+    Dk = [M[k] + K - 1 for k in range(K)]
+    D = max(Dk)
     flags = eng.flags            # [R][S][4][K]
-    solve = (flags[:, :, 0, k0:k1] & L.FLAG_SOLVE) != 0
-    nodeBins = S * (k1 - k0) if shard == 'nodes' else S * K
+    solve = (flags[:, :, 0, :] & L.FLAG_SOLVE) != 0
     byts = []
     for r in range(R):
-        ns = int(solve[r].sum())
-        nn = (solve[r].size - ns)
-        byts.append(F * (ns * alg_bytes_update(D, True) + nn * alg_bytes_update(D, False)))
+        b = 0
+        for k in range(k0, k1):
+            ns = int(solve[r, :, k].sum())
+            b += F * (ns * alg_bytes_update(Dk[k], True) + (S - ns) * alg_bytes_update(Dk[k], False))
+        byts.append(b)
     byts = np.array(byts, dtype=np.float64)
     avg_ms = float(upd_ms.mean())
     achieved = float(byts.mean() / (avg_ms * 1e-3) / 1e9)
@@ -249,7 +259,7 @@ def main():
             'vs_baseline': None,
             'dtype': 'c64',
             'data': f'synthetic random-IR scenes (seeded), {Stot} scenes x {K} nodes x {F} bins x {R} rounds per step',
-            'config': {'workload': wl['desc'], 'scenes_per_gpu': S, 'K': K, 'M': M[0], 'D': D, 'bins': F,
+            'config': {'workload': wl['desc'], 'scenes_per_gpu': S, 'K': K, 'M': M, 'D': Dk, 'bins': F,
                        'rounds': R, 'shard': shard, 'gevd_rank': 1, 'graph': not args.no_graph},
             'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': achieved / HBM_PEAK_GBS,
@@ -320,7 +330,7 @@ def cpu_baseline(M, wl, dp, wp, seconds):
     sc.get_vad_per_frame(dp.DFTsize, dp.Ns, wp.vadMinProportionActive)
     K, F = len(M), dp.DFTsize // 2 + 1
     # gate round from the counters (the oracle reproduces it exactly)
-    D = M[0] + K - 1
+    D = max(M) + K - 1
     starts = []
     for nd in sc.wasn:
         v = nd.vadPerFrame
