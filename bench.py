@@ -64,6 +64,10 @@ WORKLOADS = {
     'small': dict(M=[2] * 4, dur=3.0, nodeUpdating='asy', desc='small smoke workload K=4 x 2, 3 s'),
     # BASELINE.json configs[4] scene shape (tests/battery20230919_perf_asfctofL.py:14-88):
     # K=2, MK=[2,3], fewSamples + efficientSpSBC (T(z) compression), L=64; run with --scenes 512
+    # BASELINE.json configs[3]: batch DANSE (d_batch), K=32 x 8 mics (D=39), 20 iterations, asy,
+    # T = 10.01 s (non-aligned, quirk Q9); one WASN per GPU, replicas across ranks
+    'D': dict(M=[8] * 32, dur=10.01, nodeUpdating='asy', batch=True, iters=20,
+              desc='D: batch GEVD-DANSE r1, K=32 x 8 mics (D=39), 20 iterations, asy, 10.01 s'),
     'E_L64': dict(M=[2, 3], dur=10.0, nodeUpdating='asy', extra=dict(broadcastType='fewSamples', broadcastLength=64),
                   desc='E: GEVD-DANSE r1, K=2, MK=[2,3], fewSamples L=64 (T(z)), asy, 10 s'),
 }
@@ -125,6 +129,8 @@ def main():
     from danse_amd import _lib as L
 
     wl = WORKLOADS[args.workload]
+    if wl.get('batch'):
+        return bench_batch(args, wl, rank, world, local, dist)
     M = wl['M']
     K = len(M)
     dp, wp = _wl_params(wl)
@@ -145,10 +151,12 @@ def main():
         nodes = None
     t0 = time.time()
     scenes = []
-    for sd in seeds:
+    for i, sd in enumerate(seeds):
         sc = make_scene(M, sigDur=wl['dur'], seed=1000 + sd, nodes=nodes)
         sc.get_vad_per_frame(dp.DFTsize, dp.Ns, wp.vadMinProportionActive)
         scenes.append(sc)
+        if (i + 1) % 64 == 0:
+            print(f'# {i + 1}/{len(seeds)} scenes generated', file=sys.stderr, flush=True)
     tScene = time.time() - t0
     eng = DanseEngine(scenes, dp, vadMinProp=wp.vadMinProportionActive, device=local, keepHistory=True,
                       nodeRange=(k0, k1))
@@ -269,6 +277,73 @@ def main():
                          'alg_bytes_per_launch': float(byts.mean())},
             'cpu_baseline': cpu,
             'diag_nonpd': int(np.sum(diag)),
+            'scene_gen_s': tScene,
+        }
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def bench_batch(args, wl, rank, world, local, dist):
+    """Batch DANSE (config D): a step is one full danse_batch run (STFT, then
+    per iteration z, the MFMA Y.Y^H covariance contraction over VAD / non-VAD
+    frames, every node's solve, external filters, estimates, ISTFT and MMSE
+    cost) over S WASNs per GPU.  value = iterations x nodes x STFT frames x
+    bins / s.  Roofline of the dominant kernel (herk_kernel) comes from the
+    rocprofv3 kernel statistics of the same command, not from live
+    events: the kernel is internal to danse_batch_run."""
+    import torch
+    from danse_amd import params as P
+    from danse_amd.batch import BatchEngine
+    from danse_amd.scene import make_scene
+    M, K, S = wl['M'], len(wl['M']), args.scenes
+    dp, wp = _battery_params(M, wl['nodeUpdating'])
+    dp.simType = 'batch'
+    dp.maxBatchUpdates = wl['iters']
+    t0 = time.time()
+    scenes = []
+    for sd in range(rank * S, (rank + 1) * S):
+        sc = make_scene(M, sigDur=wl['dur'], seed=2000 + sd)
+        sc.get_vad_per_frame(dp.DFTsize, dp.Ns, wp.vadMinProportionActive)
+        scenes.append(sc)
+    tScene = time.time() - t0
+    eng = BatchEngine(scenes, dp, device=local)
+    for _ in range(args.warmup):
+        eng.run()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.run()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t1
+    if dist is not None:
+        tt = torch.tensor([el], dtype=torch.float64, device=f'cuda:{local}')
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    F = eng.F
+    fu_per_step = S * world * K * eng.nseg * F * eng.iters
+    D = M[0] + K - 1
+    herk_flops = S * K * eng.iters * 4.0 * F * D * (D + 1) * eng.nseg   # SURVEY §8d (Hermitian half)
+    if rank == 0:
+        line = {
+            'metric': 'DANSE frame-updates/sec (nodes x bins)', 'value': fu_per_step * args.steps / el,
+            'unit': 'frame-updates/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
+            'ms_per_step': el / args.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak',
+            'vs_baseline': None, 'dtype': 'c64',
+            'data': f'synthetic random-IR scenes (seeded), {S * world} WASNs x {K} nodes x {eng.nseg} frames x {F} '
+                    f'bins x {eng.iters} iterations per step',
+            'config': {'workload': wl['desc'], 'wasns_per_gpu': S, 'K': K, 'M': M[0], 'D': D, 'bins': F,
+                       'frames': eng.nseg, 'iterations': eng.iters, 'shard': 'replicas'},
+            'roofline': None,
+            'herk_alg_flops_per_step_per_gpu': herk_flops,
+            'cpu_baseline': None,
             'scene_gen_s': tScene,
         }
         print(json.dumps(line), flush=True)

@@ -257,20 +257,31 @@ __global__ void __launch_bounds__(256) batch_est_kernel(const cf* __restrict__ Y
     for (int j = 0; j < D - Mk; ++j) acc = acc + cmul(wf[Mk + j], zl[(j < k) ? j : j + 1]);
     return acc;
   };
+  // each bin once; the Hermitian mirror n >= F reads bin 1024 - n back from LDS
+  cf* dl = lds[wv];
+#pragma unroll
+  for (int j = 0; j < 9; ++j) {
+    const int n = l + 64 * j;
+    if (n < F) {
+      const cf d = dh(n);
+      dhat[(((long long)s * K + k) * nfr + t) * F + n] = d;
+      dl[n] = d;
+    }
+  }
+  wfft::wave_sync();
   cf v[16];
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
     const int n = l + 64 * j;
     if (n < F) {
-      const cf d = dh(n);
-      dhat[(((long long)s * K + k) * nfr + t) * F + n] = d;
-      cf x = conjg(d);
+      cf x = conjg(dl[n]);
       if (n == 0 || n == F - 1) x.im = 0.0f;   // irfft ignores the imaginary DC / Nyquist parts
       v[j] = x;
     } else {
-      v[j] = dh(1024 - n);
+      v[j] = dl[1024 - n];
     }
   }
+  wfft::wave_sync();
   wfft::fft1024(v, lds[wv], tw);
   float* out = frames + (((long long)s * K + k) * nfr + t) * 1024;
 #pragma unroll
@@ -495,8 +506,8 @@ int danse_batch_create(const danse_batch_cfg* c, int device, danse_batch** out) 
   BCHK(balloc(&eng->dCost, (size_t)c->iters * S * K));
   int Dmax = 0;
   for (int k = 0; k < K; ++k) Dmax = std::max(Dmax, eng->D[k]);
-  BCHK(balloc(&eng->wTmp, (size_t)S * F * Dmax));
-  BCHK(balloc(&eng->dDiag, (size_t)S * F));
+  BCHK(balloc(&eng->wTmp, (size_t)K * S * F * Dmax));   // one solve launch covers a run of nodes
+  BCHK(balloc(&eng->dDiag, (size_t)K * S * F));
   (void)Mmax;
   *out = eng;
   return 0;
@@ -579,21 +590,33 @@ int danse_batch_run(danse_batch* eng, void* stream) {
     BCHK(hipGetLastError());
     launch_herk(eng, st);
     BCHK(hipGetLastError());
-    for (int k = 0; k < K; ++k) {
+    // Solves (perform_update, d_core.py:298-326): consecutive solving nodes
+    // of one filter dimension have adjacent [S][F][D][D] SCM blocks, so one
+    // launch covers the whole run (K*S*F bins for equal D: a full chip
+    // instead of S*F bins per launch).
+    const size_t pitch = (size_t)eng->wStride * sizeof(cf);
+    for (int k = 0; k < K;) {
       const int D = eng->D[k];
-      cf* wNext = eng->wHist + eng->wOff[k] + (long long)(it + 1) * F * D;
       const size_t rowB = (size_t)F * D * sizeof(cf);
-      const size_t pitch = (size_t)eng->wStride * sizeof(cf);
-      if (eng->doSolve[(size_t)it * K + k]) {
-        const cf* Ry = eng->Ryy + eng->scmOff[k];
-        const cf* Rn = eng->Rnn + eng->scmOff[k];
-        if (!launch_filter_update_class(class_dmax(D), Ry, Rn, S * F, D, eng->gevd, eng->rank, eng->ref, eng->wTmp,
-                                        eng->dDiag, st))
-          return bfail(eng, "no solver class for this filter dimension");
-        BCHK(hipMemcpy2DAsync(wNext, pitch, eng->wTmp, rowB, rowB, S, hipMemcpyDeviceToDevice, st));
-      } else {
+      if (!eng->doSolve[(size_t)it * K + k]) {
+        cf* wNext = eng->wHist + eng->wOff[k] + (long long)(it + 1) * F * D;
         BCHK(hipMemcpy2DAsync(wNext, pitch, wNext - (long long)F * D, pitch, rowB, S, hipMemcpyDeviceToDevice, st));
+        ++k;
+        continue;
       }
+      int k1 = k + 1;
+      while (k1 < K && eng->D[k1] == D && eng->doSolve[(size_t)it * K + k1]) ++k1;
+      const cf* Ry = eng->Ryy + eng->scmOff[k];
+      const cf* Rn = eng->Rnn + eng->scmOff[k];
+      if (!launch_filter_update_class(class_dmax(D), Ry, Rn, (k1 - k) * S * F, D, eng->gevd, eng->rank, eng->ref,
+                                      eng->wTmp, eng->dDiag, st))
+        return bfail(eng, "no solver class for this filter dimension");
+      for (int q = k; q < k1; ++q) {
+        cf* wNext = eng->wHist + eng->wOff[q] + (long long)(it + 1) * F * D;
+        BCHK(hipMemcpy2DAsync(wNext, pitch, eng->wTmp + (long long)(q - k) * S * F * D, rowB, rowB, S,
+                              hipMemcpyDeviceToDevice, st));
+      }
+      k = k1;
     }
     hipLaunchKernelGGL(batch_ext_kernel, dim3(512), dim3(256), 0, st, S, K, it, eng->dM, eng->dD, eng->dExtMode,
                        eng->ref, eng->dBetaExt, eng->alphaExt, eng->wHist, eng->dWOff, eng->wStride, H, eng->wExtHist,
