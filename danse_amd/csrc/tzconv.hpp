@@ -31,17 +31,19 @@ namespace tzc {
 constexpr int kN = 1024;
 constexpr int kA = 2 * kN - 1;          // IR length
 constexpr int kR = 8;                   // outputs per thread
-constexpr int kMC = 4;                  // sensors per LDS pass
+constexpr int kMC = 2;                  // sensors per LDS pass (26.6 KB of LDS: 6 workgroups per CU)
 constexpr int kThr = 256;
 constexpr int kIrPad = 16;              // zero taps past the IR end (tile overhang)
 constexpr int kIrSlots = kA + kIrPad;
 DANSE_DEV int phys(int x) { return x + (x >> 3); }
 constexpr int kIrPhys = kIrSlots + kIrSlots / 8 + 1;
 
-struct ConvLds {
-  float ys[kMC][kN];
-  float as[kMC][kIrPhys];
-  float red[kThr * kR];
+union ConvLds {
+  struct {
+    float ys[kMC][kN];
+    float as[kMC][kIrPhys];
+  } in;
+  float red[kThr * kR];   // partial sums, after the last pass
 };
 
 // One wave: IR of one (filter, sensor).  wAt(k) = wHat[k] for k in [0, N/2];
@@ -95,17 +97,17 @@ DANSE_DEV void conv_block(ConvLds& sm, int M, int L, YF yAt, AF aAt, OF out) {
     __syncthreads();   // previous pass's reads are done
     for (int e = t; e < kN * mc; e += kThr) {
       const int q = e / mc, mm = e - q * mc;
-      sm.ys[mm][q] = yAt(q, m0 + mm);
+      sm.in.ys[mm][q] = yAt(q, m0 + mm);
     }
     for (int e = t; e < kIrSlots * mc; e += kThr) {
       const int i = e / mc, mm = e - i * mc;
-      sm.as[mm][phys(i)] = i < kA ? aAt(i, m0 + mm) : 0.f;
+      sm.in.as[mm][phys(i)] = i < kA ? aAt(i, m0 + mm) : 0.f;
     }
     __syncthreads();
     if (active) {
       for (int mm = 0; mm < mc; ++mm) {
-        const float* ym = sm.ys[mm];
-        const float* am = sm.as[mm];
+        const float* ym = sm.in.ys[mm];
+        const float* am = sm.in.as[mm];
         // win[s] = a[d0 - q - 7 + s], s = 0..14, for the block q .. q + 7:
         // a[d0 + r - (q + u)] = win[r - u + 7]
         int q = q0;
@@ -131,7 +133,8 @@ DANSE_DEV void conv_block(ConvLds& sm, int M, int L, YF yAt, AF aAt, OF out) {
       }
     }
   }
-  // reduce over the G q ranges
+  // reduce over the G q ranges (red aliases the frame / IR tiles)
+  __syncthreads();
 #pragma unroll
   for (int r = 0; r < kR; ++r) sm.red[t * kR + r] = acc[r];
   __syncthreads();
