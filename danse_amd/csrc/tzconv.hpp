@@ -17,10 +17,10 @@
 //     z[ii] = sum_m sum_q yq[q][m] wIR[id_ii - q][m],  id_ii = 2N - 1 - L + 1 + ii
 // (taps outside [0, 2N - 2] are the reference's zero padding).  One 256-thread
 // workgroup per filter; the frame and the IR of up to kMC sensors sit in LDS.
-// A thread owns kR = 8 consecutive outputs over a contiguous range of q and
-// slides a 15-tap window through the IR, so every LDS read feeds 4 FMAs; the
-// IR is stored with one pad slot per 8 taps so the 64 lanes of a wave (output
-// blocks 8 apart) hit 64 distinct banks.  Partial sums over the q ranges are
+// A thread owns kR = 16 consecutive outputs over a contiguous range of q and
+// slides a 23-tap window through the IR, so every LDS read feeds 5.6 FMAs;
+// the IR is stored with one pad slot per 16 taps so the lanes of a wave
+// (output blocks 16 apart, stride 17 after padding) hit distinct banks.  Partial sums over the q ranges are
 // reduced through LDS.
 #pragma once
 #include "wfft.hpp"
@@ -30,13 +30,13 @@ namespace tzc {
 
 constexpr int kN = 1024;
 constexpr int kA = 2 * kN - 1;          // IR length
-constexpr int kR = 8;                   // outputs per thread
+constexpr int kR = 16;                  // outputs per thread
 constexpr int kMC = 2;                  // sensors per LDS pass (26.6 KB of LDS: 6 workgroups per CU)
 constexpr int kThr = 256;
 constexpr int kIrPad = 16;              // zero taps past the IR end (tile overhang)
 constexpr int kIrSlots = kA + kIrPad;
-DANSE_DEV int phys(int x) { return x + (x >> 3); }
-constexpr int kIrPhys = kIrSlots + kIrSlots / 8 + 1;
+DANSE_DEV int phys(int x) { return x + (x >> 4); }
+constexpr int kIrPhys = kIrSlots + kIrSlots / 16 + 1;
 
 union ConvLds {
   struct {
@@ -108,13 +108,13 @@ DANSE_DEV void conv_block(ConvLds& sm, int M, int L, YF yAt, AF aAt, OF out) {
       for (int mm = 0; mm < mc; ++mm) {
         const float* ym = sm.in.ys[mm];
         const float* am = sm.in.as[mm];
-        // win[s] = a[d0 - q - 7 + s], s = 0..14, for the block q .. q + 7:
+        // win[s] = a[d0 - q - 7 + s], s = 0..kR+6, for the block q .. q + 7:
         // a[d0 + r - (q + u)] = win[r - u + 7]
         int q = q0;
         for (; q + 8 <= q1; q += 8) {
-          float win[15];
+          float win[kR + 7];
 #pragma unroll
-          for (int s = 0; s < 15; ++s) {
+          for (int s = 0; s < kR + 7; ++s) {
             const int x = d0 - q - 7 + s;   // >= 1 always: d0 >= N, q <= N - 8
             win[s] = am[phys(x)];
           }
