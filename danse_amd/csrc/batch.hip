@@ -252,8 +252,12 @@ __global__ void __launch_bounds__(256) batch_est_kernel(const cf* __restrict__ Y
     const cf* yl = Y + (((long long)s * F + f) * nseg + t) * MT + base[k];
     const cf* zl = Z + (((long long)s * F + f) * nseg + t) * K;
     const cf* wf = w + (long long)f * D;
+    // unrolled so that several independent gathers are in flight per lane
+    // (the kernel is latency-bound on the strided Y / Z reads)
     cf acc = cf{0.0f, 0.0f};
+#pragma unroll 4
     for (int i = 0; i < Mk; ++i) acc = acc + cmul(wf[i], yl[i]);
+#pragma unroll 8
     for (int j = 0; j < D - Mk; ++j) acc = acc + cmul(wf[Mk + j], zl[(j < k) ? j : j + 1]);
     return acc;
   };
