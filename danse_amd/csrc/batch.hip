@@ -323,19 +323,32 @@ __global__ void batch_ola_kernel(const float* __restrict__ frames, int S, int K,
 }
 
 // MMSE cost of iteration it: mean over [trim, T - trim) of |clean - d|^2
-// (get_mmse_cost, d_batch.py), fixed-order tree reduction in double.
-__global__ void __launch_bounds__(256) batch_cost_kernel(const float* __restrict__ clean, const float* __restrict__ d,
-                                                         int T, int trim, double* __restrict__ cost) {
-  __shared__ double red[256];
+// (get_mmse_cost, d_batch.py), fixed-order tree reduction in double.  1024
+// threads with four independent accumulators each: the double add chains,
+// not HBM, bound this kernel (one workgroup per (scene, node)).
+constexpr int kCostThr = 1024;
+__global__ void __launch_bounds__(kCostThr) batch_cost_kernel(const float* __restrict__ clean,
+                                                              const float* __restrict__ d, int T, int trim,
+                                                              double* __restrict__ cost) {
+  __shared__ double red[kCostThr];
   const long long sk = blockIdx.x;
-  double acc = 0.0;
-  for (int x = trim + threadIdx.x; x < T - trim; x += blockDim.x) {
-    const double e = (double)clean[sk * T + x] - (double)d[sk * T + x];
-    acc += e * e;
+  const float* c = clean + sk * T;
+  const float* dd = d + sk * T;
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  const int hi = T - trim;
+  for (int x0 = trim + threadIdx.x; x0 < hi; x0 += 4 * kCostThr) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int x = x0 + u * kCostThr;
+      if (x < hi) {
+        const double e = (double)c[x] - (double)dd[x];
+        acc[u] += e * e;
+      }
+    }
   }
-  red[threadIdx.x] = acc;
+  red[threadIdx.x] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
   __syncthreads();
-  for (int w = 128; w > 0; w >>= 1) {
+  for (int w = kCostThr / 2; w > 0; w >>= 1) {
     if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
     __syncthreads();
   }
@@ -635,7 +648,7 @@ int danse_batch_run(danse_batch* eng, void* stream) {
                        eng->dWin, eng->dD_);
     BCHK(hipGetLastError());
     if (eng->clean) {
-      hipLaunchKernelGGL(batch_cost_kernel, dim3(S * K), dim3(256), 0, st, eng->clean, eng->dD_, eng->T, eng->trim,
+      hipLaunchKernelGGL(batch_cost_kernel, dim3(S * K), dim3(kCostThr), 0, st, eng->clean, eng->dD_, eng->T, eng->trim,
                          eng->dCost + (size_t)it * S * K);
       BCHK(hipGetLastError());
     }
