@@ -322,6 +322,22 @@ __global__ void batch_ola_kernel(const float* __restrict__ frames, int S, int K,
   }
 }
 
+// Solved filters of a run of nodes k0 .. k0 + nRun - 1 (equal D) from the
+// solver's [node][scene][F][D] output into slot `slot` of each node's
+// history: one launch instead of one strided copy per node.
+__global__ void batch_wstore_kernel(const cf* __restrict__ wTmp, int nRun, int S, int FD, int k0,
+                                    const long long* __restrict__ wOff, long long wStride, int slot,
+                                    cf* __restrict__ wHist) {
+  const long long n = (long long)nRun * S * FD;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+    const int i = (int)(e % FD);
+    const long long qs = e / FD;
+    const int s = (int)(qs % S);
+    const int q = (int)(qs / S);
+    wHist[(long long)s * wStride + wOff[k0 + q] + (long long)slot * FD + i] = wTmp[e];
+  }
+}
+
 // MMSE cost of iteration it: mean over [trim, T - trim) of |clean - d|^2
 // (get_mmse_cost, d_batch.py), fixed-order tree reduction in double.  1024
 // threads with four independent accumulators each: the double add chains,
@@ -628,11 +644,9 @@ int danse_batch_run(danse_batch* eng, void* stream) {
       if (!launch_filter_update_class(class_dmax(D), Ry, Rn, (k1 - k) * S * F, D, eng->gevd, eng->rank, eng->ref,
                                       eng->wTmp, eng->dDiag, st))
         return bfail(eng, "no solver class for this filter dimension");
-      for (int q = k; q < k1; ++q) {
-        cf* wNext = eng->wHist + eng->wOff[q] + (long long)(it + 1) * F * D;
-        BCHK(hipMemcpy2DAsync(wNext, pitch, eng->wTmp + (long long)(q - k) * S * F * D, rowB, rowB, S,
-                              hipMemcpyDeviceToDevice, st));
-      }
+      hipLaunchKernelGGL(batch_wstore_kernel, dim3(1024), dim3(256), 0, st, eng->wTmp, k1 - k, S, F * D, k,
+                         eng->dWOff, eng->wStride, it + 1, eng->wHist);
+      BCHK(hipGetLastError());
       k = k1;
     }
     hipLaunchKernelGGL(batch_ext_kernel, dim3(512), dim3(256), 0, st, S, K, it, eng->dM, eng->dD, eng->dExtMode,
