@@ -83,7 +83,8 @@ __global__ void batch_z_kernel(const cf* __restrict__ Y, int S, int K, int MT, i
     const cf* wx = wExtHist + (long long)s * wExtStride + wExtOff[q] + ((long long)slot * F + f) * Mq;
     const cf* yy = Y + sft * MT + base[q];
     cf acc = cf{0.0f, 0.0f};
-    for (int m = 0; m < Mq; ++m) acc = acc + cmul(wx[m], yy[m]);
+#pragma unroll 8
+    for (int m = 0; m < Mq; ++m) acc = acc + cmul(wx[m], yy[m]);   // loads in flight together
     Z[e] = acc;
   }
 }
