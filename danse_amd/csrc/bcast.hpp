@@ -131,7 +131,8 @@ __global__ void __launch_bounds__(256) bcast_kernel(const BcastArgs a) {
         if (f < F) {
           const cf Y = invSqNs * v[c];
           if (!(a.dbg & 32)) dst[f] = Y;
-          if (!up) zp[c] = zp[c] + ((a.dbg & 16) ? Y : cmul(wx[(long long)f * Mk + m], Y));
+          // (fewSamples: z comes from the T(z) chunk, no fused spectrum here)
+          if (!up && !a.fsTab) zp[c] = zp[c] + ((a.dbg & 16) ? Y : cmul(wx[(long long)f * Mk + m], Y));
         }
       }
     }
