@@ -107,8 +107,10 @@ __global__ void __launch_bounds__(256) bcast_kernel(const BcastArgs a) {
     const int bEnd = a.bcEnd[r * a.K + k];
     const int uEnd = a.upEnd[r * a.K + k];
     const bool needUp = (r == 0) || (uEnd != a.bcEnd[(r - 1) * a.K + k]);
+    // wExt[r]: history slot r, or ring slot r & 1 (the update kernels write
+    // wExt[r + 1] into slot (r + 1) & 1 when the history is not kept)
     const cf* wx = a.wExtHist + (long long)s * a.wExtStride + a.wExtNodeOff[k] +
-                   (a.wExtHistory ? (long long)r * F * Mk : 0);
+                   (long long)(a.wExtHistory ? r : (r & 1)) * F * Mk;
     cf zp[16];
 #pragma unroll
     for (int c = 0; c < 16; ++c) zp[c] = cf{0.0f, 0.0f};

@@ -135,6 +135,11 @@ class DanseEngine:
         else:
             self.rt = compile_rounds(events, fs, p, K)
         self.R = R = self.rt.nRounds
+        if (self.k0, self.k1) != (0, K) and (p.computeCentralised or p.computeSingleSensorBroadcast):
+            # the centralised / SSBC observation vectors read every node's raw
+            # local spectra and the centralised VAD averages every node's VAD;
+            # a node-sharded engine only analyses (and only has) its own nodes
+            raise NotImplementedError('centralised / single-sensor-broadcast estimates on a node-sharded engine')
         if not self.rt.synchronous and (p.computeCentralised or p.computeSingleSensorBroadcast):
             raise NotImplementedError('centralised / single-sensor-broadcast estimates with asynchronous (SRO) '
                                       'clocks are not on the device path')

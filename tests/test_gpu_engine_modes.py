@@ -1,0 +1,120 @@
+"""HIP online engine at the benched shape and in its non-default modes
+(``-m gpu``, through the C-ABI):
+
+* config B's real shape (K = 8 x 4 mics, D = 11: the ``update_kernel_lane<11>``
+  instantiation ``bench.py`` times) against the float64 oracle, asy and seq;
+* ``keepHistory=False`` (two-slot filter rings) gives the same estimates as
+  the full history;
+* node sharding (``nodeRange``) in ONE process: two engines own the two
+  halves of the nodes and share one fused-spectra buffer (what the RCCL
+  all-gather of ``danse_amd.dist`` fills on separate GPUs); their results
+  equal the unsharded engine's, including SRO lags and fewSamples streams.
+"""
+import numpy as np
+import pytest
+
+from golden_cases import ONLINE_CASES, BATTERY
+from _util import make_case_params, make_case_scene, rel_err
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip('torch')
+
+
+def _bin_rel(w, wr):
+    return np.linalg.norm(w - wr, axis=-1) / np.maximum(np.linalg.norm(wr, axis=-1), 1e-30)
+
+
+def _stats(e):
+    e = np.asarray(e).ravel()
+    return dict(median=float(np.median(e)), p99=float(np.percentile(e, 99)), max=float(e.max()))
+
+
+def _case(name):
+    return [c for c in ONLINE_CASES if c['name'] == name][0]
+
+
+def _scene_params(case):
+    sc = make_case_scene(case)
+    dp, wp = make_case_params(case)
+    sc.get_vad_per_frame(dp.DFTsize, dp.Ns, wp.vadMinProportionActive)
+    return sc, dp, wp
+
+
+B_SHAPE = [dict(name=f'online_B_shape_K8x4_{nu}', M=[4] * 8, dur=4.0, seed=31,
+                danse=dict(BATTERY, nodeUpdating=nu)) for nu in ('asy', 'seq')]
+
+
+@pytest.mark.parametrize('case', B_SHAPE, ids=lambda c: c['name'])
+def test_config_B_shape_vs_oracle(case):
+    """K = 8 x 4 (D = 11), 4 s: the lane-per-bin kernel class the bench times."""
+    from danse_amd.core import danse_multi
+    from oracle import danse_ref_cpu as O
+    sc, dp, wp = _scene_params(case)
+    dv = danse_multi([sc], dp)[0]
+    ov = O.danse(sc, dp, vadMinProp=wp.vadMinProportionActive)
+    assert np.array_equal(dv.startRound, ov.startRound)
+    assert np.array_equal(dv.nInternalFilterUps, ov.nInternalFilterUps)
+    assert int(np.sum(dv.diag)) == 0
+    errs = []
+    for k in range(8):
+        s0 = int(ov.startRound[k])
+        errs.append(_bin_rel(dv.wTilde[k][:, s0 + 1:dv.nRounds + 1], ov.wTilde[k][:, s0 + 1:dv.nRounds + 1]))
+    st = _stats(np.concatenate([e.ravel() for e in errs]))
+    de = rel_err(dv.d, ov.d)
+    print(case['name'], 'w', st, 'd', de)
+    assert st['median'] <= 1e-5 and st['p99'] <= 1e-4, st
+    assert de <= 1e-4
+
+
+@pytest.mark.parametrize('name', ['online_B_k4m3_asy', 'online_A_k2m1_seq', 'online_E_fs_L64_asy'])
+def test_keep_history_false_matches(name):
+    """Two-slot rings for w / wExt (keepHistory=False) read wExt[r] from the
+    ring slot the previous update wrote: same d / dhat as the full history."""
+    from danse_amd.core import danse_multi
+    case = _case(name)
+    sc, dp, wp = _scene_params(case)
+    full = danse_multi([sc], dp, keepHistory=True)[0]
+    ring = danse_multi([sc], dp, keepHistory=False)[0]
+    for nm in ('d', 'dhat', 'dLocal', 'dCentr', 'dSSBC'):
+        if hasattr(full, nm):
+            assert np.array_equal(getattr(full, nm), getattr(ring, nm)), nm
+
+
+@pytest.mark.parametrize('name', ['online_B_k4m3_asy', 'online_C_sro_noflags_seq', 'online_E_fs_L128_sro_comp'])
+def test_sharded_engines_match_unsharded(name):
+    """Two engines with nodeRange halves on one device, one shared fused
+    spectra buffer (the all-gather's destination), bcast of both before the
+    update of both each round, as ``danse_amd.dist.ShardedRun`` does."""
+    from danse_amd.core import danse_multi
+    from danse_amd.engine import DanseEngine
+    from danse_amd.dist import ShardedEngine
+    case = _case(name)
+    sc, dp, wp = _scene_params(case)
+    ref = danse_multi([sc], dp)[0]
+    K = len(case['M'])
+    h = K // 2
+    engs = [DanseEngine([sc], dp, nodeRange=(0, h)), DanseEngine([sc], dp, nodeRange=(h, K))]
+    ad = [ShardedEngine(e) for e in engs]
+    zbuf = torch.zeros(ad[0].zspec_numel(), dtype=torch.float32, device='cuda')
+    for a in ad:
+        a.set_zspec(zbuf)
+        a.reset()
+    R = engs[0].R
+    for r in range(R):
+        for a in ad:
+            a.bcast(r)
+        for a in ad:
+            a.update(r)
+    for a in ad:
+        a.finish()
+    torch.cuda.synchronize()
+    outs = [e.outputs()[0] for e in engs]
+    for i, (e, o) in enumerate(zip(engs, outs)):
+        for k in range(e.k0, e.k1):
+            assert np.array_equal(o.d[:, k], ref.d[:, k]), (name, k)
+            assert np.array_equal(o.wTilde[k], ref.wTilde[k]), (name, k)
+            assert np.array_equal(o.wTildeExt[k], ref.wTildeExt[k]), (name, k)
+            if hasattr(ref, 'dLocal'):
+                assert np.array_equal(o.dLocal[:, k], ref.dLocal[:, k]), (name, k)
+        e.close()

@@ -146,9 +146,11 @@ def test_online_engine_vs_oracle(case, golden_dir):
             assert e <= 1e-4, (nm, e)
     # golden (reference itself): same d
     g = np.load(golden_dir / f"{case['name']}.npz")
-    print('   d vs reference golden', rel_err(dv.d, g['d']))
+    dg = rel_err(dv.d, g['d'])
+    print('   d vs reference golden', dg)
     assert st['median'] <= 1e-5 and st['p99'] <= 1e-4, st
     assert de <= 1e-4
+    assert dg <= 1e-4, dg
 
 
 # Filter dimensions above 16 (64-lane solver class, solver64.hpp): config C
@@ -202,9 +204,10 @@ def test_batch_engine_vs_oracle(case, golden_dir):
     de = rel_err(out.d, ov.d)
     ce = float(np.max(np.abs(out.mmseCost - np.array(ov.mmseCost, dtype=float)) / np.abs(np.array(ov.mmseCost, dtype=float))))
     g = np.load(golden_dir / f"{case['name']}.npz")
-    print(case['name'], 'w', st, 'd', de, 'cost', ce, 'd vs golden', rel_err(out.d, g['d']))
+    dg = rel_err(out.d, g['d'])
+    print(case['name'], 'w', st, 'd', de, 'cost', ce, 'd vs golden', dg)
     assert st['median'] <= 1e-5 and st['p99'] <= 1e-4, st
-    assert de <= 1e-4 and ce <= 1e-4
+    assert de <= 1e-4 and ce <= 1e-4 and dg <= 1e-4
 
 
 def test_batch_covmats_op():
