@@ -34,10 +34,10 @@ class DanseCfg(ctypes.Structure):
         ('k0', _c_i32), ('k1', _c_i32),
         ('gevd', _c_i32), ('rank', _c_i32), ('ref', _c_i32), ('families', _c_i32),
         ('alphaExt', ctypes.c_float),
-        ('extMode', _p_i32), ('beta', _p_f32), ('betaExt', _p_f32),
+        ('extMode', _p_i32), ('beta', ctypes.POINTER(ctypes.c_double)), ('betaExt', _p_f32),
         ('winAnalysis', _p_f32), ('winSynthesis', _p_f32),
         ('bcEnd', _p_i32), ('upEnd', _p_i32), ('flags', _p_u8),
-        ('w0', _p_f32), ('wExt0', _p_f32), ('wExtTarget0', _p_f32), ('scmInit', _p_f32),
+        ('w0', _p_f32), ('wExt0', _p_f32), ('wExtTarget0', _p_f32), ('scmInit', ctypes.POINTER(ctypes.c_double)),
         ('keepHistory', _c_i32),
         ('zLag', _p_u8), ('zPhase', ctypes.POINTER(ctypes.c_double)),
         ('fsTab', _p_i32), ('zStreamLen', _c_i32),

@@ -24,6 +24,7 @@ OBJ = HERE / '_obj'
 OUT = HERE / 'libdanse_mi355x.so'
 INC = HERE.parent / 'include'
 CLASSES = list(range(1, 17)) + [24, 32, 40, 48, 56, 64]
+LANE_MAX_D = 12   # csrc/classes.hpp kLaneMaxD
 FLAGS = ['--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC']
 
 
@@ -32,7 +33,11 @@ def _units():
     u = [('danse_engine.o', CSRC / 'danse_engine.hip', []), ('batch.o', CSRC / 'batch.hip', []),
          ('dxcp.o', CSRC / 'dxcp.hip', []), ('tz.o', CSRC / 'tz.hip', [])]
     for n in CLASSES:
-        u.append((f'update_d{n}.o', CSRC / 'update_class.hip', [f'-DDANSE_DMAX={n}']))
+        # lane-per-bin classes: no SLP packing of the float32 complex math
+        # (the packed pairs need swapped operand copies; with them the eigen
+        # kernel spills to scratch, without them it fits the register file)
+        extra = ['-fno-slp-vectorize'] if n <= LANE_MAX_D else []
+        u.append((f'update_d{n}.o', CSRC / 'update_class.hip', [f'-DDANSE_DMAX={n}', *extra]))
     return u
 
 

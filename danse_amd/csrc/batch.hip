@@ -101,12 +101,17 @@ struct HerkNode {
 // chains).  C = sum_t y_t y_t^H:  Re C = Yr^T Yr + Yi^T Yi,
 // Im C = Yi^T Yr - Yr^T Yi; tile pairs (I >= J) of 16 x 16, the upper
 // triangle by symmetry.
-template <int NT>
+DANSE_DEV void store_scm(cf* p, cf v) { *p = v; }
+DANSE_DEV void store_scm(cd* p, cf v) { *p = cdk(v); }
+
+// (TN: complex float, or complex double for the engine's Rnn, which the
+// mixed-precision filter update factors in float64)
+template <int NT, typename TN>
 __global__ void __launch_bounds__(64) herk_kernel(const cf* __restrict__ Y, const cf* __restrict__ Z, int S, int K,
                                                   int MT, int nseg, const int* __restrict__ base,
                                                   const HerkNode* __restrict__ nodes, int nNodes,
                                                   const int* __restrict__ frames, const int* __restrict__ nvad,
-                                                  cf* __restrict__ Ryy, cf* __restrict__ Rnn) {
+                                                  cf* __restrict__ Ryy, TN* __restrict__ Rnn) {
   constexpr int F = 513;
   constexpr int NP = NT * (NT + 1) / 2;
   const int l = threadIdx.x;
@@ -167,7 +172,7 @@ __global__ void __launch_bounds__(64) herk_kernel(const cf* __restrict__ Y, cons
     }
     // mean over the frames (np.mean of an empty set is NaN, as in the reference)
     const float sc = (cnt > 0) ? 1.0f / (float)cnt : __builtin_nanf("");
-    cf* out = (pass ? Rnn : Ryy) + nd.scmOff + ((long long)s * F + f) * D * D;
+    const long long o = nd.scmOff + ((long long)s * F + f) * D * D;
     int p = 0;
 #pragma unroll
     for (int I = 0; I < NT; ++I) {
@@ -180,8 +185,14 @@ __global__ void __launch_bounds__(64) herk_kernel(const cf* __restrict__ Y, cons
           if (row < D && col < D && (I != J || col <= row)) {
             cf c = cf{sc * are[p][rg], sc * aim[p][rg]};
             if (row == col) c.im = 0.0f;
-            out[(long long)row * D + col] = c;
-            if (row != col) out[(long long)col * D + row] = conjg(c);
+            const long long e0 = o + (long long)row * D + col, e1 = o + (long long)col * D + row;
+            if (pass) {
+              store_scm(Rnn + e0, c);
+              if (row != col) store_scm(Rnn + e1, conjg(c));
+            } else {
+              Ryy[e0] = c;
+              if (row != col) Ryy[e1] = conjg(c);
+            }
           }
         }
         ++p;
@@ -394,7 +405,8 @@ struct danse_batch {
   HerkNode* dNodes = nullptr;
   std::vector<HerkNode> nodes;
   float *dWin = nullptr, *dBetaExt = nullptr, *dFramesTD = nullptr, *dD_ = nullptr;
-  cf *dTw = nullptr, *Y = nullptr, *Z = nullptr, *Ryy = nullptr, *Rnn = nullptr, *wHist = nullptr, *wExtHist = nullptr,
+  cd* Rnn = nullptr;   // complex double (filter update in mixed precision)
+  cf *dTw = nullptr, *Y = nullptr, *Z = nullptr, *Ryy = nullptr, *wHist = nullptr, *wExtHist = nullptr,
      *tgt = nullptr, *dhat = nullptr, *wTmp = nullptr;
   double* dCost = nullptr;
   int* dDiag = nullptr;
@@ -580,7 +592,7 @@ static void launch_herk(danse_batch* e, hipStream_t st) {
       const int nN = all ? e->K : 1;
       const unsigned grid = (unsigned)(e->S * nN * e->F);
 #define DANSE_HERK(NTV)                                                                                             \
-  hipLaunchKernelGGL(herk_kernel<NTV>, dim3(grid), dim3(64), 0, st, e->Y, e->Z, e->S, e->K, e->MT, e->nseg, e->dBase, \
+  hipLaunchKernelGGL((herk_kernel<NTV, cd>), dim3(grid), dim3(64), 0, st, e->Y, e->Z, e->S, e->K, e->MT, e->nseg, e->dBase, \
                      dn, nN, e->dFrames, e->dNvad, e->Ryy, e->Rnn)
       if (nt == 1) DANSE_HERK(1);
       else if (nt == 2) DANSE_HERK(2);
@@ -641,7 +653,7 @@ int danse_batch_run(danse_batch* eng, void* stream) {
       int k1 = k + 1;
       while (k1 < K && eng->D[k1] == D && eng->doSolve[(size_t)it * K + k1]) ++k1;
       const cf* Ry = eng->Ryy + eng->scmOff[k];
-      const cf* Rn = eng->Rnn + eng->scmOff[k];
+      const cd* Rn = eng->Rnn + eng->scmOff[k];
       if (!launch_filter_update_class(class_dmax(D), Ry, Rn, (k1 - k) * S * F, D, eng->gevd, eng->rank, eng->ref,
                                       eng->wTmp, eng->dDiag, st))
         return bfail(eng, "no solver class for this filter dimension");
@@ -753,7 +765,7 @@ int danse_batch_covmats(const float* Y, int32_t B, int32_t Tf, int32_t D, const 
     const int nb = std::min(513, B - b0);
     const int nt = (D + 15) / 16;
 #define DANSE_HERK1(NTV)                                                                                       \
-  hipLaunchKernelGGL(herk_kernel<NTV>, dim3(nb), dim3(64), 0, st, Yc + (size_t)b0 * Tf * D, (const cf*)nullptr, 1, 1, \
+  hipLaunchKernelGGL((herk_kernel<NTV, cf>), dim3(nb), dim3(64), 0, st, Yc + (size_t)b0 * Tf * D, (const cf*)nullptr, 1, 1, \
                      D, Tf, dBase, dNode, 1, dFl, dNv, Ry + (size_t)b0 * D * D, Rn + (size_t)b0 * D * D)
     if (nt == 1) DANSE_HERK1(1);
     else if (nt == 2) DANSE_HERK1(2);

@@ -24,7 +24,7 @@ constexpr bool class_packed(int D) { return D <= kLaneMaxD; }
 
 #define DANSE_DECLARE_CLASS(N)                                                                      \
   void launch_update_d##N(const UpdateArgs& a, hipStream_t st);                                     \
-  void launch_filter_update_d##N(const cf* Ryy, const cf* Rnn, int B, int D, int gevd, int rank,   \
+  void launch_filter_update_d##N(const cf* Ryy, const cd* Rnn, int B, int D, int gevd, int rank,   \
                                  int ref, cf* w, int* diag, hipStream_t st);
 DANSE_FOR_EACH_CLASS(DANSE_DECLARE_CLASS)
 #undef DANSE_DECLARE_CLASS
@@ -39,7 +39,7 @@ inline bool launch_update_class(int DMAX, const UpdateArgs& a, hipStream_t st) {
   }
 }
 
-inline bool launch_filter_update_class(int DMAX, const cf* Ryy, const cf* Rnn, int B, int D, int gevd, int rank,
+inline bool launch_filter_update_class(int DMAX, const cf* Ryy, const cd* Rnn, int B, int D, int gevd, int rank,
                                        int ref, cf* w, int* diag, hipStream_t st) {
   switch (DMAX) {
 #define DANSE_CASE(N) \

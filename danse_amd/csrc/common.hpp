@@ -45,6 +45,38 @@ DANSE_DEV cf cdiv_real(cf a, float s) {
   return cf{a.re * r, a.im * r};
 }
 
+// Complex double: the noise SCM Rnn and its Cholesky factor (the filter
+// update is conditioned by cond(Rnn); see DESIGN.md "Precision").
+struct cd {
+  double re, im;
+};
+DANSE_DEV cd cdk(cf a) { return cd{(double)a.re, (double)a.im}; }
+DANSE_DEV cf cfk(cd a) { return cf{(float)a.re, (float)a.im}; }
+DANSE_DEV cd conjg(cd a) { return cd{a.re, -a.im}; }
+DANSE_DEV cd operator+(cd a, cd b) { return cd{a.re + b.re, a.im + b.im}; }
+DANSE_DEV cd operator-(cd a, cd b) { return cd{a.re - b.re, a.im - b.im}; }
+DANSE_DEV cd operator*(double s, cd a) { return cd{s * a.re, s * a.im}; }
+// acc += a * b
+DANSE_DEV void fma_c(cd& acc, cd a, cd b) {
+  acc.re = fma(a.re, b.re, fma(-a.im, b.im, acc.re));
+  acc.im = fma(a.re, b.im, fma(a.im, b.re, acc.im));
+}
+// acc -= a * b
+DANSE_DEV void fms_c(cd& acc, cd a, cd b) {
+  acc.re = fma(-a.re, b.re, fma(a.im, b.im, acc.re));
+  acc.im = fma(-a.re, b.im, fma(-a.im, b.re, acc.im));
+}
+// acc += a * conj(b)
+DANSE_DEV void fma_cc(cd& acc, cd a, cd b) {
+  acc.re = fma(a.re, b.re, fma(a.im, b.im, acc.re));
+  acc.im = fma(a.im, b.re, fma(-a.re, b.im, acc.im));
+}
+// acc -= a * conj(b)
+DANSE_DEV void fms_cc(cd& acc, cd a, cd b) {
+  acc.re = fma(-a.re, b.re, fma(-a.im, b.im, acc.re));
+  acc.im = fma(-a.im, b.re, fma(a.re, b.im, acc.im));
+}
+
 DANSE_DEV int lane_id() { return __lane_id(); }
 
 // ---------------------------------------------------------------------------

@@ -45,18 +45,21 @@ struct danse_engine {
   std::vector<FamNode> fns;   // all family-nodes (owned nodes)
   std::vector<int> chanList;
   std::vector<Class> classes;
-  long long scmStride = 0, wStride = 0, wExtStride = 0, tgtStride = 0;
+  long long scmStride = 0, wStride = 0, wExtStride = 0, tgtStride = 0, gStride = 0;
   std::vector<long long> wExtNodeOff;
   // device
   int *dM = nullptr, *dBase = nullptr, *dBcEnd = nullptr, *dUpEnd = nullptr, *dChan = nullptr;
   uint8_t* dFlags = nullptr;
   uint8_t* dZLag = nullptr;
   double* dZPhase = nullptr;
-  float *dBeta = nullptr, *dBetaExt = nullptr, *dhA = nullptr, *dhS = nullptr, *dNorm = nullptr;
+  double* dBeta = nullptr;
+  float *dBetaExt = nullptr, *dhA = nullptr, *dhS = nullptr, *dNorm = nullptr;
   cf* dTw = nullptr;
   long long* dWExtNodeOff = nullptr;
   const float* y = nullptr;
-  cf *Yspec = nullptr, *Zspec = nullptr, *Ryy = nullptr, *Rnn = nullptr, *wHist = nullptr, *wExtHist = nullptr,
+  cd* Rnn = nullptr;   // complex double (DESIGN.md "Precision"); same element offsets as Ryy
+  cf *Lscr = nullptr, *Gscr = nullptr;   // lane classes: float64-factor hand-over (kernels_lane.hpp)
+  cf *Yspec = nullptr, *Zspec = nullptr, *Ryy = nullptr, *wHist = nullptr, *wExtHist = nullptr,
      *wExtTarget = nullptr, *dhat = nullptr;
   float *zPrev = nullptr, *zStream = nullptr, *d = nullptr;
   int* diag = nullptr;
@@ -67,7 +70,8 @@ struct danse_engine {
   int bcastAblate = 0;   // DANSE_BCAST_ABLATE (diagnostics only; results are wrong when set)
   // initial-state copies for danse_engine_reset
   std::vector<long long> initW0Off, initScmOff, extSrcOff, tgtOff;
-  cf *dW0 = nullptr, *dScm0 = nullptr, *dExt0 = nullptr, *dTgt0 = nullptr;
+  cf *dW0 = nullptr, *dExt0 = nullptr, *dTgt0 = nullptr;
+  cd* dScm0 = nullptr;
   FamNode* dFnAll = nullptr;
   long long *dInitW0Off = nullptr, *dInitScmOff = nullptr, *dExtSrcOff = nullptr, *dTgtOff = nullptr;
   // fewSamples broadcasts (cfg.fsTab): T(z) IRs [S][K][Mmax][2N-1], schedule
@@ -105,7 +109,7 @@ static void pick_class(int D, int& G, int& DMAX) {
 // Re-initialise filters (slot 0 of the histories) and SCMs of every
 // (scene, family-node): one block row per (scene, family-node).
 __global__ void reset_fam_kernel(const FamNode* fns, int nFN, const long long* w0Off, const long long* scmOff,
-                                 const cf* w0, const cf* scm0, cf* wHist, long long wStride, cf* Ryy, cf* Rnn,
+                                 const cf* w0, const cd* scm0, cf* wHist, long long wStride, cf* Ryy, cd* Rnn,
                                  long long scmStride, int F) {
   const int s = blockIdx.y / nFN;
   const int i = blockIdx.y % nFN;
@@ -125,8 +129,8 @@ __global__ void reset_fam_kernel(const FamNode* fns, int nFN, const long long* w
     } else {
       src = e % ((long long)D * D);
     }
-    const cf v = scm0[scmOff[i] + src];
-    Ryy[s * scmStride + fn.scmOff + e] = v;
+    const cd v = scm0[scmOff[i] + src];
+    Ryy[s * scmStride + fn.scmOff + e] = cfk(v);
     Rnn[s * scmStride + fn.scmOff + e] = v;
     if (e < nW) wHist[s * wStride + fn.wOff + e] = w0[w0Off[i] + e];
   }
@@ -323,6 +327,8 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
       scmOff += fn.packed ? (long long)F * fn.D * (fn.D + 1) / 2 : (long long)F * fn.D * fn.D;
       fn.wOff = wOff;
       wOff += histW * F * fn.D;
+      fn.gOff = eng->gStride;
+      eng->gStride += (long long)F * fn.D;
       eng->fns.push_back(fn);
     }
   }
@@ -380,7 +386,7 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
     HIPCHK(dalloc(&eng->dZPhase, (size_t)R * K * K));
     HIPCHK(hipMemcpy(eng->dZPhase, c->zPhase, (size_t)R * K * K * sizeof(double), hipMemcpyHostToDevice));
   }
-  HIPCHK(hipMemcpy(eng->dBeta, c->beta, (size_t)S * K * sizeof(float), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(eng->dBeta, c->beta, (size_t)S * K * sizeof(double), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(eng->dBetaExt, c->betaExt, (size_t)S * K * sizeof(float), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(eng->dhA, c->winAnalysis, c->N * sizeof(float), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(eng->dhS, c->winSynthesis, c->N * sizeof(float), hipMemcpyHostToDevice));
@@ -441,6 +447,8 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
   }
   HIPCHK(dalloc(&eng->Ryy, (size_t)S * eng->scmStride));
   HIPCHK(dalloc(&eng->Rnn, (size_t)S * eng->scmStride));
+  HIPCHK(dalloc(&eng->Lscr, (size_t)S * eng->scmStride));
+  HIPCHK(dalloc(&eng->Gscr, (size_t)S * eng->gStride));
   HIPCHK(dalloc(&eng->wHist, (size_t)S * eng->wStride));
   HIPCHK(dalloc(&eng->wExtHist, (size_t)S * eng->wExtStride));
   HIPCHK(dalloc(&eng->wExtTarget, (size_t)S * eng->tgtStride));
@@ -455,7 +463,7 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
   HIPCHK(hipMemset(eng->d, 0, (size_t)kMaxFam * S * K * c->T * sizeof(float)));
   HIPCHK(hipMemset(eng->diag, 0, (size_t)S * K * kMaxFam * sizeof(int)));
   HIPCHK(hipMemset(eng->Ryy, 0, (size_t)S * eng->scmStride * sizeof(cf)));
-  HIPCHK(hipMemset(eng->Rnn, 0, (size_t)S * eng->scmStride * sizeof(cf)));
+  HIPCHK(hipMemset(eng->Rnn, 0, (size_t)S * eng->scmStride * sizeof(cd)));
   HIPCHK(hipMemset(eng->wHist, 0, (size_t)S * eng->wStride * sizeof(cf)));
   HIPCHK(hipMemset(eng->wExtHist, 0, (size_t)S * eng->wExtStride * sizeof(cf)));
 
@@ -463,7 +471,8 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
   // (family-major); keep device copies so that danse_engine_reset() can
   // re-initialise the state on a stream.
   {
-    std::vector<cf> w0h, scmh;
+    std::vector<cf> w0h;
+    std::vector<cd> scmh;
     long long w0Off = 0, scmInOff = 0;
     for (int fam = 0; fam < kMaxFam; ++fam) {
       if (!((eng->families >> fam) & 1)) continue;
@@ -476,8 +485,8 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
             for (long long e = 0; e < (long long)F * D; ++e)
               w0h.push_back(c->w0 ? cf{c->w0[2 * (w0Off + e)], c->w0[2 * (w0Off + e) + 1]} : cf{0.0f, 0.0f});
             for (long long e = 0; e < (long long)D * D; ++e)
-              scmh.push_back(c->scmInit ? cf{c->scmInit[2 * (scmInOff + e)], c->scmInit[2 * (scmInOff + e) + 1]}
-                                        : cf{0.0f, 0.0f});
+              scmh.push_back(c->scmInit ? cd{c->scmInit[2 * (scmInOff + e)], c->scmInit[2 * (scmInOff + e) + 1]}
+                                        : cd{0.0, 0.0});
           }
         }
         w0Off += (long long)F * D;
@@ -500,7 +509,7 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
     HIPCHK(dalloc(&eng->dExt0, exth.size()));
     HIPCHK(dalloc(&eng->dTgt0, tgth.size()));
     HIPCHK(hipMemcpy(eng->dW0, w0h.data(), w0h.size() * sizeof(cf), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(eng->dScm0, scmh.data(), scmh.size() * sizeof(cf), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(eng->dScm0, scmh.data(), scmh.size() * sizeof(cd), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(eng->dExt0, exth.data(), exth.size() * sizeof(cf), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(eng->dTgt0, tgth.data(), tgth.size() * sizeof(cf), hipMemcpyHostToDevice));
     eng->extSrcOff.assign(K, 0);
@@ -535,7 +544,7 @@ void danse_engine_destroy(danse_engine* eng) {
                   eng->dBeta, eng->dBetaExt,
                   eng->dhA, eng->dhS, eng->dNorm, eng->dTw, eng->dWExtNodeOff, eng->Yspec,
                   eng->ownZspec ? eng->Zspec : nullptr, eng->Ryy,
-                  eng->Rnn, eng->wHist, eng->wExtHist, eng->wExtTarget, eng->dhat, eng->zPrev, eng->zStream, eng->d,
+                  eng->Rnn, eng->Lscr, eng->Gscr, eng->wHist, eng->wExtHist, eng->wExtTarget, eng->dhat, eng->zPrev, eng->zStream, eng->d,
                   eng->diag, eng->dW0, eng->dScm0, eng->dExt0, eng->dTgt0, eng->dFnAll, eng->dInitW0Off,
                   eng->dInitScmOff, eng->dExtSrcOff, eng->dTgtOff, eng->dFsTab, eng->wIR, eng->dSn};
   for (void* p : ptrs)
@@ -573,7 +582,8 @@ static UpdateArgs make_update(danse_engine* e, int r) {
   a.S = e->S; a.K = e->K; a.MT = e->MT; a.F = e->F; a.R = e->R; a.r = r;
   a.chanList = e->dChan; a.flags = e->dFlags; a.Yspec = e->Yspec; a.Zspec = e->Zspec;
   a.zLag = e->dZLag; a.zPhase = e->dZPhase;
-  a.Ryy = e->Ryy; a.Rnn = e->Rnn; a.scmStride = e->scmStride; a.wHist = e->wHist; a.wStride = e->wStride;
+  a.Ryy = e->Ryy; a.Rnn = e->Rnn; a.scmStride = e->scmStride;
+  a.Lscr = e->Lscr; a.Gscr = e->Gscr; a.gStride = e->gStride; a.wHist = e->wHist; a.wStride = e->wStride;
   a.wHistory = e->keepHistory; a.wExtHist = e->wExtHist; a.wExtStride = e->wExtStride; a.wExtHistory = e->keepHistory;
   a.wExtTarget = e->wExtTarget; a.tgtStride = e->tgtStride; a.dhat = e->dhat; a.beta = e->dBeta;
   a.betaExt = e->dBetaExt; a.alphaExt = e->alphaExt; a.gevd = e->gevd; a.rank = e->rank; a.diag = e->diag;
@@ -834,7 +844,7 @@ int danse_wola_analysis(const float* x, int32_t C, int32_t T, const int32_t* end
   return 0;
 }
 
-int danse_filter_update(const float* Ryy, const float* Rnn, int32_t B, int32_t D, int32_t gevd, int32_t rank,
+int danse_filter_update(const float* Ryy, const double* Rnn, int32_t B, int32_t D, int32_t gevd, int32_t rank,
                         int32_t ref, float* w, int32_t* diag, void* stream) {
   danse_engine* eng = nullptr;
   if (D < 1 || D > 64) return fail(nullptr, "D must be in [1, 64]");
@@ -844,7 +854,7 @@ int danse_filter_update(const float* Ryy, const float* Rnn, int32_t B, int32_t D
   pick_class(D, G, DM);
   hipStream_t st = (hipStream_t)stream;
   const cf* a = (const cf*)Ryy;
-  const cf* n = (const cf*)Rnn;
+  const cd* n = (const cd*)Rnn;
   cf* o = (cf*)w;
   launch_filter_update_class(DM, a, n, B, D, gevd, rank, ref, o, diag, st);
   HIPCHK(hipGetLastError());

@@ -35,6 +35,7 @@ struct FamNode {
   long long wOff;     // complex-element offset within one scene's w-history block
   long long wExtOff;  // DANSE only: offset within one scene's wExt-history block
   long long tgtOff;   // DANSE only: offset within one scene's target block
+  long long gOff;     // offset within one scene's g = L^H e_ref hand-over block ([D][F])
 };
 
 struct UpdateArgs {
@@ -48,9 +49,12 @@ struct UpdateArgs {
   const cf* Zspec;         // [2][K][S][F]: slot r & 1 holds the senders' round-r frames
   const uint8_t* zLag;     // [R][K][K] or null: 1 = consume sender q's round r-1 frame (SROs)
   const double* zPhase;    // [R][K][K] or null: SRO phase-compensation offsets (samples)
-  cf* Ryy;                 // per scene stride scmStride
-  cf* Rnn;
+  cf* Ryy;                 // per scene stride scmStride (complex float)
+  cd* Rnn;                 // same element offsets, complex double (DESIGN.md "Precision")
   long long scmStride;
+  cf* Lscr;                // lane classes: float32 L^-1 hand-over, the Ryy layout
+  cf* Gscr;                // lane classes: g = L^H e_ref hand-over, per scene stride gStride
+  long long gStride;
   cf* wHist;               // per scene stride wStride
   long long wStride;
   int wHistory;            // 1: [R+1][F][D] per family-node; 0: 2 slots
@@ -60,7 +64,7 @@ struct UpdateArgs {
   cf* wExtTarget;
   long long tgtStride;
   cf* dhat;                // [fam][S][K][R][F]
-  const float* beta;       // [S*K]
+  const double* beta;      // [S*K]
   const float* betaExt;    // [S*K]
   float alphaExt;
   int gevd, rank;
@@ -156,50 +160,57 @@ __global__ void __launch_bounds__(64) update_kernel(const UpdateArgs a) {
 
   // ---- observation vector yhat_li
   const cf y = load_y(a, d, s, f, li, act);
-  const float beta = a.beta[s * a.K + d.k];
-  const float invD = 1.0f / (float)D;
+  const double beta = a.beta[s * a.K + d.k];
   const long long matOff = (long long)s * a.scmStride + d.scmOff + (long long)f * D * D;
   const int rowc = act ? li : 0;
 
+  // Ryy row in float32; Rnn row averaged in float64 (then rounded for this
+  // class's float32 solver)
   cf A[DMAX], B[DMAX];
-  auto load_rows = [&](const cf* P, cf (&X)[DMAX]) {
+  const bool needY = (opY != 0) || solve;
+  const bool needN = (opN != 0) || solve;
+  if (needY) {
     sfor<0, DMAX>([&](auto cc) {
       constexpr int c = decltype(cc)::value;
       const int cl = (c < D) ? c : D - 1;
-      const cf v = P[matOff + (long long)rowc * D + cl];
-      X[c] = (act && c < D) ? v : cf{0.0f, 0.0f};
+      const cf v = a.Ryy[matOff + (long long)rowc * D + cl];
+      A[c] = (act && c < D) ? v : cf{0.0f, 0.0f};
     });
-  };
-  auto store_rows = [&](cf* P, const cf (&X)[DMAX]) {
-    if (act && valid) {
-      sfor<0, DMAX>([&](auto cc) {
-        constexpr int c = decltype(cc)::value;
-        if (c < D) P[matOff + (long long)li * D + c] = X[c];
-      });
-    }
-  };
-  // R[li][c] <- yy^H (first-frame basis) or beta R + (1 - beta) yy^H,
-  // yy^H[li][c] = (1/D) y_li conj(y_c)
-  auto apply_op = [&](cf (&X)[DMAX], int op) {
+  }
+  if (opY) {
+    const float by = (float)beta, cy = (opY == DANSE_OP_SET) ? (float)(1.0 / D) : (float)((1.0 - beta) / D);
     sfor<0, DMAX>([&](auto cc) {
       constexpr int c = decltype(cc)::value;
       const cf yc = gbcast<G, c>(y);
-      const cf yy = invD * mulc(y, yc);   // y = 0 on lanes >= D
-      if (op == DANSE_OP_SET) X[c] = yy;
-      else X[c] = beta * X[c] + (1.0f - beta) * yy;
+      const cf yy = cy * mulc(y, yc);   // y = 0 on lanes >= D
+      A[c] = (opY == DANSE_OP_SET) ? yy : by * A[c] + yy;
     });
-  };
-  const bool needY = (opY != 0) || solve;
-  const bool needN = (opN != 0) || solve;
-  if (needY) load_rows(a.Ryy, A);
-  if (needN) load_rows(a.Rnn, B);
-  if (opY) {
-    apply_op(A, opY);
-    store_rows(a.Ryy, A);
+    if (act && valid) {
+      sfor<0, DMAX>([&](auto cc) {
+        constexpr int c = decltype(cc)::value;
+        if (c < D) a.Ryy[matOff + (long long)li * D + c] = A[c];
+      });
+    }
   }
-  if (opN) {
-    apply_op(B, opN);
-    store_rows(a.Rnn, B);
+  if (needN) {
+    const double cy = (opN == DANSE_OP_SET) ? 1.0 / D : (1.0 - beta) / D;
+    const double cx = (opN == DANSE_OP_SET) ? 0.0 : beta;
+    const cd yl = cdk(y);
+    sfor<0, DMAX>([&](auto cc) {
+      constexpr int c = decltype(cc)::value;
+      const int cl = (c < D) ? c : D - 1;
+      cd x = a.Rnn[matOff + (long long)rowc * D + cl];
+      if (!(act && c < D)) x = cd{0.0, 0.0};
+      if (opN) {
+        cd yy = cd{0.0, 0.0};
+        fma_cc(yy, yl, cdk(gbcast<G, c>(y)));
+        x = cx * x;
+        x.re = fma(cy, yy.re, x.re);
+        x.im = fma(cy, yy.im, x.im);
+        if (act && valid && c < D) a.Rnn[matOff + (long long)li * D + c] = x;
+      }
+      B[c] = cfk(x);
+    });
   }
 
   // ---- filter
@@ -229,7 +240,7 @@ __global__ void __launch_bounds__(64) update_kernel(const UpdateArgs a) {
 // Stand-alone batched filter update (danse_filter_update): one bin per lane
 // group, Ryy / Rnn as [B][D][D] complex64.
 template <int G, int DMAX, int RMAX>
-__global__ void __launch_bounds__(64) filter_update_kernel(const cf* Ryy, const cf* Rnn, int B, int D, int gevd,
+__global__ void __launch_bounds__(64) filter_update_kernel(const cf* Ryy, const cd* Rnn, int B, int D, int gevd,
                                                           int rank, int ref, cf* w, int* diag) {
   constexpr int NB = 64 / G;
   __shared__ SolverLDS<DMAX> lds[NB];
@@ -245,7 +256,7 @@ __global__ void __launch_bounds__(64) filter_update_kernel(const cf* Ryy, const 
     constexpr int c = decltype(cc)::value;
     const int cl = (c < D) ? c : D - 1;
     const cf a = Ryy[((long long)b * D + row) * D + cl];
-    const cf n = Rnn[((long long)b * D + row) * D + cl];
+    const cf n = cfk(Rnn[((long long)b * D + row) * D + cl]);
     A[c] = (act && c < D) ? a : cf{0.0f, 0.0f};
     Bm[c] = (act && c < D) ? n : cf{0.0f, 0.0f};
   });

@@ -28,49 +28,58 @@ __global__ void __launch_bounds__(64) update_kernel_big(const UpdateArgs a) {
   const bool solve = (fl & DANSE_FLAG_SOLVE) != 0;
 
   const cf y = load_y(a, d, s, f, li, act);
-  const float beta = a.beta[s * a.K + d.k];
-  const float invD = 1.0f / (float)D;
+  const double beta = a.beta[s * a.K + d.k];
   const long long matOff = (long long)s * a.scmStride + d.scmOff + (long long)f * D * D;
   const int rowc = act ? li : 0;
 
+  // Ryy row in float32; Rnn row averaged in float64 (then rounded for this
+  // class's float32 solver)
   Row<DMAX> A, B;
-  auto load_rows = [&](const cf* P, Row<DMAX>& X) {
-    rzero(X);
+  const bool needY = (opY != 0) || solve;
+  const bool needN = (opN != 0) || solve;
+  if (needY) {
+    rzero(A);
     cols_below<DMAX>(D, [&](auto cc) {
       constexpr int c = decltype(cc)::value;
       const int cl = (c < D) ? c : D - 1;
-      const cf v = P[matOff + (long long)rowc * D + cl];
-      ws<c>(X, (act && c < D) ? v : cf{0.0f, 0.0f});
+      const cf v = a.Ryy[matOff + (long long)rowc * D + cl];
+      ws<c>(A, (act && c < D) ? v : cf{0.0f, 0.0f});
     });
-  };
-  auto store_rows = [&](cf* P, const Row<DMAX>& X) {
+  }
+  if (opY) {
+    const float by = (float)beta, cy = (opY == DANSE_OP_SET) ? (float)(1.0 / D) : (float)((1.0 - beta) / D);
+    cols_below<DMAX>(D, [&](auto cc) {
+      constexpr int c = decltype(cc)::value;
+      const cf yy = cy * mulc(y, rl(y, c));   // y = 0 on lanes >= D
+      ws<c>(A, (opY == DANSE_OP_SET) ? yy : by * rs<c>(A) + yy);
+    });
     if (act) {
       cols_below<DMAX>(D, [&](auto cc) {
         constexpr int c = decltype(cc)::value;
-        if (c < D) P[matOff + (long long)li * D + c] = rs<c>(X);
+        if (c < D) a.Ryy[matOff + (long long)li * D + c] = rs<c>(A);
       });
     }
-  };
-  auto apply_op = [&](Row<DMAX>& X, int op) {
+  }
+  if (needN) {
+    rzero(B);
+    const double cy = (opN == DANSE_OP_SET) ? 1.0 / D : (1.0 - beta) / D;
+    const double cx = (opN == DANSE_OP_SET) ? 0.0 : beta;
+    const cd yl = cdk(y);
     cols_below<DMAX>(D, [&](auto cc) {
       constexpr int c = decltype(cc)::value;
-      const cf yc = rl(y, c);
-      const cf yy = invD * mulc(y, yc);   // y = 0 on lanes >= D
-      if (op == DANSE_OP_SET) ws<c>(X, yy);
-      else ws<c>(X, beta * rs<c>(X) + (1.0f - beta) * yy);
+      const int cl = (c < D) ? c : D - 1;
+      cd x = a.Rnn[matOff + (long long)rowc * D + cl];
+      if (!(act && c < D)) x = cd{0.0, 0.0};
+      if (opN) {
+        cd yy = cd{0.0, 0.0};
+        fma_cc(yy, yl, cdk(rl(y, c)));
+        x = cx * x;
+        x.re = fma(cy, yy.re, x.re);
+        x.im = fma(cy, yy.im, x.im);
+        if (act && c < D) a.Rnn[matOff + (long long)li * D + c] = x;
+      }
+      ws<c>(B, cfk(x));
     });
-  };
-  const bool needY = (opY != 0) || solve;
-  const bool needN = (opN != 0) || solve;
-  if (needY) load_rows(a.Ryy, A);
-  if (needN) load_rows(a.Rnn, B);
-  if (opY) {
-    apply_op(A, opY);
-    store_rows(a.Ryy, A);
-  }
-  if (opN) {
-    apply_op(B, opN);
-    store_rows(a.Rnn, B);
   }
 
   const long long wBase = (long long)s * a.wStride + d.wOff;
@@ -95,7 +104,7 @@ __global__ void __launch_bounds__(64) update_kernel_big(const UpdateArgs a) {
 }
 
 template <int DMAX, int RMAX>
-__global__ void __launch_bounds__(64) filter_update_kernel_big(const cf* Ryy, const cf* Rnn, int B, int D, int gevd,
+__global__ void __launch_bounds__(64) filter_update_kernel_big(const cf* Ryy, const cd* Rnn, int B, int D, int gevd,
                                                               int rank, int ref, cf* w, int* diag) {
   using namespace big;
   __shared__ LDS<DMAX> lds;
@@ -110,7 +119,7 @@ __global__ void __launch_bounds__(64) filter_update_kernel_big(const cf* Ryy, co
     constexpr int c = decltype(cc)::value;
     const int cl = (c < D) ? c : D - 1;
     const cf va = Ryy[((long long)b * D + row) * D + cl];
-    const cf vn = Rnn[((long long)b * D + row) * D + cl];
+    const cf vn = cfk(Rnn[((long long)b * D + row) * D + cl]);
     ws<c>(A, (act && c < D) ? va : cf{0.0f, 0.0f});
     ws<c>(Bm, (act && c < D) ? vn : cf{0.0f, 0.0f});
   });

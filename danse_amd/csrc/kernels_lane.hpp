@@ -1,103 +1,159 @@
 // update / filter kernels for small filter dimensions (D <= kLaneMaxD):
-// one (scene, family-node, bin) per LANE (solver1.hpp).  Same per-bin work as
-// update_kernel in kernels.hpp -- SCM update (d_classes.py:2048-2267), filter
-// update (d_classes.py:3320-3387), external filters (d_classes.py:1627-1694),
-// dhat = w^H yhat (d_base.py:2075) -- with the SCMs of this class stored as
-// packed lower triangles, bin-minor ([D(D+1)/2][F] per family-node), so a
-// wave's 64 lanes read and write every SCM entry as one coalesced 512-byte
-// access.
+// one (scene, family-node, bin) per LANE (solver_mixed.hpp).  Same per-bin
+// work as update_kernel in kernels.hpp -- SCM update (d_classes.py:
+// 2048-2267), filter update (d_classes.py:3320-3387), external filters
+// (d_classes.py:1627-1694), dhat = w^H yhat (d_base.py:2075) -- with the
+// SCMs of this class stored as packed lower triangles, bin-minor
+// ([D(D+1)/2][F] per family-node), so a wave's 64 lanes read and write
+// every SCM entry as one coalesced access (512 B for the float32 Ryy, 1 KiB
+// for the float64 Rnn).
+//
+// Two launches per round (the float64 factorisation and the float32 eigen
+// work each get the whole register file):
+//   scm_factor_kernel_lane  SCM recursion (Ryy float32 or Rnn float64, as the
+//                           VAD selects); on solve frames the float64
+//                           Cholesky + inverse of Rnn, handed over as the
+//                           float32 Li = L^-1 ([tri][F], the Ryy layout) and
+//                           g = L^H e_ref ([D][F]); MWF solves completely here
+//   gevd_tail_kernel_lane   C = Li Ryy Li^H, eigen part, w, external filters,
+//                           dhat
 #pragma once
 #include "kernels.hpp"
-#include "solver1.hpp"
+#include "solver_mixed.hpp"
 
 namespace danse {
 
-template <int D, int RMAX, bool GEVD>
-__global__ void __launch_bounds__(64) update_kernel_lane(const UpdateArgs a) {
+struct LaneIdx {
+  int f, s, fni;
+  bool valid;
+};
+DANSE_DEV LaneIdx lane_index(const UpdateArgs& a) {
+  const long long total = (long long)a.S * a.nFN * a.F;
+  long long gid = (long long)blockIdx.x * 64 + threadIdx.x;
+  LaneIdx x;
+  x.valid = gid < total;
+  if (!x.valid) gid = total - 1;
+  x.f = (int)(gid % a.F);
+  const long long t = gid / a.F;
+  x.fni = (int)(t % a.nFN);
+  x.s = (int)(t / a.nFN);
+  return x;
+}
+
+template <int D, bool GEVD>
+__global__ void __launch_bounds__(64) scm_factor_kernel_lane(const UpdateArgs a) {
   using namespace lane;
   constexpr int NT = tri_n(D);
-  const int F = a.F;
-  const long long total = (long long)a.S * a.nFN * F;
-  long long gid = (long long)blockIdx.x * 64 + threadIdx.x;
-  const bool valid = gid < total;
-  if (!valid) gid = total - 1;
-  const int f = (int)(gid % F);
-  const long long t = gid / F;
-  const int fni = (int)(t % a.nFN);
-  const int s = (int)(t / a.nFN);
-  const FamNode d = a.fn[fni];
-  const int r = a.r;
+  const LaneIdx ix = lane_index(a);
+  const int F = a.F, f = ix.f, s = ix.s, r = a.r;
+  const bool valid = ix.valid;
+  const FamNode d = a.fn[ix.fni];
   const uint8_t fl = a.flags[(((long long)r * a.S + s) * kMaxFam + d.fam) * a.K + d.k];
   const int opY = fl & 3, opN = (fl >> 2) & 3;
-  const bool solve = (fl & DANSE_FLAG_SOLVE) != 0;
-  const bool pregiven = (fl & DANSE_FLAG_PREGIVEN) != 0;
+  const bool solve = (fl & DANSE_FLAG_SOLVE) != 0 && (fl & DANSE_FLAG_PREGIVEN) == 0;
+  if (!(opY || opN || solve)) return;   // no SCM work this round (pregiven replay)
 
   cf y[D];
   if (opY || opN) {
-    sfor<0, D>([&](auto ic) {
-      constexpr int i = decltype(ic)::value;
-      y[i] = load_y(a, d, s, f, i, true);
-    });
+    sfor<0, D>([&](auto ic) { y[decltype(ic)::value] = load_y(a, d, s, f, decltype(ic)::value, true); });
   }
-  const float beta = a.beta[s * a.K + d.k];
-  const float invD = 1.0f / (float)D;
+  const double beta = a.beta[s * a.K + d.k];
   const long long base = (long long)s * a.scmStride + d.scmOff + f;
 
-  // Rnn first, then Ryy, so that at most one triangle plus the Cholesky
-  // factor's LDS copy is live: the GEVD keeps L in LDS, the MWF only the
-  // column Rnn[:, ref].
-  __shared__ cf Ls[(D * (D - 1) / 2 > 0) ? D * (D - 1) / 2 : 1][64];
-  const int lane_ = threadIdx.x;
-  PTri<D> X;
-  auto load = [&](const cf* Pm) {
-    sfor<0, NT>([&](auto ec) {
-      constexpr int e = decltype(ec)::value;
-      X.a[e] = Pm[base + (long long)e * F];
-    });
-  };
-  auto store = [&](cf* Pm) {
-    if (valid) {
-      sfor<0, NT>([&](auto ec) {
-        constexpr int e = decltype(ec)::value;
-        Pm[base + (long long)e * F] = X.a[e];
-      });
-    }
-  };
-  // X <- yy^H (first-frame basis) or beta X + (1 - beta) yy^H, yy^H = y y^H / D
-  auto apply = [&](int op) {
+  // ---- SCM recursion (the VAD selects one of Ryy / Rnn per frame):
+  // SCM <- yy^H (first-frame basis) or beta SCM + (1 - beta) yy^H, yy^H = y y^H / D
+  if (opY) {
+    PTri<D> A;
+    sfor<0, NT>([&](auto ec) { A.a[decltype(ec)::value] = a.Ryy[base + (long long)decltype(ec)::value * F]; });
+    const float by = (float)beta, cy = (opY == DANSE_OP_SET) ? (float)(1.0 / D) : (float)((1.0 - beta) / D);
     sfor<0, D>([&](auto ic) {
       constexpr int i = decltype(ic)::value;
       sfor<0, i + 1>([&](auto jc) {
         constexpr int j = decltype(jc)::value;
-        const cf yy = invD * mulc(y[i], y[j]);
-        X.a[P(i, j)] = (op == DANSE_OP_SET) ? yy : beta * X.a[P(i, j)] + (1.0f - beta) * yy;
+        const cf yy = cy * mulc(y[i], y[j]);
+        A.a[P(i, j)] = (opY == DANSE_OP_SET) ? yy : by * A.a[P(i, j)] + yy;
+        if constexpr (i == j) A.a[P(i, j)].im = 0.0f;
       });
     });
-  };
-  const bool gsolve = solve && GEVD;
-  bool ok = true;
-  float invd[D], ldiag[D];
-  cf ncol[D];
+    if (valid) {
+      sfor<0, NT>([&](auto ec) { a.Ryy[base + (long long)decltype(ec)::value * F] = A.a[decltype(ec)::value]; });
+    }
+  }
+  PTriD<D> N;
   if (opN || solve) {
-    load(a.Rnn);
-    if (opN) {
-      apply(opN);
-      store(a.Rnn);
-    }
-    if (gsolve) {
-      ok = chol<D>(X, invd);
-      to_lds<D>(X, Ls, lane_, ldiag);
-    } else if (solve) {
-      herm_col<D>(X, d.ref, ncol);
+    sfor<0, NT>([&](auto ec) { N.a[decltype(ec)::value] = a.Rnn[base + (long long)decltype(ec)::value * F]; });
+    sfor<0, D>([&](auto ic) { N.a[P(decltype(ic)::value, decltype(ic)::value)].im = 0.0; });
+  }
+  if (opN) {
+    const double cy = (opN == DANSE_OP_SET) ? 1.0 / D : (1.0 - beta) / D;
+    const double cx = (opN == DANSE_OP_SET) ? 0.0 : beta;
+    sfor<0, D>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      const cd yi = cdk(y[i]);
+      sfor<0, i + 1>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        cd yy = cd{0.0, 0.0};
+        fma_cc(yy, yi, cdk(y[j]));
+        cd x = cx * N.a[P(i, j)];
+        x.re = fma(cy, yy.re, x.re);
+        x.im = (i == j) ? 0.0 : fma(cy, yy.im, x.im);
+        N.a[P(i, j)] = x;
+      });
+    });
+    if (valid) {
+      sfor<0, NT>([&](auto ec) { a.Rnn[base + (long long)decltype(ec)::value * F] = N.a[decltype(ec)::value]; });
     }
   }
-  if (opY || solve) {
-    load(a.Ryy);
-    if (opY) {
-      apply(opY);
-      store(a.Ryy);
+  if (!solve) return;
+
+  bool ok = true;
+  if constexpr (GEVD) {
+    // float64 Cholesky + inverse of Rnn; hand-over in float32
+    ok = chol64<D>(N);
+    cf g[D];
+    ref_row<D>(N, d.ref, g);
+    tri_inv64<D>(N);
+    if (valid) {
+      sfor<0, NT>([&](auto ec) { a.Lscr[base + (long long)decltype(ec)::value * F] = cfk(N.a[decltype(ec)::value]); });
+      const long long gb = (long long)s * a.gStride + d.gOff + f;
+      sfor<0, D>([&](auto ic) { a.Gscr[gb + (long long)decltype(ic)::value * F] = g[decltype(ic)::value]; });
     }
+  } else {
+    // MWF, float64 throughout: w = Ryy^-1 (Ryy - Rnn) e_ref
+    cd ncol[D];
+    sfor<0, D>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      cd c = cd{0.0, 0.0};
+      sfor<0, D>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        if (k == d.ref) c = hermd<i, k>(N);
+      });
+      ncol[i] = c;
+    });
+    asm volatile("" ::: "memory");
+    PTri<D> A;
+    sfor<0, NT>([&](auto ec) { A.a[decltype(ec)::value] = a.Ryy[base + (long long)decltype(ec)::value * F]; });
+    cf w[D];
+    ok = mwf_filter_mixed<D>(A, ncol, d.ref, w);
+    const int slotNext = a.wHistory ? r + 1 : ((r + 1) & 1);
+    cf* wNext = a.wHist + (long long)s * a.wStride + d.wOff + ((long long)slotNext * F + f) * D;
+    if (valid) sfor<0, D>([&](auto ic) { wNext[decltype(ic)::value] = w[decltype(ic)::value]; });
   }
+  if (!ok && valid) atomicOr(&a.diag[(s * a.K + d.k) * kMaxFam + d.fam], 1);
+}
+
+template <int D, int RMAX, bool GEVD>
+__global__ void __launch_bounds__(64) gevd_tail_kernel_lane(const UpdateArgs a) {
+  using namespace lane;
+  constexpr int NT = tri_n(D);
+  const LaneIdx ix = lane_index(a);
+  const int F = a.F, f = ix.f, s = ix.s, r = a.r;
+  const bool valid = ix.valid;
+  const FamNode d = a.fn[ix.fni];
+  const uint8_t fl = a.flags[(((long long)r * a.S + s) * kMaxFam + d.fam) * a.K + d.k];
+  const bool solve = (fl & DANSE_FLAG_SOLVE) != 0;
+  const bool pregiven = (fl & DANSE_FLAG_PREGIVEN) != 0;
+  const long long base = (long long)s * a.scmStride + d.scmOff + f;
 
   const long long wBase = (long long)s * a.wStride + d.wOff;
   const int slotPrev = a.wHistory ? r : (r & 1);
@@ -105,18 +161,28 @@ __global__ void __launch_bounds__(64) update_kernel_lane(const UpdateArgs a) {
   cf* wPrev = a.wHist + wBase + ((long long)slotPrev * F + f) * D;
   cf* wNext = a.wHist + wBase + ((long long)slotNext * F + f) * D;
   cf w[D];
-  if (pregiven) {
+  if (pregiven || (solve && !GEVD)) {
+    // pre-given history, or the MWF filter scm_factor_kernel_lane solved
     sfor<0, D>([&](auto ic) { w[decltype(ic)::value] = wNext[decltype(ic)::value]; });
   } else if (solve) {
-    if constexpr (GEVD) gevd_filter<D, RMAX>(X, LTri<D>{Ls, lane_}, invd, ldiag, a.rank, d.ref, w);
-    else ok = mwf_filter<D>(X, ncol, d.ref, w);
-    if (!ok && valid) atomicOr(&a.diag[(s * a.K + d.k) * kMaxFam + d.fam], 1);
+    if constexpr (GEVD) {
+      __shared__ cf Ls[NT][64];
+      sfor<0, NT>([&](auto ec) { Ls[decltype(ec)::value][threadIdx.x] = a.Lscr[base + (long long)decltype(ec)::value * F]; });
+      const LdsTri<D> Li{Ls, (int)threadIdx.x};
+      cf g[D];
+      const long long gb = (long long)s * a.gStride + d.gOff + f;
+      sfor<0, D>([&](auto ic) { g[decltype(ic)::value] = a.Gscr[gb + (long long)decltype(ic)::value * F]; });
+      PTri<D> A;
+      sfor<0, NT>([&](auto ec) { A.a[decltype(ec)::value] = a.Ryy[base + (long long)decltype(ec)::value * F]; });
+      congruence<D>(A, Li);
+      gevd_filter_mixed<D, RMAX>(A, Li, g, a.rank, w);
+    }
+    if (valid) sfor<0, D>([&](auto ic) { wNext[decltype(ic)::value] = w[decltype(ic)::value]; });
   } else {
     sfor<0, D>([&](auto ic) { w[decltype(ic)::value] = wPrev[decltype(ic)::value]; });
+    if (valid) sfor<0, D>([&](auto ic) { wNext[decltype(ic)::value] = w[decltype(ic)::value]; });
   }
-  if (valid && !pregiven) {
-    sfor<0, D>([&](auto ic) { wNext[decltype(ic)::value] = w[decltype(ic)::value]; });
-  }
+  asm volatile("" ::: "memory");
 
   // external filters (DANSE family), d_classes.py:1627-1694
   if (d.extMode >= 0 && !pregiven && valid) {
@@ -144,8 +210,7 @@ __global__ void __launch_bounds__(64) update_kernel_lane(const UpdateArgs a) {
       }
     });
   }
-  // dhat = w^H yhat, DC / Nyquist forced real (quirk Q7); yhat re-read (L2)
-  // rather than held in registers across the solve
+  // dhat = w^H yhat, DC / Nyquist forced real (quirk Q7)
   cf dh = cf{0.0f, 0.0f};
   sfor<0, D>([&](auto ic) {
     constexpr int i = decltype(ic)::value;
@@ -156,40 +221,65 @@ __global__ void __launch_bounds__(64) update_kernel_lane(const UpdateArgs a) {
 }
 
 // Stand-alone batched filter update (danse_filter_update) on full [B][D][D]
-// SCM pairs: one batch item per lane.
+// SCM pairs (Ryy complex float, Rnn complex double): one batch item per lane,
+// the same two phases (float64 factorisation, float32 eigen work) in one
+// kernel (the operator is not performance critical).
 template <int D, int RMAX>
-__global__ void __launch_bounds__(64) filter_update_kernel_lane(const cf* Ryy, const cf* Rnn, int Bn, int gevd,
+__global__ void __launch_bounds__(64) filter_update_kernel_lane(const cf* Ryy, const cd* Rnn, int Bn, int gevd,
                                                                int rank, int ref, cf* w, int* diag) {
   using namespace lane;
   int b = blockIdx.x * 64 + threadIdx.x;
   const bool valid = b < Bn;
   if (!valid) b = Bn - 1;
-  __shared__ cf Ls[(D * (D - 1) / 2 > 0) ? D * (D - 1) / 2 : 1][64];
-  const int lane_ = threadIdx.x;
-  PTri<D> X;
-  auto load = [&](const cf* M) {
+  __shared__ cf Ls[tri_n(D)][64];
+  __shared__ cf Gs[D][64];
+  const LdsTri<D> Li{Ls, (int)threadIdx.x};
+  auto load = [&](auto* src, auto& X) {
     sfor<0, D>([&](auto ic) {
       constexpr int i = decltype(ic)::value;
       sfor<0, i + 1>([&](auto jc) {
         constexpr int j = decltype(jc)::value;
-        X.a[P(i, j)] = M[((long long)b * D + i) * D + j];
+        X.a[P(i, j)] = src[((long long)b * D + i) * D + j];
       });
     });
   };
   cf wv[D];
   bool ok = true;
-  load(Rnn);
+  {
+    PTriD<D> N;
+    load(Rnn, N);
+    if (gevd) {
+      ok = chol64<D>(N);
+      cf g[D];
+      ref_row<D>(N, ref, g);
+      sfor<0, D>([&](auto ic) { Gs[decltype(ic)::value][threadIdx.x] = g[decltype(ic)::value]; });
+      tri_inv64<D>(N);
+      store_tri<D>(N, Ls, threadIdx.x);
+    } else {
+      cd ncol[D];
+      sfor<0, D>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        cd c = cd{0.0, 0.0};
+        sfor<0, D>([&](auto kc) {
+          constexpr int k = decltype(kc)::value;
+          if (k == ref) c = hermd<i, k>(N);
+        });
+        ncol[i] = c;
+      });
+      asm volatile("" ::: "memory");
+      PTri<D> A;
+      load(Ryy, A);
+      ok = mwf_filter_mixed<D>(A, ncol, ref, wv);
+    }
+  }
   if (gevd) {
-    float invd[D], ldiag[D];
-    ok = chol<D>(X, invd);
-    to_lds<D>(X, Ls, lane_, ldiag);
-    load(Ryy);
-    gevd_filter<D, RMAX>(X, LTri<D>{Ls, lane_}, invd, ldiag, rank, ref, wv);
-  } else {
-    cf ncol[D];
-    herm_col<D>(X, ref, ncol);
-    load(Ryy);
-    ok = mwf_filter<D>(X, ncol, ref, wv);
+    asm volatile("" ::: "memory");
+    PTri<D> A;
+    load(Ryy, A);
+    cf g[D];
+    sfor<0, D>([&](auto ic) { g[decltype(ic)::value] = Gs[decltype(ic)::value][threadIdx.x]; });
+    congruence<D>(A, Li);
+    gevd_filter_mixed<D, RMAX>(A, Li, g, rank, wv);
   }
   if (valid) {
     sfor<0, D>([&](auto ic) { w[(long long)b * D + decltype(ic)::value] = wv[decltype(ic)::value]; });

@@ -5,15 +5,11 @@
 // work for 64 bins, where the lane-group solvers (solver.hpp) spend most of
 // their issue slots on row broadcasts and idle lanes.
 //
-// GEVD (rank R), the LAPACK sequence zpotrf -> zhegst -> zhetrd -> bisection
-// -> inverse iteration -> back-transform, all statically unrolled on D:
-//   Rnn = L L^H                               (right-looking Cholesky)
-//   C = L^-1 Ryy L^-H                         (zhegs2, lower, itype 1)
+// This file holds the float32 eigen part of the GEVD, statically unrolled on
+// D (the float64 factorisation in front of it is solver_mixed.hpp):
 //   C = Q T Q^H                               (Householder, complex subdiag)
 //   top-R eigenvalues of |T| by bisection     (Sturm counts)
 //   x_r by inverse iteration on |T|, v_r = Q P x_r (P: subdiagonal phases)
-//   w = sum_r (1 - 1/l_r) L^-H v_r (v_r^H L^H e_ref)
-// MWF: w = Ryy^-1 (Ryy - Rnn) e_ref by Cholesky of Ryy.
 #pragma once
 #include "solver.hpp"
 
@@ -30,156 +26,11 @@ struct PTri {
   template <int I, int J>
   DANSE_DEV cf at() const { return a[P(I, J)]; }
 };
-constexpr int SL(int i, int j) { return i * (i - 1) / 2 + j; }   // strictly lower, i > j
-// ... or the STRICTLY lower part in LDS, one 8-byte column per lane
-// ([entry][lane]: every access of a wave is 512 contiguous bytes,
-// conflict-free; a lane only ever touches its own column, so no barrier is
-// needed).  The Cholesky factor lives here during the GEVD so that Ryy's
-// triangle and the Householder work fit in the register file; its (real)
-// diagonal stays in registers.  D(D-1)/2 entries = 28 KB per wave at D = 11,
-// so 5 waves fit a CU's 160 KB.
-template <int D>
-struct LTri {
-  cf (*p)[64];
-  int lane;
-  template <int I, int J>
-  DANSE_DEV cf at() const {
-    static_assert(I > J, "strictly lower entries only");
-    return p[SL(I, J)][lane];
-  }
-  DANSE_DEV cf at_dyn(int e) const { return p[e][lane]; }
-};
-template <int D>
-DANSE_DEV void to_lds(const PTri<D>& X, cf (*p)[64], int lane, float (&ldiag)[D]) {
-  sfor<0, D>([&](auto ic) {
-    constexpr int i = decltype(ic)::value;
-    ldiag[i] = X.a[P(i, i)].re;
-    sfor<0, i>([&](auto jc) {
-      constexpr int j = decltype(jc)::value;
-      p[SL(i, j)][lane] = X.a[P(i, j)];
-    });
-  });
-}
-
 // Full Hermitian element (i, j) from the packed lower triangle.
 template <int I, int J, int D>
 DANSE_DEV cf herm(const PTri<D>& X) {
   if constexpr (I >= J) return X.a[P(I, J)];
   else return conjg(X.a[P(J, I)]);
-}
-
-// Right-looking Cholesky in place: X = L L^H (lower), invd[j] = 1 / L[j][j].
-template <int D>
-DANSE_DEV bool chol(PTri<D>& X, float (&invd)[D]) {
-  bool ok = true;
-  sfor<0, D>([&](auto jc) {
-    constexpr int j = decltype(jc)::value;
-    const float p0 = X.a[P(j, j)].re;
-    ok = ok && (p0 > 1e-37f);
-    const float piv = fmaxf(p0, 1e-37f);
-    const float inv = frsq(piv);
-    X.a[P(j, j)] = cf{piv * inv, 0.0f};
-    invd[j] = inv;
-    sfor<j + 1, D>([&](auto ic) {
-      constexpr int i = decltype(ic)::value;
-      X.a[P(i, j)] = inv * X.a[P(i, j)];
-    });
-    sfor<j + 1, D>([&](auto ic) {
-      constexpr int i = decltype(ic)::value;
-      const cf lij = X.a[P(i, j)];
-      sfor<j + 1, i + 1>([&](auto kc) {
-        constexpr int k = decltype(kc)::value;
-        fms_cc(X.a[P(i, k)], lij, X.a[P(k, j)]);   // X[i][k] -= L[i][j] conj(L[k][j])
-      });
-    });
-  });
-  return ok;
-}
-
-// x <- L^-1 x
-template <int D, typename LM>
-DANSE_DEV void fwd(const LM& L, const float (&invd)[D], cf (&x)[D]) {
-  sfor<0, D>([&](auto ic) {
-    constexpr int i = decltype(ic)::value;
-    cf acc = x[i];
-    sfor<0, i>([&](auto kc) {
-      constexpr int k = decltype(kc)::value;
-      fms_c(acc, L.template at<i, k>(), x[k]);
-    });
-    x[i] = invd[i] * acc;
-  });
-}
-
-// x <- L^-H x
-template <int D, typename LM>
-DANSE_DEV void bwd_h(const LM& L, const float (&invd)[D], cf (&x)[D]) {
-  sfor_down<D, 0>([&](auto ic) {
-    constexpr int i = decltype(ic)::value;
-    cf acc = x[i];
-    sfor<i + 1, D>([&](auto kc) {
-      constexpr int k = decltype(kc)::value;
-      // (L^H)[i][k] = conj(L[k][i])
-      const cf l = L.template at<k, i>();
-      acc.re -= l.re * x[k].re + l.im * x[k].im;
-      acc.im -= l.re * x[k].im - l.im * x[k].re;
-    });
-    x[i] = invd[i] * acc;
-  });
-}
-
-// A <- L^-1 A L^-H on the packed lower triangle (LAPACK zhegs2, itype 1,
-// lower): per column k, scale, axpy, her2 of the trailing block, axpy, and a
-// forward substitution of the column with the trailing block of L.
-template <int D, typename LM>
-DANSE_DEV void hegst(PTri<D>& A, const LM& L, const float (&invd)[D]) {
-  sfor<0, D>([&](auto kc) {
-    constexpr int k = decltype(kc)::value;
-    const float ib = invd[k];
-    const float akk = A.a[P(k, k)].re * ib * ib;
-    A.a[P(k, k)] = cf{akk, 0.0f};
-    if constexpr (k + 1 < D) {
-      const float ct = -0.5f * akk;
-      sfor<k + 1, D>([&](auto ic) {
-        constexpr int i = decltype(ic)::value;
-        const cf l = L.template at<i, k>();
-        cf x = ib * A.a[P(i, k)];
-        x.re = fmaf(ct, l.re, x.re);
-        x.im = fmaf(ct, l.im, x.im);
-        A.a[P(i, k)] = x;
-      });
-      // her2: A[i][j] -= x_i conj(y_j) + y_i conj(x_j), k < j <= i
-      sfor<k + 1, D>([&](auto ic) {
-        constexpr int i = decltype(ic)::value;
-        const cf xi = A.a[P(i, k)], yi = L.template at<i, k>();
-        sfor<k + 1, i + 1>([&](auto jc) {
-          constexpr int j = decltype(jc)::value;
-          cf t = A.a[P(i, j)];
-          fms_cc(t, xi, L.template at<j, k>());
-          fms_cc(t, yi, A.a[P(j, k)]);
-          if constexpr (i == j) t.im = 0.0f;
-          A.a[P(i, j)] = t;
-        });
-      });
-      sfor<k + 1, D>([&](auto ic) {
-        constexpr int i = decltype(ic)::value;
-        const cf l = L.template at<i, k>();
-        cf x = A.a[P(i, k)];
-        x.re = fmaf(ct, l.re, x.re);
-        x.im = fmaf(ct, l.im, x.im);
-        A.a[P(i, k)] = x;
-      });
-      // forward substitution with L[k+1:, k+1:]
-      sfor<k + 1, D>([&](auto ic) {
-        constexpr int i = decltype(ic)::value;
-        cf acc = A.a[P(i, k)];
-        sfor<k + 1, i>([&](auto jc) {
-          constexpr int j = decltype(jc)::value;
-          fms_c(acc, L.template at<i, j>(), A.a[P(j, k)]);
-        });
-        A.a[P(i, k)] = invd[i] * acc;
-      });
-    }
-  });
 }
 
 // Householder tridiagonalisation of the Hermitian A (packed lower), in
@@ -331,12 +182,12 @@ DANSE_DEV void tri_eigvec(const float (&a)[D], const float (&e2)[D], float lam, 
   }
 }
 
-// GEVD filter of one bin: A = Ryy (destroyed), L / invd = Cholesky factor of
-// Rnn (chol).  Returns w in wv.
-template <int D, int RMAX>
-DANSE_DEV void gevd_filter(PTri<D>& A, const LTri<D>& L, const float (&invd)[D], const float (&ldiag)[D], int R,
-                           int ref, cf (&wv)[D]) {
-  hegst<D>(A, L, invd);
+// Top-R eigenpairs of the Hermitian C (packed lower, destroyed):
+// Householder tridiagonalisation, bisection for the eigenvalues (descending),
+// inverse iteration on |T|, subdiagonal phases and the back-transform.
+// fn(r, lambda_r, v_r) is called once per rank r < R (v_r unit 2-norm).
+template <int D, int RMAX, typename Fn>
+DANSE_DEV void gevd_eig(PTri<D>& A, int R, Fn&& fn) {
   cf u0[D], b[D];
   tridiag<D>(A, u0, b);
   float ta[D], e2[D];
@@ -362,11 +213,15 @@ DANSE_DEV void gevd_filter(PTri<D>& A, const LTri<D>& L, const float (&invd)[D],
   lo -= 2.0f * 1.2e-7f * scale + pivmin;
   hi += 2.0f * 1.2e-7f * scale + pivmin;
   const float pert = 1.2e-7f * fmaxf(tnorm, 1e-30f);
-  sfor<0, D>([&](auto ic) { wv[decltype(ic)::value] = cf{0.0f, 0.0f}; });
   float prev[RMAX][D];
   sfor<0, RMAX>([&](auto rc) {
     constexpr int r = decltype(rc)::value;
-    if (r >= R) return;
+    // (rank >= 1 is checked at create time: no runtime test for r = 0, which
+    // would keep the whole eigen work behind a branch and double its
+    // register footprint)
+    if constexpr (r > 0) {
+      if (r >= R) return;
+    }
     // bisection for the (r+1)-th largest eigenvalue: count(x) >= D - r <=> x > lambda_r
     float lo_r = lo, hi_r = hi;
     for (int it = 0; it < 32; ++it) {
@@ -401,44 +256,8 @@ DANSE_DEV void gevd_filter(PTri<D>& A, const LTri<D>& L, const float (&invd)[D],
       fms_c(v[j + 1], u0[j], s2);
       sfor<j + 2, D>([&](auto ic) { fms_c(v[decltype(ic)::value], A.a[P(decltype(ic)::value, j)], s2); });
     });
-    // sr = v^H g with g = L^H e_ref, g_i = conj(L[ref][i]) for i <= ref
-    cf sr = cf{0.0f, 0.0f};
-    sfor<0, D>([&](auto ic) {
-      constexpr int i = decltype(ic)::value;
-      if (i < ref) sr = sr + cmul(v[i], conjg(L.at_dyn(ref * (ref - 1) / 2 + i)));
-      if (i == ref) sr = sr + ldiag[i] * conjg(v[i]);
-    });
-    bwd_h<D>(L, invd, v);
-    const float coef = 1.0f - frcp(lam);
-    const cf cs = coef * sr;
-    sfor<0, D>([&](auto ic) { fma_c(wv[decltype(ic)::value], v[decltype(ic)::value], cs); });
+    fn(r, lam, v);
   });
-}
-
-// Column ref of the full Hermitian matrix: col[i] = X[i][ref].
-template <int D>
-DANSE_DEV void herm_col(const PTri<D>& X, int ref, cf (&col)[D]) {
-  sfor<0, D>([&](auto ic) {
-    constexpr int i = decltype(ic)::value;
-    col[i] = cf{0.0f, 0.0f};
-    sfor<0, D>([&](auto rc) {
-      constexpr int rr = decltype(rc)::value;
-      if (rr == ref) col[i] = herm<i, rr>(X);
-    });
-  });
-}
-
-// MWF filter: A = Ryy (destroyed), ncol = Rnn[:, ref].
-// w = Ryy^-1 (Ryy - Rnn) e_ref, the difference formed first as the reference does.
-template <int D>
-DANSE_DEV bool mwf_filter(PTri<D>& A, const cf (&ncol)[D], int ref, cf (&wv)[D]) {
-  herm_col<D>(A, ref, wv);
-  sfor<0, D>([&](auto ic) { wv[decltype(ic)::value] = wv[decltype(ic)::value] - ncol[decltype(ic)::value]; });
-  float invd[D];
-  const bool ok = chol<D>(A, invd);
-  fwd<D>(A, invd, wv);
-  bwd_h<D>(A, invd, wv);
-  return ok;
 }
 
 }  // namespace lane

@@ -297,7 +297,7 @@ class DanseEngine:
                 else:
                     scm.append(sl[:D, :D].ravel())
         self._w0 = _cf32(np.concatenate(w0))
-        self._scm = _cf32(np.concatenate(scm))
+        self._scm = np.ascontiguousarray(np.concatenate(scm).astype(np.complex128)).view(np.float64)
         ext = [init_complex_filter((F, self.M[k]), p.referenceSensor, **fi).ravel() for k in range(K)]
         self._wExt0 = _cf32(np.concatenate(ext))
         self._tgt0 = self._wExt0.copy()
@@ -312,7 +312,7 @@ class DanseEngine:
             else:
                 extMode.append(L.EXT_RELAX)
         self._extMode = np.array(extMode, dtype=np.int32)
-        beta = np.zeros((S, K), dtype=np.float32)
+        beta = np.zeros((S, K), dtype=np.float64)
         betaE = np.zeros((S, K), dtype=np.float32)
         for s, sc in enumerate(self.scenes):
             for k, nd in enumerate(sc.wasn):
@@ -334,13 +334,13 @@ class DanseEngine:
         c.families = self.famMask
         c.alphaExt = float(p.alphaExternalFilters)
         c.extMode = _ptr(self._extMode, ctypes.c_int32)
-        c.beta, c.betaExt = _ptr(self._beta, ctypes.c_float), _ptr(self._betaE, ctypes.c_float)
+        c.beta, c.betaExt = _ptr(self._beta, ctypes.c_double), _ptr(self._betaE, ctypes.c_float)
         c.winAnalysis, c.winSynthesis = _ptr(self._hA, ctypes.c_float), _ptr(self._hS, ctypes.c_float)
         c.bcEnd, c.upEnd = _ptr(self._bc, ctypes.c_int32), _ptr(self._up, ctypes.c_int32)
         c.flags = _ptr(self._flags, ctypes.c_uint8)
         c.w0, c.wExt0, c.wExtTarget0 = (_ptr(self._w0, ctypes.c_float), _ptr(self._wExt0, ctypes.c_float),
                                         _ptr(self._tgt0, ctypes.c_float))
-        c.scmInit = _ptr(self._scm, ctypes.c_float)
+        c.scmInit = _ptr(self._scm, ctypes.c_double)
         c.keepHistory = int(bool(self.keepHistory))
         c.zLag = _ptr(self._zLag, ctypes.c_uint8)
         c.zPhase = _ptr(self._zPhase, ctypes.c_double)

@@ -82,7 +82,7 @@ typedef struct danse_cfg {
   int32_t families;     /* bitmask of enum danse_family                           */
   float alphaExt;       /* alphaExternalFilters                                   */
   const int32_t* extMode;   /* [K]                                                */
-  const float* beta;        /* [S*K] SCM forgetting factor per (scene, node)      */
+  const double* beta;       /* [S*K] SCM forgetting factor per (scene, node)      */
   const float* betaExt;     /* [S*K] external-filter forgetting factor            */
   const float* winAnalysis; /* [N] */
   const float* winSynthesis;/* [N] */
@@ -96,8 +96,9 @@ typedef struct danse_cfg {
                                scene; NULL = zeros                                 */
   const float* wExt0;       /* initial external filters, per node: [F][M_k] complex */
   const float* wExtTarget0; /* initial external-filter targets, same layout        */
-  const float* scmInit;     /* initial SCM slice per family-node: [D][D] complex,
-                               tiled over bins and scenes (Ryy = Rnn); NULL = 0    */
+  const double* scmInit;    /* initial SCM slice per family-node: [D][D] complex
+                               double, tiled over bins and scenes (Ryy = Rnn;
+                               Rnn is kept in double, Ryy in float); NULL = 0     */
   int32_t keepHistory;      /* 1: keep w / wExt for every iteration (reference
                                layout needs it for the SNR replay)                  */
   /* asynchronous clocks (SROs), host-computed from the event order
@@ -203,9 +204,11 @@ int danse_wola_analysis(const float* x, int32_t C, int32_t T, const int32_t* end
                         const float* win, int32_t N, int32_t Ns, float* out, void* stream);
 
 /* Batched filter update on full SCM pairs (update_w / update_w_gevd,
- * d_classes.py:3320-3387): Ryy, Rnn: [B][D][D] complex (device), w: [B][D].
+ * d_classes.py:3320-3387): Ryy: [B][D][D] complex float, Rnn: [B][D][D]
+ * complex double (device; the noise SCM conditions the update and is
+ * factored in double), w: [B][D] complex float.
  * gevd != 0 -> rank-`rank` GEVD, else MWF. diag: [B] int32 or NULL. */
-int danse_filter_update(const float* Ryy, const float* Rnn, int32_t B, int32_t D, int32_t gevd,
+int danse_filter_update(const float* Ryy, const double* Rnn, int32_t B, int32_t D, int32_t gevd,
                         int32_t rank, int32_t ref, float* w, int32_t* diag, void* stream);
 
 /* Batch-mode SCM contraction (update_covmats_batch, d_classes.py:3272-3304):

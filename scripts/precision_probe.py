@@ -71,7 +71,7 @@ def gevd_mix(Ryy, Rnn, refSensorIdx, rank=1, rq64=False):
     return out
 
 
-def gevd_planA(Ryy, Rnn, refSensorIdx, rank=1):
+def gevd_planA(Ryy, Rnn, refSensorIdx, rank=1, li32=False, cong32=False):
     """The device plan: Ryy as stored (fp32), fp64 Cholesky of Rnn, fp64
     triangular inverse, C = Linv Ryy Linv^H in fp64 rounded to complex64,
     complex64 eigen step, x = Linv^H v in fp64."""
@@ -79,14 +79,18 @@ def gevd_planA(Ryy, Rnn, refSensorIdx, rank=1):
     for f in range(Ryy.shape[0]):
         L = np.linalg.cholesky(Rnn[f])
         Li = sla.solve_triangular(L, np.eye(L.shape[0]), lower=True)
-        C = (Li @ Ryy[f] @ Li.conj().T).astype(np.complex64)
+        if cong32:
+            L32, A32 = Li.astype(np.complex64), Ryy[f].astype(np.complex64)
+            C = L32 @ A32 @ L32.conj().T
+        else:
+            C = (Li @ Ryy[f] @ Li.conj().T).astype(np.complex64)
         s, V = np.linalg.eigh(C)
         idx = np.flip(np.argsort(s))
         s, V = s[idx], V[:, idx]
         g = L.conj().T[:, refSensorIdx].astype(np.complex64)
         for r in range(rank):
             v = V[:, r]
-            x = Li.conj().T @ v.astype(complex)
+            x = (Li.astype(np.complex64).conj().T @ v) if li32 else (Li.conj().T @ v.astype(complex))
             out[f] += (1 - 1 / float(s[r])) * x * complex(v.conj() @ g)
     return out
 
@@ -97,8 +101,8 @@ def run(args):
     sc = make_case_scene(case)
     dp, wp = make_case_params(case)
     sc.get_vad_per_frame(dp.DFTsize, dp.Ns, wp.vadMinProportionActive)
-    fft32 = mode in ('fft32', 'state32', 'all32', 'mixC', 'mixD', 'ryy32', 'rnn32', 'planA')
-    ryyAcc32 = mode == 'planA'
+    fft32 = mode in ('fft32', 'state32', 'all32', 'mixC', 'mixD', 'ryy32', 'rnn32', 'planA', 'planB', 'planC')
+    ryyAcc32 = mode in ('planA', 'planB', 'planC')
     scm32 = mode in ('scm32', 'state32', 'all32')
     solve32 = mode in ('solve32', 'all32')
 
@@ -121,6 +125,10 @@ def run(args):
         O.update_w_gevd = gevd32
     elif mode == 'planA':
         O.update_w_gevd = gevd_planA
+    elif mode == 'planC':
+        O.update_w_gevd = lambda a, b, refSensorIdx, rank=1: gevd_planA(a, b, refSensorIdx, rank, li32=True, cong32=True)
+    elif mode == 'planB':
+        O.update_w_gevd = lambda a, b, refSensorIdx, rank=1: gevd_planA(a, b, refSensorIdx, rank, li32=True)
     elif mode == 'ryy32':
         O.update_w_gevd = lambda a, b, refSensorIdx, rank=1: gevd_mix(a.astype(np.complex64).astype(complex), b, refSensorIdx, rank)
     elif mode == 'rnn32':

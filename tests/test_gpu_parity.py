@@ -67,7 +67,8 @@ def test_filter_update_kat(case, golden_dir):
     g = np.load(golden_dir / f"{case['name']}.npz")
     Ryy, Rnn = kat_inputs(case)
     F, D = case['F'], case['D']
-    a, n = _dev_cf(Ryy), _dev_cf(Rnn)
+    a = _dev_cf(Ryy)
+    n = torch.from_numpy(np.ascontiguousarray(np.asarray(Rnn, dtype=np.complex128)).view(np.float64)).cuda()
     w = torch.empty((F, D, 2), dtype=torch.float32, device='cuda')
     diag = torch.zeros(F, dtype=torch.int32, device='cuda')
     L.check(lib.danse_filter_update(ctypes.c_void_p(a.data_ptr()), ctypes.c_void_p(n.data_ptr()), F, D,
