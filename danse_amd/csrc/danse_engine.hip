@@ -45,7 +45,7 @@ struct danse_engine {
   std::vector<FamNode> fns;   // all family-nodes (owned nodes)
   std::vector<int> chanList;
   std::vector<Class> classes;
-  long long scmStride = 0, wStride = 0, wExtStride = 0, tgtStride = 0, gStride = 0;
+  long long scmStride = 0, wStride = 0, wExtStride = 0, tgtStride = 0;
   std::vector<long long> wExtNodeOff;
   // device
   int *dM = nullptr, *dBase = nullptr, *dBcEnd = nullptr, *dUpEnd = nullptr, *dChan = nullptr;
@@ -58,7 +58,6 @@ struct danse_engine {
   long long* dWExtNodeOff = nullptr;
   const float* y = nullptr;
   cd* Rnn = nullptr;   // complex double (DESIGN.md "Precision"); same element offsets as Ryy
-  cf *Lscr = nullptr, *Gscr = nullptr;   // lane classes: float64-factor hand-over (kernels_lane.hpp)
   cf *Yspec = nullptr, *Zspec = nullptr, *Ryy = nullptr, *wHist = nullptr, *wExtHist = nullptr,
      *wExtTarget = nullptr, *dhat = nullptr;
   float *zPrev = nullptr, *zStream = nullptr, *d = nullptr;
@@ -327,8 +326,6 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
       scmOff += fn.packed ? (long long)F * fn.D * (fn.D + 1) / 2 : (long long)F * fn.D * fn.D;
       fn.wOff = wOff;
       wOff += histW * F * fn.D;
-      fn.gOff = eng->gStride;
-      eng->gStride += (long long)F * fn.D;
       eng->fns.push_back(fn);
     }
   }
@@ -447,8 +444,6 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
   }
   HIPCHK(dalloc(&eng->Ryy, (size_t)S * eng->scmStride));
   HIPCHK(dalloc(&eng->Rnn, (size_t)S * eng->scmStride));
-  HIPCHK(dalloc(&eng->Lscr, (size_t)S * eng->scmStride));
-  HIPCHK(dalloc(&eng->Gscr, (size_t)S * eng->gStride));
   HIPCHK(dalloc(&eng->wHist, (size_t)S * eng->wStride));
   HIPCHK(dalloc(&eng->wExtHist, (size_t)S * eng->wExtStride));
   HIPCHK(dalloc(&eng->wExtTarget, (size_t)S * eng->tgtStride));
@@ -544,7 +539,7 @@ void danse_engine_destroy(danse_engine* eng) {
                   eng->dBeta, eng->dBetaExt,
                   eng->dhA, eng->dhS, eng->dNorm, eng->dTw, eng->dWExtNodeOff, eng->Yspec,
                   eng->ownZspec ? eng->Zspec : nullptr, eng->Ryy,
-                  eng->Rnn, eng->Lscr, eng->Gscr, eng->wHist, eng->wExtHist, eng->wExtTarget, eng->dhat, eng->zPrev, eng->zStream, eng->d,
+                  eng->Rnn, eng->wHist, eng->wExtHist, eng->wExtTarget, eng->dhat, eng->zPrev, eng->zStream, eng->d,
                   eng->diag, eng->dW0, eng->dScm0, eng->dExt0, eng->dTgt0, eng->dFnAll, eng->dInitW0Off,
                   eng->dInitScmOff, eng->dExtSrcOff, eng->dTgtOff, eng->dFsTab, eng->wIR, eng->dSn};
   for (void* p : ptrs)
@@ -583,7 +578,7 @@ static UpdateArgs make_update(danse_engine* e, int r) {
   a.chanList = e->dChan; a.flags = e->dFlags; a.Yspec = e->Yspec; a.Zspec = e->Zspec;
   a.zLag = e->dZLag; a.zPhase = e->dZPhase;
   a.Ryy = e->Ryy; a.Rnn = e->Rnn; a.scmStride = e->scmStride;
-  a.Lscr = e->Lscr; a.Gscr = e->Gscr; a.gStride = e->gStride; a.wHist = e->wHist; a.wStride = e->wStride;
+  a.wHist = e->wHist; a.wStride = e->wStride;
   a.wHistory = e->keepHistory; a.wExtHist = e->wExtHist; a.wExtStride = e->wExtStride; a.wExtHistory = e->keepHistory;
   a.wExtTarget = e->wExtTarget; a.tgtStride = e->tgtStride; a.dhat = e->dhat; a.beta = e->dBeta;
   a.betaExt = e->dBetaExt; a.alphaExt = e->alphaExt; a.gevd = e->gevd; a.rank = e->rank; a.diag = e->diag;

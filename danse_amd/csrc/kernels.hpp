@@ -35,7 +35,6 @@ struct FamNode {
   long long wOff;     // complex-element offset within one scene's w-history block
   long long wExtOff;  // DANSE only: offset within one scene's wExt-history block
   long long tgtOff;   // DANSE only: offset within one scene's target block
-  long long gOff;     // offset within one scene's g = L^H e_ref hand-over block ([D][F])
 };
 
 struct UpdateArgs {
@@ -52,9 +51,6 @@ struct UpdateArgs {
   cf* Ryy;                 // per scene stride scmStride (complex float)
   cd* Rnn;                 // same element offsets, complex double (DESIGN.md "Precision")
   long long scmStride;
-  cf* Lscr;                // lane classes: float32 L^-1 hand-over, the Ryy layout
-  cf* Gscr;                // lane classes: g = L^H e_ref hand-over, per scene stride gStride
-  long long gStride;
   cf* wHist;               // per scene stride wStride
   long long wStride;
   int wHistory;            // 1: [R+1][F][D] per family-node; 0: 2 slots

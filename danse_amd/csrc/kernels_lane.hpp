@@ -8,15 +8,15 @@
 // every SCM entry as one coalesced access (512 B for the float32 Ryy, 1 KiB
 // for the float64 Rnn).
 //
-// Two launches per round (the float64 factorisation and the float32 eigen
-// work each get the whole register file):
-//   scm_factor_kernel_lane  SCM recursion (Ryy float32 or Rnn float64, as the
-//                           VAD selects); on solve frames the float64
-//                           Cholesky + inverse of Rnn, handed over as the
-//                           float32 Li = L^-1 ([tri][F], the Ryy layout) and
-//                           g = L^H e_ref ([D][F]); MWF solves completely here
-//   gevd_tail_kernel_lane   C = Li Ryy Li^H, eigen part, w, external filters,
-//                           dhat
+// Per lane, in two phases that never hold their big arrays at once:
+//   1. SCM recursion (Ryy float32 or Rnn float64, as the VAD selects); on
+//      solve frames the float64 Cholesky + inverse of Rnn, handed to phase 2
+//      through LDS as the float32 Li = L^-1 and g = L^H e_ref ([entry][lane],
+//      39 KiB per wave at D = 11); MWF solves completely here, in float64;
+//   2. C = Li Ryy Li^H (Ryy re-read, L2), eigen part, w, external filters,
+//      dhat.
+// (No SLP packing in these classes -- build.py -- and no runtime rank test
+// for r = 0 in gevd_eig: either one doubles the register footprint.)
 #pragma once
 #include "kernels.hpp"
 #include "solver_mixed.hpp"
@@ -40,8 +40,8 @@ DANSE_DEV LaneIdx lane_index(const UpdateArgs& a) {
   return x;
 }
 
-template <int D, bool GEVD>
-__global__ void __launch_bounds__(64) scm_factor_kernel_lane(const UpdateArgs a) {
+template <int D, int RMAX, bool GEVD>
+__global__ void __launch_bounds__(64) update_kernel_lane(const UpdateArgs a) {
   using namespace lane;
   constexpr int NT = tri_n(D);
   const LaneIdx ix = lane_index(a);
@@ -51,7 +51,8 @@ __global__ void __launch_bounds__(64) scm_factor_kernel_lane(const UpdateArgs a)
   const uint8_t fl = a.flags[(((long long)r * a.S + s) * kMaxFam + d.fam) * a.K + d.k];
   const int opY = fl & 3, opN = (fl >> 2) & 3;
   const bool solve = (fl & DANSE_FLAG_SOLVE) != 0 && (fl & DANSE_FLAG_PREGIVEN) == 0;
-  if (!(opY || opN || solve)) return;   // no SCM work this round (pregiven replay)
+  __shared__ cf Ls[NT][64];
+  __shared__ cf Gs[D][64];
 
   cf y[D];
   if (opY || opN) {
@@ -79,6 +80,7 @@ __global__ void __launch_bounds__(64) scm_factor_kernel_lane(const UpdateArgs a)
       sfor<0, NT>([&](auto ec) { a.Ryy[base + (long long)decltype(ec)::value * F] = A.a[decltype(ec)::value]; });
     }
   }
+  asm volatile("" ::: "memory");   // the Ryy work above is done before the float64 triangle loads
   PTriD<D> N;
   if (opN || solve) {
     sfor<0, NT>([&](auto ec) { N.a[decltype(ec)::value] = a.Rnn[base + (long long)decltype(ec)::value * F]; });
@@ -104,20 +106,17 @@ __global__ void __launch_bounds__(64) scm_factor_kernel_lane(const UpdateArgs a)
       sfor<0, NT>([&](auto ec) { a.Rnn[base + (long long)decltype(ec)::value * F] = N.a[decltype(ec)::value]; });
     }
   }
-  if (!solve) return;
-
   bool ok = true;
+  if (solve) {
   if constexpr (GEVD) {
     // float64 Cholesky + inverse of Rnn; hand-over in float32
-    ok = chol64<D>(N);
+    double invd[D];
+    ok = chol64<D>(N, invd);
     cf g[D];
     ref_row<D>(N, d.ref, g);
-    tri_inv64<D>(N);
-    if (valid) {
-      sfor<0, NT>([&](auto ec) { a.Lscr[base + (long long)decltype(ec)::value * F] = cfk(N.a[decltype(ec)::value]); });
-      const long long gb = (long long)s * a.gStride + d.gOff + f;
-      sfor<0, D>([&](auto ic) { a.Gscr[gb + (long long)decltype(ic)::value * F] = g[decltype(ic)::value]; });
-    }
+    tri_inv64<D>(N, invd);
+    store_tri<D>(N, Ls, threadIdx.x);
+    sfor<0, D>([&](auto ic) { Gs[decltype(ic)::value][threadIdx.x] = g[decltype(ic)::value]; });
   } else {
     // MWF, float64 throughout: w = Ryy^-1 (Ryy - Rnn) e_ref
     cd ncol[D];
@@ -140,38 +139,24 @@ __global__ void __launch_bounds__(64) scm_factor_kernel_lane(const UpdateArgs a)
     if (valid) sfor<0, D>([&](auto ic) { wNext[decltype(ic)::value] = w[decltype(ic)::value]; });
   }
   if (!ok && valid) atomicOr(&a.diag[(s * a.K + d.k) * kMaxFam + d.fam], 1);
-}
-
-template <int D, int RMAX, bool GEVD>
-__global__ void __launch_bounds__(64) gevd_tail_kernel_lane(const UpdateArgs a) {
-  using namespace lane;
-  constexpr int NT = tri_n(D);
-  const LaneIdx ix = lane_index(a);
-  const int F = a.F, f = ix.f, s = ix.s, r = a.r;
-  const bool valid = ix.valid;
-  const FamNode d = a.fn[ix.fni];
-  const uint8_t fl = a.flags[(((long long)r * a.S + s) * kMaxFam + d.fam) * a.K + d.k];
-  const bool solve = (fl & DANSE_FLAG_SOLVE) != 0;
+  }
+  asm volatile("" ::: "memory");
   const bool pregiven = (fl & DANSE_FLAG_PREGIVEN) != 0;
-  const long long base = (long long)s * a.scmStride + d.scmOff + f;
-
+  const bool solveT = (fl & DANSE_FLAG_SOLVE) != 0;
   const long long wBase = (long long)s * a.wStride + d.wOff;
   const int slotPrev = a.wHistory ? r : (r & 1);
   const int slotNext = a.wHistory ? r + 1 : ((r + 1) & 1);
   cf* wPrev = a.wHist + wBase + ((long long)slotPrev * F + f) * D;
   cf* wNext = a.wHist + wBase + ((long long)slotNext * F + f) * D;
   cf w[D];
-  if (pregiven || (solve && !GEVD)) {
+  if (pregiven || (solveT && !GEVD)) {
     // pre-given history, or the MWF filter scm_factor_kernel_lane solved
     sfor<0, D>([&](auto ic) { w[decltype(ic)::value] = wNext[decltype(ic)::value]; });
-  } else if (solve) {
+  } else if (solveT) {
     if constexpr (GEVD) {
-      __shared__ cf Ls[NT][64];
-      sfor<0, NT>([&](auto ec) { Ls[decltype(ec)::value][threadIdx.x] = a.Lscr[base + (long long)decltype(ec)::value * F]; });
       const LdsTri<D> Li{Ls, (int)threadIdx.x};
       cf g[D];
-      const long long gb = (long long)s * a.gStride + d.gOff + f;
-      sfor<0, D>([&](auto ic) { g[decltype(ic)::value] = a.Gscr[gb + (long long)decltype(ic)::value * F]; });
+      sfor<0, D>([&](auto ic) { g[decltype(ic)::value] = Gs[decltype(ic)::value][threadIdx.x]; });
       PTri<D> A;
       sfor<0, NT>([&](auto ec) { A.a[decltype(ec)::value] = a.Ryy[base + (long long)decltype(ec)::value * F]; });
       congruence<D>(A, Li);
@@ -220,6 +205,7 @@ __global__ void __launch_bounds__(64) gevd_tail_kernel_lane(const UpdateArgs a) 
   if (valid) a.dhat[((((long long)d.fam * a.S + s) * a.K + d.k) * a.R + r) * F + f] = dh;
 }
 
+
 // Stand-alone batched filter update (danse_filter_update) on full [B][D][D]
 // SCM pairs (Ryy complex float, Rnn complex double): one batch item per lane,
 // the same two phases (float64 factorisation, float32 eigen work) in one
@@ -249,11 +235,12 @@ __global__ void __launch_bounds__(64) filter_update_kernel_lane(const cf* Ryy, c
     PTriD<D> N;
     load(Rnn, N);
     if (gevd) {
-      ok = chol64<D>(N);
+      double invd[D];
+      ok = chol64<D>(N, invd);
       cf g[D];
       ref_row<D>(N, ref, g);
       sfor<0, D>([&](auto ic) { Gs[decltype(ic)::value][threadIdx.x] = g[decltype(ic)::value]; });
-      tri_inv64<D>(N);
+      tri_inv64<D>(N, invd);
       store_tri<D>(N, Ls, threadIdx.x);
     } else {
       cd ncol[D];

@@ -41,17 +41,28 @@ DANSE_DEV cd hermd(const PTriD<D>& X) {
   else return conjg(X.a[P(J, I)]);
 }
 
-// Right-looking Cholesky in place, float64: X = L L^H (lower, real diagonal).
+// 1 / sqrt(x), float64: hardware estimate + two Newton steps (no IEEE
+// divide / sqrt sequences on the pivot chain).
+DANSE_DEV double rsqrt64(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  y = y * fma(-0.5 * x * y, y, 1.5);
+  y = y * fma(-0.5 * x * y, y, 1.5);
+  return y;
+}
+
+// Right-looking Cholesky in place, float64: X = L L^H (lower, real diagonal);
+// invd[j] = 1 / L[j][j].
 template <int D>
-DANSE_DEV bool chol64(PTriD<D>& X) {
+DANSE_DEV bool chol64(PTriD<D>& X, double (&invd)[D]) {
   bool ok = true;
   sfor<0, D>([&](auto jc) {
     constexpr int j = decltype(jc)::value;
     const double p0 = X.a[P(j, j)].re;
     ok = ok && (p0 > 1e-300);
-    const double l = sqrt(p0 > 1e-300 ? p0 : 1e-300);
-    const double inv = 1.0 / l;
-    X.a[P(j, j)] = cd{l, 0.0};
+    const double piv = p0 > 1e-300 ? p0 : 1e-300;
+    const double inv = rsqrt64(piv);
+    invd[j] = inv;
+    X.a[P(j, j)] = cd{piv * inv, 0.0};
     sfor<j + 1, D>([&](auto ic) {
       constexpr int i = decltype(ic)::value;
       X.a[P(i, j)] = inv * X.a[P(i, j)];
@@ -87,10 +98,10 @@ DANSE_DEV void ref_row(const PTriD<D>& L, int ref, cf (&g)[D]) {
 // Li[i][j] = -(1 / L[j][j]) sum_{k=j+1..i} Li[i][k] L[k][j], columns from the
 // last, rows from the bottom (so every L entry is read before it is replaced).
 template <int D>
-DANSE_DEV void tri_inv64(PTriD<D>& X) {
+DANSE_DEV void tri_inv64(PTriD<D>& X, const double (&invd)[D]) {
   sfor_down<D, 0>([&](auto jc) {
     constexpr int j = decltype(jc)::value;
-    const double ajj = 1.0 / X.a[P(j, j)].re;
+    const double ajj = invd[j];
     X.a[P(j, j)] = cd{ajj, 0.0};
     sfor_down<D, j + 1>([&](auto ic) {
       constexpr int i = decltype(ic)::value;
@@ -195,13 +206,14 @@ DANSE_DEV bool mwf_filter_mixed(const PTri<D>& A, const cd (&ncol)[D], int ref, 
     });
     r[i] = c - ncol[i];
   });
-  const bool ok = chol64<D>(X);
+  double invd[D];
+  const bool ok = chol64<D>(X, invd);
   // r <- L^-1 r
   sfor<0, D>([&](auto ic) {
     constexpr int i = decltype(ic)::value;
     cd acc = r[i];
     sfor<0, i>([&](auto kc) { fms_c(acc, X.a[P(i, decltype(kc)::value)], r[decltype(kc)::value]); });
-    r[i] = (1.0 / X.a[P(i, i)].re) * acc;
+    r[i] = invd[i] * acc;
   });
   // r <- L^-H r
   sfor_down<D, 0>([&](auto ic) {
@@ -211,7 +223,7 @@ DANSE_DEV bool mwf_filter_mixed(const PTri<D>& A, const cd (&ncol)[D], int ref, 
       constexpr int k = decltype(kc)::value;
       fms_c(acc, conjg(X.a[P(k, i)]), r[k]);
     });
-    r[i] = (1.0 / X.a[P(i, i)].re) * acc;
+    r[i] = invd[i] * acc;
   });
   sfor<0, D>([&](auto ic) { wv[decltype(ic)::value] = cfk(r[decltype(ic)::value]); });
   return ok;

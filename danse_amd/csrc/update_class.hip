@@ -24,14 +24,9 @@ void DANSE_CAT(launch_update_d, DANSE_DMAX)(const UpdateArgs& a, hipStream_t st)
   if constexpr (kG == 1) {
     const long long lanes = (long long)a.S * a.nFN * a.F;
     const unsigned grid = (unsigned)((lanes + 63) / 64);
-    if (!a.gevd) {
-      hipLaunchKernelGGL((scm_factor_kernel_lane<kD, false>), dim3(grid), dim3(64), 0, st, a);
-      hipLaunchKernelGGL((gevd_tail_kernel_lane<kD, 1, false>), dim3(grid), dim3(64), 0, st, a);
-    } else {
-      hipLaunchKernelGGL((scm_factor_kernel_lane<kD, true>), dim3(grid), dim3(64), 0, st, a);
-      if (r1) hipLaunchKernelGGL((gevd_tail_kernel_lane<kD, 1, true>), dim3(grid), dim3(64), 0, st, a);
-      else hipLaunchKernelGGL((gevd_tail_kernel_lane<kD, kRMax, true>), dim3(grid), dim3(64), 0, st, a);
-    }
+    if (!a.gevd) hipLaunchKernelGGL((update_kernel_lane<kD, 1, false>), dim3(grid), dim3(64), 0, st, a);
+    else if (r1) hipLaunchKernelGGL((update_kernel_lane<kD, 1, true>), dim3(grid), dim3(64), 0, st, a);
+    else hipLaunchKernelGGL((update_kernel_lane<kD, kRMax, true>), dim3(grid), dim3(64), 0, st, a);
   } else if constexpr (kG == 64) {
     const unsigned grid = (unsigned)(a.S * a.nFN * a.F);
     if (r1) hipLaunchKernelGGL((update_kernel_big<kD, 1>), dim3(grid), dim3(64), 0, st, a);
