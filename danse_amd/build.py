@@ -23,7 +23,7 @@ CSRC = HERE / 'csrc'
 OBJ = HERE / '_obj'
 OUT = HERE / 'libdanse_mi355x.so'
 INC = HERE.parent / 'include'
-CLASSES = list(range(1, 17)) + [24, 32, 40, 48, 56, 64]
+CLASSES = list(range(1, 13)) + [16, 24, 32, 40, 48, 56, 64]
 LANE_MAX_D = 12   # csrc/classes.hpp kLaneMaxD
 FLAGS = ['--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC']
 

@@ -104,14 +104,14 @@ struct HerkNode {
 DANSE_DEV void store_scm(cf* p, cf v) { *p = v; }
 DANSE_DEV void store_scm(cd* p, cf v) { *p = cdk(v); }
 
-// (TN: complex float, or complex double for the engine's Rnn, which the
-// mixed-precision filter update factors in float64)
+// (T: complex float for the stand-alone operator, complex double for the
+// engine, whose solve classes take both SCMs in double)
 template <int NT, typename TN>
 __global__ void __launch_bounds__(64) herk_kernel(const cf* __restrict__ Y, const cf* __restrict__ Z, int S, int K,
                                                   int MT, int nseg, const int* __restrict__ base,
                                                   const HerkNode* __restrict__ nodes, int nNodes,
                                                   const int* __restrict__ frames, const int* __restrict__ nvad,
-                                                  cf* __restrict__ Ryy, TN* __restrict__ Rnn) {
+                                                  TN* __restrict__ Ryy, TN* __restrict__ Rnn) {
   constexpr int F = 513;
   constexpr int NP = NT * (NT + 1) / 2;
   const int l = threadIdx.x;
@@ -190,8 +190,8 @@ __global__ void __launch_bounds__(64) herk_kernel(const cf* __restrict__ Y, cons
               store_scm(Rnn + e0, c);
               if (row != col) store_scm(Rnn + e1, conjg(c));
             } else {
-              Ryy[e0] = c;
-              if (row != col) Ryy[e1] = conjg(c);
+              store_scm(Ryy + e0, c);
+              if (row != col) store_scm(Ryy + e1, conjg(c));
             }
           }
         }
@@ -405,8 +405,8 @@ struct danse_batch {
   HerkNode* dNodes = nullptr;
   std::vector<HerkNode> nodes;
   float *dWin = nullptr, *dBetaExt = nullptr, *dFramesTD = nullptr, *dD_ = nullptr;
-  cd* Rnn = nullptr;   // complex double (filter update in mixed precision)
-  cf *dTw = nullptr, *Y = nullptr, *Z = nullptr, *Ryy = nullptr, *wHist = nullptr, *wExtHist = nullptr,
+  cd *Ryy = nullptr, *Rnn = nullptr;   // complex double (the solve classes' input)
+  cf *dTw = nullptr, *Y = nullptr, *Z = nullptr, *wHist = nullptr, *wExtHist = nullptr,
      *tgt = nullptr, *dhat = nullptr, *wTmp = nullptr;
   double* dCost = nullptr;
   int* dDiag = nullptr;
@@ -652,7 +652,7 @@ int danse_batch_run(danse_batch* eng, void* stream) {
       }
       int k1 = k + 1;
       while (k1 < K && eng->D[k1] == D && eng->doSolve[(size_t)it * K + k1]) ++k1;
-      const cf* Ry = eng->Ryy + eng->scmOff[k];
+      const cd* Ry = eng->Ryy + eng->scmOff[k];
       const cd* Rn = eng->Rnn + eng->scmOff[k];
       if (!launch_filter_update_class(class_dmax(D), Ry, Rn, (k1 - k) * S * F, D, eng->gevd, eng->rank, eng->ref,
                                       eng->wTmp, eng->dDiag, st))

@@ -1,10 +1,10 @@
 // Size classes of the update / filter kernels, one translation unit each
 // (update_class.hip compiled with -DDANSE_DMAX=N, so the build parallelises;
 // the engine dispatches by DMAX at launch time):
-//   D <= kLaneMaxD   one bin per LANE, packed-triangle SCMs (solver1.hpp)
-//   D in 13..16      lane groups of G = 16, one row per lane (solver.hpp)
-//   D in 17..64      one bin per wavefront, runtime pivot loops (solver64.hpp),
-//                    DMAX = D rounded up to a multiple of 8
+//   D <= kLaneMaxD   one bin per LANE, packed-triangle SCMs (kernels_lane.hpp,
+//                    solver_mixed.hpp)
+//   D in 13..64      one bin per wavefront, runtime pivot loops (kernels_big.hpp,
+//                    solver64m.hpp), DMAX = D rounded up to a multiple of 8
 #pragma once
 #include "kernels.hpp"
 
@@ -12,19 +12,18 @@ namespace danse {
 
 constexpr int kMaxDMax = 64;
 constexpr int kLaneMaxD = 12;
-constexpr int class_dmax(int D) { return D <= 16 ? D : ((D + 7) / 8) * 8; }
-constexpr int class_group(int DMAX) { return DMAX <= kLaneMaxD ? 1 : (DMAX <= 16 ? 16 : 64); }
+constexpr int class_dmax(int D) { return D <= kLaneMaxD ? D : ((D + 7) / 8) * 8; }
+constexpr int class_group(int DMAX) { return DMAX <= kLaneMaxD ? 1 : 64; }
 // SCM storage of a class: packed lower triangle, bin-minor ([D(D+1)/2][F])
 // for the lane kernels; full rows ([F][D][D]) otherwise.
 constexpr bool class_packed(int D) { return D <= kLaneMaxD; }
 
 #define DANSE_FOR_EACH_CLASS(X) \
-  X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16) X(24) X(32) X(40) \
-  X(48) X(56) X(64)
+  X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(16) X(24) X(32) X(40) X(48) X(56) X(64)
 
 #define DANSE_DECLARE_CLASS(N)                                                                      \
   void launch_update_d##N(const UpdateArgs& a, hipStream_t st);                                     \
-  void launch_filter_update_d##N(const cf* Ryy, const cd* Rnn, int B, int D, int gevd, int rank,   \
+  void launch_filter_update_d##N(const cd* Ryy, const cd* Rnn, int B, int D, int gevd, int rank,   \
                                  int ref, cf* w, int* diag, hipStream_t st);
 DANSE_FOR_EACH_CLASS(DANSE_DECLARE_CLASS)
 #undef DANSE_DECLARE_CLASS
@@ -39,7 +38,7 @@ inline bool launch_update_class(int DMAX, const UpdateArgs& a, hipStream_t st) {
   }
 }
 
-inline bool launch_filter_update_class(int DMAX, const cf* Ryy, const cd* Rnn, int B, int D, int gevd, int rank,
+inline bool launch_filter_update_class(int DMAX, const cd* Ryy, const cd* Rnn, int B, int D, int gevd, int rank,
                                        int ref, cf* w, int* diag, hipStream_t st) {
   switch (DMAX) {
 #define DANSE_CASE(N) \

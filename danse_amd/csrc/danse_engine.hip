@@ -839,7 +839,7 @@ int danse_wola_analysis(const float* x, int32_t C, int32_t T, const int32_t* end
   return 0;
 }
 
-int danse_filter_update(const float* Ryy, const double* Rnn, int32_t B, int32_t D, int32_t gevd, int32_t rank,
+int danse_filter_update(const double* Ryy, const double* Rnn, int32_t B, int32_t D, int32_t gevd, int32_t rank,
                         int32_t ref, float* w, int32_t* diag, void* stream) {
   danse_engine* eng = nullptr;
   if (D < 1 || D > 64) return fail(nullptr, "D must be in [1, 64]");
@@ -848,7 +848,7 @@ int danse_filter_update(const float* Ryy, const double* Rnn, int32_t B, int32_t 
   int G, DM;
   pick_class(D, G, DM);
   hipStream_t st = (hipStream_t)stream;
-  const cf* a = (const cf*)Ryy;
+  const cd* a = (const cd*)Ryy;
   const cd* n = (const cd*)Rnn;
   cf* o = (cf*)w;
   launch_filter_update_class(DM, a, n, B, D, gevd, rank, ref, o, diag, st);

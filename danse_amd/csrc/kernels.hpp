@@ -12,7 +12,8 @@
 //       analysis of the z frame every receiver will use
 //        (process_incoming_signals_buffers + build_ytilde,
 //         d_classes.py:1701-1807,1893-1934).
-//   update_kernel (one wavefront per 64/G frequency bins of one family-node):
+//   update kernels (kernels_lane.hpp: one bin per lane, D <= 12;
+//       kernels_big.hpp: one bin per wavefront, D <= 64):
 //       SCM update (d_classes.py:2048-2267), filter update (update_w /
 //       update_w_gevd, d_classes.py:3320-3387), external filters
 //       (d_classes.py:1627-1694), dhat = w^H yhat (d_base.py:2075).
@@ -128,141 +129,5 @@ DANSE_DEV void node_bin_tail(const UpdateArgs& a, const FamNode& d, int s, int f
     a.dhat[((((long long)d.fam * a.S + s) * a.K + d.k) * a.R + r) * F + f] = dh;
   }
 }
-
-template <int G, int DMAX, int RMAX>
-__global__ void __launch_bounds__(64) update_kernel(const UpdateArgs a) {
-  static_assert(DMAX <= G, "a lane group must hold every row");
-  constexpr int NB = 64 / G;
-  __shared__ SolverLDS<DMAX> lds[NB];
-  const int lane = threadIdx.x;
-  const int li = lane & (G - 1);
-  const int gi = lane / G;
-  const int F = a.F;
-  const int nBB = (F + NB - 1) / NB;
-  const int bb = blockIdx.x % nBB;
-  const int t = blockIdx.x / nBB;
-  const int fni = t % a.nFN;
-  const int s = t / a.nFN;
-  const FamNode d = a.fn[fni];
-  const int D = d.D;
-  int f = bb * NB + gi;
-  const bool valid = f < F;
-  if (!valid) f = F - 1;
-  const bool act = li < D;
-  const int r = a.r;
-  const uint8_t fl = a.flags[(((long long)r * a.S + s) * kMaxFam + d.fam) * a.K + d.k];
-  const int opY = fl & 3, opN = (fl >> 2) & 3;
-  const bool solve = (fl & DANSE_FLAG_SOLVE) != 0;
-
-  // ---- observation vector yhat_li
-  const cf y = load_y(a, d, s, f, li, act);
-  const double beta = a.beta[s * a.K + d.k];
-  const long long matOff = (long long)s * a.scmStride + d.scmOff + (long long)f * D * D;
-  const int rowc = act ? li : 0;
-
-  // Ryy row in float32; Rnn row averaged in float64 (then rounded for this
-  // class's float32 solver)
-  cf A[DMAX], B[DMAX];
-  const bool needY = (opY != 0) || solve;
-  const bool needN = (opN != 0) || solve;
-  if (needY) {
-    sfor<0, DMAX>([&](auto cc) {
-      constexpr int c = decltype(cc)::value;
-      const int cl = (c < D) ? c : D - 1;
-      const cf v = a.Ryy[matOff + (long long)rowc * D + cl];
-      A[c] = (act && c < D) ? v : cf{0.0f, 0.0f};
-    });
-  }
-  if (opY) {
-    const float by = (float)beta, cy = (opY == DANSE_OP_SET) ? (float)(1.0 / D) : (float)((1.0 - beta) / D);
-    sfor<0, DMAX>([&](auto cc) {
-      constexpr int c = decltype(cc)::value;
-      const cf yc = gbcast<G, c>(y);
-      const cf yy = cy * mulc(y, yc);   // y = 0 on lanes >= D
-      A[c] = (opY == DANSE_OP_SET) ? yy : by * A[c] + yy;
-    });
-    if (act && valid) {
-      sfor<0, DMAX>([&](auto cc) {
-        constexpr int c = decltype(cc)::value;
-        if (c < D) a.Ryy[matOff + (long long)li * D + c] = A[c];
-      });
-    }
-  }
-  if (needN) {
-    const double cy = (opN == DANSE_OP_SET) ? 1.0 / D : (1.0 - beta) / D;
-    const double cx = (opN == DANSE_OP_SET) ? 0.0 : beta;
-    const cd yl = cdk(y);
-    sfor<0, DMAX>([&](auto cc) {
-      constexpr int c = decltype(cc)::value;
-      const int cl = (c < D) ? c : D - 1;
-      cd x = a.Rnn[matOff + (long long)rowc * D + cl];
-      if (!(act && c < D)) x = cd{0.0, 0.0};
-      if (opN) {
-        cd yy = cd{0.0, 0.0};
-        fma_cc(yy, yl, cdk(gbcast<G, c>(y)));
-        x = cx * x;
-        x.re = fma(cy, yy.re, x.re);
-        x.im = fma(cy, yy.im, x.im);
-        if (act && valid && c < D) a.Rnn[matOff + (long long)li * D + c] = x;
-      }
-      B[c] = cfk(x);
-    });
-  }
-
-  // ---- filter
-  const long long wBase = (long long)s * a.wStride + d.wOff;
-  const int slotPrev = a.wHistory ? r : (r & 1);
-  const int slotNext = a.wHistory ? r + 1 : ((r + 1) & 1);
-  cf* wPrev = a.wHist + wBase + ((long long)slotPrev * F + f) * D;
-  cf* wNext = a.wHist + wBase + ((long long)slotNext * F + f) * D;
-  cf w;
-  const bool pregiven = (fl & DANSE_FLAG_PREGIVEN) != 0;
-  if (pregiven) {
-    w = act ? wNext[act ? li : 0] : cf{0.0f, 0.0f};
-  } else if (solve) {
-    bool ok = true;
-    if (a.gevd) w = gevd_filter<G, DMAX, RMAX>(A, B, lds[gi], li, D, a.rank, d.ref, ok);
-    else w = mwf_filter<G, DMAX>(A, B, lds[gi], li, D, d.ref, ok);
-    if (!ok && li == 0 && valid) atomicOr(&a.diag[(s * a.K + d.k) * kMaxFam + d.fam], 1);
-  } else {
-    w = act ? wPrev[act ? li : 0] : cf{0.0f, 0.0f};
-  }
-  if (act && valid && !pregiven) wNext[li] = w;
-
-  const cf dh = gsum<G>(act ? cmul(w, y) : cf{0.0f, 0.0f});
-  node_bin_tail(a, d, s, f, li, fl, pregiven, valid, w, y, dh);
-}
-
-// Stand-alone batched filter update (danse_filter_update): one bin per lane
-// group, Ryy / Rnn as [B][D][D] complex64.
-template <int G, int DMAX, int RMAX>
-__global__ void __launch_bounds__(64) filter_update_kernel(const cf* Ryy, const cd* Rnn, int B, int D, int gevd,
-                                                          int rank, int ref, cf* w, int* diag) {
-  constexpr int NB = 64 / G;
-  __shared__ SolverLDS<DMAX> lds[NB];
-  const int li = threadIdx.x & (G - 1);
-  const int gi = threadIdx.x / G;
-  int b = blockIdx.x * NB + gi;
-  const bool valid = b < B;
-  if (!valid) b = B - 1;
-  const bool act = li < D;
-  const int row = act ? li : 0;
-  cf A[DMAX], Bm[DMAX];
-  sfor<0, DMAX>([&](auto cc) {
-    constexpr int c = decltype(cc)::value;
-    const int cl = (c < D) ? c : D - 1;
-    const cf a = Ryy[((long long)b * D + row) * D + cl];
-    const cf n = cfk(Rnn[((long long)b * D + row) * D + cl]);
-    A[c] = (act && c < D) ? a : cf{0.0f, 0.0f};
-    Bm[c] = (act && c < D) ? n : cf{0.0f, 0.0f};
-  });
-  bool ok = true;
-  cf wv;
-  if (gevd) wv = gevd_filter<G, DMAX, RMAX>(A, Bm, lds[gi], li, D, rank, ref, ok);
-  else wv = mwf_filter<G, DMAX>(A, Bm, lds[gi], li, D, ref, ok);
-  if (act && valid) w[(long long)b * D + li] = wv;
-  if (diag && li == 0 && valid) diag[b] = ok ? 0 : 1;
-}
-
 
 }  // namespace danse

@@ -1,18 +1,18 @@
 // update / filter kernels for large filter dimensions (16 < D <= 64): one
 // frequency bin per wavefront, rows in chunked vector registers
-// (solver64.hpp).  Same per-bin work as update_kernel in kernels.hpp:
+// (solver64m.hpp: Rnn in float64, mixed-precision filter update).  Same per-bin work as update_kernel in kernels.hpp:
 // SCM update (d_classes.py:2048-2267), filter update (d_classes.py:
 // 3320-3387), external filters (d_classes.py:1627-1694), dhat = w^H yhat.
 #pragma once
 #include "kernels.hpp"
-#include "solver64.hpp"
+#include "solver64m.hpp"
 
 namespace danse {
 
 template <int DMAX, int RMAX>
 __global__ void __launch_bounds__(64) update_kernel_big(const UpdateArgs a) {
   using namespace big;
-  __shared__ LDS<DMAX> lds;
+  __shared__ LDSM<DMAX> lds;
   const int li = threadIdx.x;
   const int F = a.F;
   const int f = blockIdx.x % F;
@@ -32,9 +32,9 @@ __global__ void __launch_bounds__(64) update_kernel_big(const UpdateArgs a) {
   const long long matOff = (long long)s * a.scmStride + d.scmOff + (long long)f * D * D;
   const int rowc = act ? li : 0;
 
-  // Ryy row in float32; Rnn row averaged in float64 (then rounded for this
-  // class's float32 solver)
-  Row<DMAX> A, B;
+  // Ryy row in float32; Rnn row in float64
+  Row<DMAX> A;
+  RowD<DMAX> B;
   const bool needY = (opY != 0) || solve;
   const bool needN = (opN != 0) || solve;
   if (needY) {
@@ -61,7 +61,7 @@ __global__ void __launch_bounds__(64) update_kernel_big(const UpdateArgs a) {
     }
   }
   if (needN) {
-    rzero(B);
+    sfor<0, DMAX>([&](auto cc) { wsd<decltype(cc)::value>(B, cd{0.0, 0.0}); });
     const double cy = (opN == DANSE_OP_SET) ? 1.0 / D : (1.0 - beta) / D;
     const double cx = (opN == DANSE_OP_SET) ? 0.0 : beta;
     const cd yl = cdk(y);
@@ -78,7 +78,7 @@ __global__ void __launch_bounds__(64) update_kernel_big(const UpdateArgs a) {
         x.im = fma(cy, yy.im, x.im);
         if (act && c < D) a.Rnn[matOff + (long long)li * D + c] = x;
       }
-      ws<c>(B, cfk(x));
+      wsd<c>(B, x);
     });
   }
 
@@ -93,8 +93,8 @@ __global__ void __launch_bounds__(64) update_kernel_big(const UpdateArgs a) {
     w = act ? wNext[rowc] : cf{0.0f, 0.0f};
   } else if (solve) {
     bool ok = true;
-    if (a.gevd) w = gevd_filter<DMAX, RMAX>(A, B, lds, li, D, a.rank, d.ref, ok);
-    else w = mwf_filter<DMAX>(A, B, lds, li, D, d.ref, ok);
+    if (a.gevd) w = gevd_filter_mixed<DMAX, RMAX>(A, B, lds, li, D, a.rank, d.ref, ok);
+    else w = mwf_filter_mixed<DMAX>(A, rgetd(B, d.ref), lds, li, D, d.ref, ok);
     if (!ok && li == 0) atomicOr(&a.diag[(s * a.K + d.k) * kMaxFam + d.fam], 1);
   } else {
     w = act ? wPrev[rowc] : cf{0.0f, 0.0f};
@@ -104,29 +104,36 @@ __global__ void __launch_bounds__(64) update_kernel_big(const UpdateArgs a) {
 }
 
 template <int DMAX, int RMAX>
-__global__ void __launch_bounds__(64) filter_update_kernel_big(const cf* Ryy, const cd* Rnn, int B, int D, int gevd,
+__global__ void __launch_bounds__(64) filter_update_kernel_big(const cd* Ryy, const cd* Rnn, int B, int D, int gevd,
                                                               int rank, int ref, cf* w, int* diag) {
   using namespace big;
-  __shared__ LDS<DMAX> lds;
+  __shared__ LDSM<DMAX> lds;
   const int li = threadIdx.x;
   const int b = blockIdx.x;
   const bool act = li < D;
   const int row = act ? li : 0;
-  Row<DMAX> A, Bm;
-  rzero(A);
-  rzero(Bm);
+  RowD<DMAX> Y, N;
+  sfor<0, DMAX>([&](auto cc) {
+    wsd<decltype(cc)::value>(Y, cd{0.0, 0.0});
+    wsd<decltype(cc)::value>(N, cd{0.0, 0.0});
+  });
   cols_below<DMAX>(D, [&](auto cc) {
     constexpr int c = decltype(cc)::value;
     const int cl = (c < D) ? c : D - 1;
-    const cf va = Ryy[((long long)b * D + row) * D + cl];
-    const cf vn = cfk(Rnn[((long long)b * D + row) * D + cl]);
-    ws<c>(A, (act && c < D) ? va : cf{0.0f, 0.0f});
-    ws<c>(Bm, (act && c < D) ? vn : cf{0.0f, 0.0f});
+    const cd va = Ryy[((long long)b * D + row) * D + cl];
+    const cd vn = Rnn[((long long)b * D + row) * D + cl];
+    wsd<c>(Y, (act && c < D) ? va : cd{0.0, 0.0});
+    wsd<c>(N, (act && c < D) ? vn : cd{0.0, 0.0});
   });
   bool ok = true;
   cf wv;
-  if (gevd) wv = gevd_filter<DMAX, RMAX>(A, Bm, lds, li, D, rank, ref, ok);
-  else wv = mwf_filter<DMAX>(A, Bm, lds, li, D, ref, ok);
+  if (gevd) {
+    Row<DMAX> A;
+    sfor<0, DMAX>([&](auto cc) { ws<decltype(cc)::value>(A, cfk(rsd<decltype(cc)::value>(Y))); });
+    wv = gevd_filter_mixed<DMAX, RMAX>(A, N, lds, li, D, rank, ref, ok);
+  } else {
+    wv = mwf_filter64<DMAX>(Y, rgetd(N, ref), lds, li, D, ref, ok);
+  }
   if (act) w[(long long)b * D + li] = wv;
   if (diag && li == 0) diag[b] = ok ? 0 : 1;
 }

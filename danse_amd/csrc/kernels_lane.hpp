@@ -207,11 +207,11 @@ __global__ void __launch_bounds__(64) update_kernel_lane(const UpdateArgs a) {
 
 
 // Stand-alone batched filter update (danse_filter_update) on full [B][D][D]
-// SCM pairs (Ryy complex float, Rnn complex double): one batch item per lane,
-// the same two phases (float64 factorisation, float32 eigen work) in one
-// kernel (the operator is not performance critical).
+// complex double SCM pairs: one batch item per lane, the same precision plan
+// (GEVD: Rnn factored in float64, Ryy used in float32; MWF: Ryy factored in
+// float64) in one kernel (the operator is not performance critical).
 template <int D, int RMAX>
-__global__ void __launch_bounds__(64) filter_update_kernel_lane(const cf* Ryy, const cd* Rnn, int Bn, int gevd,
+__global__ void __launch_bounds__(64) filter_update_kernel_lane(const cd* Ryy, const cd* Rnn, int Bn, int gevd,
                                                                int rank, int ref, cf* w, int* diag) {
   using namespace lane;
   int b = blockIdx.x * 64 + threadIdx.x;
@@ -220,7 +220,7 @@ __global__ void __launch_bounds__(64) filter_update_kernel_lane(const cf* Ryy, c
   __shared__ cf Ls[tri_n(D)][64];
   __shared__ cf Gs[D][64];
   const LdsTri<D> Li{Ls, (int)threadIdx.x};
-  auto load = [&](auto* src, auto& X) {
+  auto load = [&](const cd* src, PTriD<D>& X) {
     sfor<0, D>([&](auto ic) {
       constexpr int i = decltype(ic)::value;
       sfor<0, i + 1>([&](auto jc) {
@@ -231,10 +231,10 @@ __global__ void __launch_bounds__(64) filter_update_kernel_lane(const cf* Ryy, c
   };
   cf wv[D];
   bool ok = true;
-  {
-    PTriD<D> N;
-    load(Rnn, N);
-    if (gevd) {
+  if (gevd) {
+    {
+      PTriD<D> N;
+      load(Rnn, N);
       double invd[D];
       ok = chol64<D>(N, invd);
       cf g[D];
@@ -242,31 +242,26 @@ __global__ void __launch_bounds__(64) filter_update_kernel_lane(const cf* Ryy, c
       sfor<0, D>([&](auto ic) { Gs[decltype(ic)::value][threadIdx.x] = g[decltype(ic)::value]; });
       tri_inv64<D>(N, invd);
       store_tri<D>(N, Ls, threadIdx.x);
-    } else {
-      cd ncol[D];
-      sfor<0, D>([&](auto ic) {
-        constexpr int i = decltype(ic)::value;
-        cd c = cd{0.0, 0.0};
-        sfor<0, D>([&](auto kc) {
-          constexpr int k = decltype(kc)::value;
-          if (k == ref) c = hermd<i, k>(N);
-        });
-        ncol[i] = c;
-      });
-      asm volatile("" ::: "memory");
-      PTri<D> A;
-      load(Ryy, A);
-      ok = mwf_filter_mixed<D>(A, ncol, ref, wv);
     }
-  }
-  if (gevd) {
     asm volatile("" ::: "memory");
     PTri<D> A;
-    load(Ryy, A);
+    sfor<0, D>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      sfor<0, i + 1>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        A.a[P(i, j)] = cfk(Ryy[((long long)b * D + i) * D + j]);
+      });
+    });
     cf g[D];
     sfor<0, D>([&](auto ic) { g[decltype(ic)::value] = Gs[decltype(ic)::value][threadIdx.x]; });
     congruence<D>(A, Li);
     gevd_filter_mixed<D, RMAX>(A, Li, g, rank, wv);
+  } else {
+    cd ncol[D];
+    sfor<0, D>([&](auto ic) { ncol[decltype(ic)::value] = Rnn[((long long)b * D + decltype(ic)::value) * D + ref]; });
+    PTriD<D> X;
+    load(Ryy, X);
+    ok = mwf_filter64<D>(X, ncol, ref, wv);
   }
   if (valid) {
     sfor<0, D>([&](auto ic) { w[(long long)b * D + decltype(ic)::value] = wv[decltype(ic)::value]; });

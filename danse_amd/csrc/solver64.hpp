@@ -1,12 +1,9 @@
-// Wavefront solvers for large filter dimensions (16 < D <= 64): one
-// frequency bin per wavefront, lane i holds ROW i of Ryy / Rnn.
-// (update_w / update_w_gevd, danse_toolbox/d_classes.py:3320-3387.)
-//
-// Same algorithm as solver.hpp (Cholesky of Rnn, C = L^-1 Ryy L^-H,
-// Householder tridiagonalisation, Sturm multisection for the top-R
-// eigenvalues, inverse iteration, back-transform), but written for code
-// size: the pivot loops run at RUN time over the actual D (no padding), the
-// column loops are unrolled over DMAX.  A row lives in chunked vector
+// Wavefront building blocks for large filter dimensions (12 < D <= 64): one
+// frequency bin per wavefront, lane i holds ROW i.  (The filter update that
+// uses them is solver64m.hpp.)  Householder tridiagonalisation, Sturm
+// multisection for the top-R eigenvalues, inverse iteration, written for
+// code size: the pivot loops run at RUN time over the actual D (no padding),
+// the column loops are unrolled over DMAX.  A row lives in chunked vector
 // registers (Row<DMAX>, processed in chunks of 8 columns) so that the
 // pivot column j -- a wave-uniform runtime index -- is read through a tree
 // of uniform branches (no scratch) and written back through LDS.  Row
@@ -86,104 +83,11 @@ DANSE_DEV void cols_below(int D, Fn&& fn) {
   });
 }
 
-// Cholesky B = L L^H on the first D rows/cols; on exit B[li][c] = L[li][c]
-// (0 above the diagonal), invd = 1 / L[li][li].
-template <int DMAX>
-DANSE_DEV bool chol(Row<DMAX>& B, cf (*U)[DMAX + 1], int li, int D, float& invd) {
-  bool ok = true;
-  invd = 0.0f;
-  for (int j = 0; j < D; ++j) {
-    cf bj = rget(B, j);
-    const float p0 = rl(bj.re, j);
-    ok = ok && (p0 > 1e-37f);
-    const float piv = fmaxf(p0, 1e-37f);
-    const float inv = frsq(piv);
-    if (li == j) {
-      bj = cf{piv * inv, 0.0f};
-      invd = inv;
-    } else if (li > j) {
-      bj = inv * bj;
-    }
-    if (li < DMAX) U[j][li] = (li >= j) ? bj : cf{0.0f, 0.0f};   // column j of L
-    cols_after<DMAX>(j, [&](auto cc) {
-      constexpr int c = decltype(cc)::value;
-      cf lcj = rl(bj, c);
-      if (!(c > j)) lcj = cf{0.0f, 0.0f};
-      cf x = rs<c>(B);
-      fms_cc(x, bj, lcj);
-      ws<c>(B, x);
-    });
-  }
-  __syncthreads();
-  sfor<0, DMAX>([&](auto cc) {
-    constexpr int c = decltype(cc)::value;
-    ws<c>(B, (c < D && li < DMAX) ? U[c][li] : cf{0.0f, 0.0f});
-  });
-  __syncthreads();
-  return ok;
-}
-
-DANSE_DEV cf elim(cf lij, float ij, int li, int j) {
-  return (li == j) ? cf{1.0f - ij, 0.0f} : ij * lij;
-}
-
-// X <- L^{-1} X  (L rows in registers)
-template <int DMAX>
-DANSE_DEV void fwd_rows(Row<DMAX>& X, const Row<DMAX>& L, float invd, int li, int D) {
-  for (int j = 0; j < D; ++j) {
-    const cf lm = elim(rget(L, j), rl(invd, j), li, j);
-    cols_below<DMAX>(D, [&](auto cc) {
-      constexpr int c = decltype(cc)::value;
-      const cf xjc = rl(rs<c>(X), j);
-      cf x = rs<c>(X);
-      fms_c(x, lm, xjc);
-      ws<c>(X, x);
-    });
-  }
-}
-
-template <int DMAX>
-DANSE_DEV cf fwd_vec(cf x, const Row<DMAX>& L, float invd, int li, int D) {
-  for (int j = 0; j < D; ++j) {
-    const cf lm = elim(rget(L, j), rl(invd, j), li, j);
-    fms_c(x, lm, rl(x, j));
-  }
-  return x;
-}
-
-// v <- L^{-H} v given Lt[c] = conj(L[c][li]) on lane li
-template <int DMAX>
-DANSE_DEV cf bwd_vec_h(cf v, const Row<DMAX>& Lt, float invd, int li, int D) {
-  for (int j = D - 1; j >= 0; --j) {
-    const cf lm = elim(rget(Lt, j), rl(invd, j), li, j);
-    fms_c(v, lm, rl(v, j));
-  }
-  return v;
-}
-
 template <int DMAX>
 struct LDS {
   cf U[DMAX][DMAX + 1];   // transpose tile, then Householder vectors U[j][i]
   float x[kRMax][DMAX];   // tridiagonal eigenvectors (Gram-Schmidt)
 };
-
-template <int DMAX>
-DANSE_DEV void herm_transpose(Row<DMAX>& X, cf (*U)[DMAX + 1], int li) {
-  if (li < DMAX) {
-    sfor<0, DMAX>([&](auto cc) {
-      constexpr int c = decltype(cc)::value;
-      U[li][c] = rs<c>(X);
-    });
-  }
-  __syncthreads();
-  if (li < DMAX) {
-    sfor<0, DMAX>([&](auto cc) {
-      constexpr int c = decltype(cc)::value;
-      ws<c>(X, conjg(U[c][li]));
-    });
-  }
-  __syncthreads();
-}
 
 // Householder tridiagonalisation of the Hermitian A (first D rows/cols).
 // u_j -> U[j][i]; returns a = T[li][li], b = T[li][li-1].
@@ -349,75 +253,6 @@ DANSE_DEV float tri_eigvec(float ta, float te, int li, int D, float lam, float p
     x = sol * frsq(nrm);
   }
   return x;
-}
-
-template <int DMAX, int RMAX>
-DANSE_DEV cf gevd_filter(Row<DMAX>& A, Row<DMAX>& B, LDS<DMAX>& S, int li, int D, int R, int ref, bool& ok) {
-  const bool act = li < D;
-  float invd;
-  ok = chol<DMAX>(B, S.U, li, D, invd);
-  fwd_rows<DMAX>(A, B, invd, li, D);     // A = L^{-1} Ryy
-  herm_transpose<DMAX>(A, S.U, li);      // A = Ryy L^{-H}
-  fwd_rows<DMAX>(A, B, invd, li, D);     // C
-  herm_transpose<DMAX>(B, S.U, li);      // B[c] = conj(L[c][li])
-  float ta;
-  cf tb;
-  tridiag<DMAX>(A, S.U, li, D, ta, tb);
-  // lane-distributed tridiagonal: e2 on lane i = |T[i+1][i]|^2 = |tb of lane i+1|^2
-  const float e2own = abs2(tb);
-  float te2 = __shfl_down(e2own, 1);
-  if (li + 1 >= D) te2 = 0.0f;
-  const float ta_ = act ? ta : 0.0f;
-  float lam[kRMax];
-  float tnorm;
-  top_eigvals<RMAX>(ta_, te2, li, D, R, lam, tnorm);
-  const float pert = 1.2e-7f * fmaxf(tnorm, 1e-30f);
-  const float te = fsqrt(te2);
-  const cf g = rget(B, ref);   // conj(L[ref][li])
-  cf w = cf{0.0f, 0.0f};
-  sfor<0, RMAX>([&](auto rc) {
-    constexpr int r = decltype(rc)::value;
-    if (r >= R) return;
-    const float x = tri_eigvec<DMAX>(ta_, te, li, D, lam[r], pert, r, S.x);
-    // phase fix: v_i = phi_i x_i, phi_{i+1} = phi_i * b_{i+1} / |b_{i+1}|
-    cf phi = cf{1.0f, 0.0f};
-    cf v = cf{0.0f, 0.0f};
-    for (int i = 0; i < D; ++i) {
-      if (li == i) v = x * phi;
-      if (i + 1 < D) {
-        const cf bb = rl(tb, i + 1);
-        const float ab2 = abs2(bb);
-        const float iab = frsq(ab2);
-        if (ab2 > 0.0f) phi = phi * cf{bb.re * iab, bb.im * iab};
-      }
-    }
-    if (r + 1 < R) {
-      if (li < DMAX) S.x[r][li] = x;
-      __syncthreads();
-    }
-    for (int j = D - 3; j >= 0; --j) {
-      const cf u = (li < DMAX) ? S.U[j][li] : cf{0.0f, 0.0f};
-      const cf s = gsum<64>(cmul(u, v));
-      fms_c(v, 2.0f * u, s);
-    }
-    const cf sr = gsum<64>(cmul(v, g));
-    const cf u = bwd_vec_h<DMAX>(v, B, invd, li, D);
-    const float coef = 1.0f - frcp(lam[r]);
-    w = w + coef * (u * sr);
-  });
-  return act ? w : cf{0.0f, 0.0f};
-}
-
-template <int DMAX>
-DANSE_DEV cf mwf_filter(Row<DMAX>& A, const Row<DMAX>& B, LDS<DMAX>& S, int li, int D, int ref, bool& ok) {
-  const bool act = li < D;
-  const cf r = rget(A, ref) - rget(B, ref);   // (Ryy - Rnn)[li][ref], as the reference forms it
-  float invd;
-  ok = chol<DMAX>(A, S.U, li, D, invd);
-  const cf t = fwd_vec<DMAX>(r, A, invd, li, D);
-  herm_transpose<DMAX>(A, S.U, li);
-  const cf w = bwd_vec_h<DMAX>(t, A, invd, li, D);
-  return act ? w : cf{0.0f, 0.0f};
 }
 
 }  // namespace big

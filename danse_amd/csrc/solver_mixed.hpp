@@ -191,11 +191,9 @@ DANSE_DEV void gevd_filter_mixed(PTri<D>& A, const LM& Li, const cf (&g)[D], int
   });
 }
 
-// MWF filter in float64: A = Ryy (float32), ncol = Rnn[:, ref] (float64).
+// MWF filter in float64: X = Ryy (float64, destroyed), ncol = Rnn[:, ref].
 template <int D>
-DANSE_DEV bool mwf_filter_mixed(const PTri<D>& A, const cd (&ncol)[D], int ref, cf (&wv)[D]) {
-  PTriD<D> X;
-  sfor<0, tri_n(D)>([&](auto ec) { X.a[decltype(ec)::value] = cdk(A.a[decltype(ec)::value]); });
+DANSE_DEV bool mwf_filter64(PTriD<D>& X, const cd (&ncol)[D], int ref, cf (&wv)[D]) {
   cd r[D];
   sfor<0, D>([&](auto ic) {
     constexpr int i = decltype(ic)::value;
@@ -227,6 +225,13 @@ DANSE_DEV bool mwf_filter_mixed(const PTri<D>& A, const cd (&ncol)[D], int ref, 
   });
   sfor<0, D>([&](auto ic) { wv[decltype(ic)::value] = cfk(r[decltype(ic)::value]); });
   return ok;
+}
+// ... with the float32 Ryy of the online engine (promoted)
+template <int D>
+DANSE_DEV bool mwf_filter_mixed(const PTri<D>& A, const cd (&ncol)[D], int ref, cf (&wv)[D]) {
+  PTriD<D> X;
+  sfor<0, tri_n(D)>([&](auto ec) { X.a[decltype(ec)::value] = cdk(A.a[decltype(ec)::value]); });
+  return mwf_filter64<D>(X, ncol, ref, wv);
 }
 
 }  // namespace lane

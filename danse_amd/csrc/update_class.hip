@@ -5,7 +5,7 @@
 #include "kernels_lane.hpp"
 
 #ifndef DANSE_DMAX
-#error "compile with -DDANSE_DMAX=<1..16, 24..64 step 8>"
+#error "compile with -DDANSE_DMAX=<1..12, 16..64 step 8>"
 #endif
 
 namespace danse {
@@ -31,16 +31,10 @@ void DANSE_CAT(launch_update_d, DANSE_DMAX)(const UpdateArgs& a, hipStream_t st)
     const unsigned grid = (unsigned)(a.S * a.nFN * a.F);
     if (r1) hipLaunchKernelGGL((update_kernel_big<kD, 1>), dim3(grid), dim3(64), 0, st, a);
     else hipLaunchKernelGGL((update_kernel_big<kD, kRMax>), dim3(grid), dim3(64), 0, st, a);
-  } else {
-    constexpr int kNB = 64 / kG;
-    const int nBB = (a.F + kNB - 1) / kNB;
-    const unsigned grid = (unsigned)(a.S * a.nFN * nBB);
-    if (r1) hipLaunchKernelGGL((update_kernel<kG, kD, 1>), dim3(grid), dim3(64), 0, st, a);
-    else hipLaunchKernelGGL((update_kernel<kG, kD, kRMax>), dim3(grid), dim3(64), 0, st, a);
   }
 }
 
-void DANSE_CAT(launch_filter_update_d, DANSE_DMAX)(const cf* Ryy, const cd* Rnn, int B, int D, int gevd, int rank,
+void DANSE_CAT(launch_filter_update_d, DANSE_DMAX)(const cd* Ryy, const cd* Rnn, int B, int D, int gevd, int rank,
                                                    int ref, cf* w, int* diag, hipStream_t st) {
   const bool r1 = !gevd || rank == 1;
   if constexpr (kG == 1) {
@@ -58,15 +52,6 @@ void DANSE_CAT(launch_filter_update_d, DANSE_DMAX)(const cf* Ryy, const cd* Rnn,
                          ref, w, diag);
     else
       hipLaunchKernelGGL((filter_update_kernel_big<kD, kRMax>), dim3(grid), dim3(64), 0, st, Ryy, Rnn, B, D, gevd,
-                         rank, ref, w, diag);
-  } else {
-    constexpr int kNB = 64 / kG;
-    const unsigned grid = (unsigned)((B + kNB - 1) / kNB);
-    if (r1)
-      hipLaunchKernelGGL((filter_update_kernel<kG, kD, 1>), dim3(grid), dim3(64), 0, st, Ryy, Rnn, B, D, gevd, rank,
-                         ref, w, diag);
-    else
-      hipLaunchKernelGGL((filter_update_kernel<kG, kD, kRMax>), dim3(grid), dim3(64), 0, st, Ryy, Rnn, B, D, gevd,
                          rank, ref, w, diag);
   }
 }

@@ -204,11 +204,11 @@ int danse_wola_analysis(const float* x, int32_t C, int32_t T, const int32_t* end
                         const float* win, int32_t N, int32_t Ns, float* out, void* stream);
 
 /* Batched filter update on full SCM pairs (update_w / update_w_gevd,
- * d_classes.py:3320-3387): Ryy: [B][D][D] complex float, Rnn: [B][D][D]
- * complex double (device; the noise SCM conditions the update and is
- * factored in double), w: [B][D] complex float.
+ * d_classes.py:3320-3387): Ryy, Rnn: [B][D][D] complex double (device), w:
+ * [B][D] complex float.  The SCM the update factors (Rnn for GEVD, Ryy for
+ * MWF) is used in double, the other one in float (DESIGN.md "Precision").
  * gevd != 0 -> rank-`rank` GEVD, else MWF. diag: [B] int32 or NULL. */
-int danse_filter_update(const float* Ryy, const double* Rnn, int32_t B, int32_t D, int32_t gevd,
+int danse_filter_update(const double* Ryy, const double* Rnn, int32_t B, int32_t D, int32_t gevd,
                         int32_t rank, int32_t ref, float* w, int32_t* diag, void* stream);
 
 /* Batch-mode SCM contraction (update_covmats_batch, d_classes.py:3272-3304):

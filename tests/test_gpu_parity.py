@@ -67,7 +67,7 @@ def test_filter_update_kat(case, golden_dir):
     g = np.load(golden_dir / f"{case['name']}.npz")
     Ryy, Rnn = kat_inputs(case)
     F, D = case['F'], case['D']
-    a = _dev_cf(Ryy)
+    a = torch.from_numpy(np.ascontiguousarray(np.asarray(Ryy, dtype=np.complex128)).view(np.float64)).cuda()
     n = torch.from_numpy(np.ascontiguousarray(np.asarray(Rnn, dtype=np.complex128)).view(np.float64)).cuda()
     w = torch.empty((F, D, 2), dtype=torch.float32, device='cuda')
     diag = torch.zeros(F, dtype=torch.int32, device='cuda')
@@ -78,13 +78,14 @@ def test_filter_update_kat(case, golden_dir):
     wg = w.cpu().numpy().view(np.complex64)[..., 0].astype(np.complex128)
     e = _bin_rel(wg, g['w'])
     st = _stats(e)
-    # fp32 floor of the same problem: LAPACK in single precision (Cholesky
-    # solve for MWF, generalized eigensolver for GEVD) vs the float64
-    # reference; the kernel must stay within 2x of it (median)
+    # for scale: LAPACK in single precision (Cholesky solve for MWF,
+    # generalized eigensolver for GEVD) on the same inputs; the device's
+    # mixed-precision update (float64 factorisation of Rnn) beats it and is
+    # held to the north-star tolerance itself
     st32 = _stats(_bin_rel(_lapack_fp32_filters(Ryy, Rnn, case), g['w']))
     print(case['name'], st, 'lapack-fp32', st32)
     assert int(diag.sum()) == 0
-    assert st['median'] <= max(1e-5, 2 * st32['median']) and st['p99'] <= max(1e-3, 2 * st32['p99']), (st, st32)
+    assert st['median'] <= 1e-5 and st['p99'] <= 1e-4, (st, st32)
 
 
 def test_wola_analysis_matches_numpy():
@@ -154,13 +155,10 @@ def test_online_engine_vs_oracle(case, golden_dir):
     assert dg <= 1e-4, dg
 
 
-# Filter dimensions above 16 (64-lane solver class, solver64.hpp): config C
+# Filter dimensions above 16 (64-lane solver class, solver64m.hpp): config C
 # shape (K=16 x 4, D=19) and two ragged cases, compared with the float64
-# oracle (the reference fixtures pin the oracle at smaller D).  Tolerance for
-# this class: the fp32 SCM recursion and solve are condition-limited on the
-# first post-gate frames (SCMs averaged over ~D frames, cond(Rnn) up to
-# 1e5), so filters are held to median <= 1e-4 / p99 <= 1e-3 and the
-# time-domain estimate -- what the metrics see -- to rel. err <= 1e-4.
+# oracle (the reference fixtures pin the oracle at smaller D); the same
+# tolerance as every other class.
 BIG_CASES = [
     dict(name='online_C_shape_K16_D19_asy', M=[4] * 16, dur=4.0, seed=21,
          danse=dict(ONLINE_CASES[1]['danse'], nodeUpdating='asy')),
@@ -184,7 +182,7 @@ def test_online_engine_large_D(case):
     assert np.array_equal(dv.nInternalFilterUps, ov.nInternalFilterUps)
     assert int(np.sum(dv.diag)) == 0
     st, de = _compare_online(case, dv, ov)
-    assert st['median'] <= 1e-4 and st['p99'] <= 1e-3, st
+    assert st['median'] <= 1e-5 and st['p99'] <= 1e-4, st
     assert de <= 1e-4
 
 
