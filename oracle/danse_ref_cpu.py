@@ -336,30 +336,31 @@ class OnlineDANSE:
             if not p.covMatSameInitForAllNodes:
                 dims = (self.Mtot, self.Mtot) if p.covMatSameInitForAllFreqs else (F, self.Mtot, self.Mtot)
                 fullSlice = init_covmats(dims, rng, *args)
+            # (the reference always allocates every family's SCMs and filter
+            # histories, d_classes.py:619-620 -- at K = 32 x 8 the centralised
+            # ones alone are ~34 GB; the restatement builds only the enabled
+            # families, which leaves every computed value unchanged)
             if p.covMatSameInitForAllFreqs:
                 def tile(s):
                     return np.tile(s, (F, 1, 1))
-                sl = fullSlice[:D, :D]
-                Rt = (tile(sl), tile(sl))
-                Rc = (tile(fullSlice), tile(fullSlice))
-                Rs = (tile(sl), tile(sl))
-                ll = fullSlice[:self.M[k], :self.M[k]]
-                Rl = (tile(ll), tile(ll))
             else:
-                sl = fullSlice[:, :D, :D]
-                Rt = (sl, sl)
-                Rc = (fullSlice, fullSlice)
-                Rs = (sl, sl)
-                ll = fullSlice[:, :self.M[k], :self.M[k]]
-                Rl = (ll, ll)
-            # reference order: Rnn, Ryy appended -> (Ryy, Rnn) same slice objects
-            self.danse.append(_SCMSet(Rt[0], Rt[1], init_complex_filter((F, nh, D), p.referenceSensor, **fi)))
-            self.ssbc.append(_SCMSet(Rs[0], Rs[1], init_complex_filter((F, nh, D), p.referenceSensor, **fi)))
+                def tile(s):
+                    return s
+            ax = (slice(None),) if not p.covMatSameInitForAllFreqs else ()
+
+            def fam(dim, on, ref=p.referenceSensor):
+                if not on:
+                    return _SCMSet(None, None, None)
+                sl = fullSlice[ax + (slice(0, dim), slice(0, dim))]
+                return _SCMSet(tile(sl), tile(sl), init_complex_filter((F, nh, dim), ref, **fi))
+
+            refC = int(np.sum(self.M[:k]) + p.referenceSensor)
+            self.danse.append(fam(D, True))
+            self.ssbc.append(fam(D, p.computeSingleSensorBroadcast))
             self.wExt.append(init_complex_filter((F, nh, self.M[k]), p.referenceSensor, **fi))
             self.wExtTarget.append(init_complex_filter((F, self.M[k]), p.referenceSensor, **fi))
-            refC = int(np.sum(self.M[:k]) + p.referenceSensor)
-            self.centr.append(_SCMSet(Rc[0], Rc[1], init_complex_filter((F, nh, self.Mtot), refC, **fi)))
-            self.local.append(_SCMSet(Rl[0], Rl[1], init_complex_filter((F, nh, self.M[k]), p.referenceSensor, **fi)))
+            self.centr.append(fam(self.Mtot, p.computeCentralised, refC))
+            self.local.append(fam(self.M[k], p.computeLocal))
         self.i = np.zeros(K, dtype=int)
         self.numUpdatesRyy = np.zeros(K, dtype=int)
         self.numUpdatesRnn = np.zeros(K, dtype=int)
@@ -709,11 +710,19 @@ class OnlineDANSE:
     def _scm_update(self, k, s: _SCMSet, y, vad):
         beta = self.beta[k]
         yyH = 1 / y.shape[1] * np.einsum('ij,ik->ijk', y, y.conj())
+        # beta * R + (1 - beta) * yyH, elementwise in the same order as the
+        # reference (bit-identical), without the extra temporaries
+        yyH_w = (1 - beta) * yyH
+
+        def avg(R):
+            out = beta * R
+            out += yyH_w
+            return out
         RyyCurr, RnnCurr = s.Ryy, s.Rnn
         if vad:
-            RyyCurr = beta * s.Ryy + (1 - beta) * yyH
+            RyyCurr = avg(s.Ryy)
         else:
-            RnnCurr = beta * s.Rnn + (1 - beta) * yyH
+            RnnCurr = avg(s.Rnn)
         if self.p.use1stFrameAsBasis:
             if self.numUpdatesRyy[k] == 1 and vad:
                 s.Ryy = yyH

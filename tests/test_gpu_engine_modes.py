@@ -118,3 +118,40 @@ def test_sharded_engines_match_unsharded(name):
             if hasattr(ref, 'dLocal'):
                 assert np.array_equal(o.dLocal[:, k], ref.dLocal[:, k]), (name, k)
         e.close()
+
+
+def test_headline_shape_K32x8_D39_vs_oracle():
+    """The north-star headline shape: online K = 32 nodes x 8 mics (D = 39,
+    the wavefront class), asy, one WASN.  The float64 oracle is bounded to
+    the first rounds after every node passed the gate (its per-bin eigh at
+    D = 39 costs ~7 s per round); the device runs the whole signal and is
+    compared on the oracle's rounds."""
+    from danse_amd.core import danse_multi
+    from oracle import danse_ref_cpu as O
+    # (the wet-speech VAD leaves ~1 non-VAD frame in 3: the D = 39 gate opens near round 150)
+    case = dict(name='online_N2_K32x8_asy', M=[8] * 32, dur=5.2, seed=41, danse=dict(BATTERY, nodeUpdating='asy'))
+    sc, dp, wp = _scene_params(case)
+    K, D = 32, 39
+    starts = []
+    for nd in sc.wasn:
+        v = nd.vadPerFrame
+        ny = np.cumsum(v)
+        nn = np.arange(1, len(v) + 1) - ny
+        starts.append(int(np.argmax((ny > D) & (nn > D))))
+    R0 = max(starts) + 2          # the oracle runs rounds [0, R0): two solve rounds of all 32 nodes
+    dv = danse_multi([sc], dp)[0]
+    ov = O.OnlineDANSE(sc, dp, vadMinProp=wp.vadMinProportionActive, maxRounds=R0).run()
+    assert np.array_equal(dv.startRound, ov.startRound)
+    assert int(np.sum(dv.diag)) == 0
+    errs = []
+    for k in range(K):
+        s0 = int(ov.startRound[k])
+        assert s0 + 1 < R0
+        errs.append(_bin_rel(dv.wTilde[k][:, s0 + 1:R0 + 1], ov.wTilde[k][:, s0 + 1:R0 + 1]).ravel())
+    st = _stats(np.concatenate(errs))
+    # d over the samples the oracle's rounds produced (update frames end at upEnd)
+    T1 = (R0 + 1) * dp.Ns - (dp.DFTsize - dp.Ns)
+    de = rel_err(dv.d[:T1], ov.d[:T1])
+    print(case['name'], 'rounds', R0, 'w', st, 'd', de)
+    assert st['median'] <= 1e-5 and st['p99'] <= 1e-4, st
+    assert de <= 1e-4
