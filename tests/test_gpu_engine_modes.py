@@ -149,8 +149,10 @@ def test_headline_shape_K32x8_D39_vs_oracle():
         assert s0 + 1 < R0
         errs.append(_bin_rel(dv.wTilde[k][:, s0 + 1:R0 + 1], ov.wTilde[k][:, s0 + 1:R0 + 1]).ravel())
     st = _stats(np.concatenate(errs))
-    # d over the samples the oracle's rounds produced (update frames end at upEnd)
-    T1 = (R0 + 1) * dp.Ns - (dp.DFTsize - dp.Ns)
+    # d over the samples the oracle's rounds completed: the last round's chunk
+    # [idxEnd - N, idxEnd) is overlap-added only up to idxEnd - (N - Ns)
+    T1 = int(ov.idxEnd) - (dp.DFTsize - dp.Ns)
+    assert T1 > R0 * dp.Ns // 2
     de = rel_err(dv.d[:T1], ov.d[:T1])
     print(case['name'], 'rounds', R0, 'w', st, 'd', de)
     assert st['median'] <= 1e-5 and st['p99'] <= 1e-4, st
