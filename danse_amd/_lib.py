@@ -84,6 +84,8 @@ SIGNATURES = {
                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     'danse_batch_covmats': (_c_i32, [ctypes.c_void_p, _c_i32, _c_i32, _c_i32, ctypes.c_void_p, ctypes.c_void_p,
                                      ctypes.c_void_p, ctypes.c_void_p]),
+    'danse_stft': (_c_i32, [ctypes.c_void_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _c_i32, ctypes.c_void_p,
+                            ctypes.c_void_p, ctypes.c_void_p]),
     'danse_batch_create': (_c_i32, [ctypes.POINTER(DanseBatchCfg), _c_i32, ctypes.POINTER(ctypes.c_void_p)]),
     'danse_batch_destroy': (None, [ctypes.c_void_p]),
     'danse_batch_last_error': (ctypes.c_char_p, [ctypes.c_void_p]),

@@ -15,13 +15,9 @@ import numpy as np
 
 from . import _lib as L
 from .engine import beta_from_t50p, init_complex_filter, _cf32, _ptr
+from .outputs import stft_frames  # noqa: F401  (re-exported)
 
 
-def stft_frames(T: int, N: int, Ns: int) -> int:
-    """Frames of ``scipy.signal.stft(..., boundary=None, padded=True)``: the
-    signal is zero-padded at the end to a whole number of hops."""
-    nadd = (-(T - N) % Ns) % N
-    return (T + nadd - N) // Ns + 1
 
 
 class BatchEngine:

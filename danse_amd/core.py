@@ -14,6 +14,7 @@ import time
 import numpy as np
 
 from .engine import DanseEngine, beta_from_t50p
+from .outputs import DANSEoutputs
 from .params import PreComputedFilters
 
 
@@ -77,9 +78,13 @@ def danse_batch(wasnObj, p, device=0):
     return out, wasnObj
 
 
-def generate_signals_for_snr_computation(pD, dv, wasnObj, danse_function=danse):
+def generate_signals_for_snr_computation(pD, dv, wasnObj, danse_function=danse, bestPerfRef=False, wCentrBatch=None):
     """``d_core.generate_signals_for_snr_computation`` (``d_core.py:550-599``):
-    noise-only and speech-only replays with the recorded filters."""
+    noise-only and speech-only replays with the recorded filters.  The
+    best-performance reference (``get_best_perf``: centralised batch estimates
+    without SROs) is not on the device path."""
+    if bestPerfRef:
+        raise NotImplementedError('bestPerfReference (d_core.get_best_perf) is not on the device path')
     pU = copy.deepcopy(pD)
     pU.preGivenFilters = PreComputedFilters(
         active=True, internalFilters=dv.wTilde, externalFilters=dv.wTildeExt,
@@ -95,3 +100,23 @@ def generate_signals_for_snr_computation(pD, dv, wasnObj, danse_function=danse):
         out[f'{key}_l'] = getattr(src, 'dLocal', None)
         out[f'{key}_ssbc'] = getattr(src, 'dSSBC', None)
     return out
+
+
+def format_output(p, dv, wasnObj, sigsSnr=None):
+    """``d_core.format_output`` (``d_core.py:105-127``): the reference's
+    ``DANSEoutputs`` from ``dv`` (and the SNR replay signals), and the
+    enhanced signals written back into the WASN nodes."""
+    out = DANSEoutputs()
+    out.import_params(p)
+    out.from_variables(dv)
+    if sigsSnr is not None:
+        out.from_snr_signals(sigsSnr)
+    for k in range(len(wasnObj.wasn)):
+        wasnObj.wasn[k].enhancedData = dv.d[:, k]
+        if dv.computeCentralised:
+            wasnObj.wasn[k].enhancedData_c = dv.dCentr[:, k]
+        if dv.computeLocal:
+            wasnObj.wasn[k].enhancedData_l = dv.dLocal[:, k]
+        if dv.computeSingleSensorBroadcast:
+            wasnObj.wasn[k].enhancedData_ssbc = dv.dSSBC[:, k]
+    return out, wasnObj

@@ -683,6 +683,39 @@ int danse_batch_run(danse_batch* eng, void* stream) {
   return 0;
 }
 
+// Whole-signal STFT operator (the reference's yinSTFT / yCentrBatch,
+// d_classes.py:915-930): the batch engine's STFT kernel on caller buffers.
+int danse_stft(const float* y, int32_t S, int32_t C, int32_t T, int32_t N, int32_t Ns, int32_t nseg,
+               const float* win, float* out, void* stream) {
+  danse_batch* eng = nullptr;
+  if (!y || !win || !out) return bfail(nullptr, "null argument");
+  if (N != 1024) return bfail(nullptr, "only N = 1024 is supported");
+  if (S < 1 || C < 1 || T < 1 || Ns < 1 || nseg < 1) return bfail(nullptr, "bad sizes");
+  static cf* tw = nullptr;
+  if (!tw) {
+    std::vector<cf> h;
+    for (int k1 = 0; k1 < 16; ++k1)
+      for (int l = 0; l < 64; ++l) {
+        const double ang = -2.0 * M_PI * (double)(l * k1) / 1024.0;
+        h.push_back(cf{(float)std::cos(ang), (float)std::sin(ang)});
+      }
+    for (int a4 = 0; a4 < 4; ++a4)
+      for (int cc = 0; cc < 16; ++cc) {
+        const double ang = -2.0 * M_PI * (double)(a4 * cc) / 64.0;
+        h.push_back(cf{(float)std::cos(ang), (float)std::sin(ang)});
+      }
+    cf* d = nullptr;
+    BCHK(balloc(&d, wfft::kTwElems));
+    BCHK(hipMemcpy(d, h.data(), h.size() * sizeof(cf), hipMemcpyHostToDevice));
+    tw = d;
+  }
+  const long long jobs = (long long)S * C * nseg;
+  hipLaunchKernelGGL(batch_stft_kernel, dim3((unsigned)((jobs + 3) / 4)), dim3(256), 0, (hipStream_t)stream, y, S, C,
+                     T, Ns, nseg, win, tw, (cf*)out);
+  BCHK(hipGetLastError());
+  return 0;
+}
+
 int danse_batch_output_bytes(danse_batch* eng, int32_t which, int32_t node, size_t* bytes) {
   if (!eng || !bytes) return bfail(eng, "null argument");
   const int S = eng->S, K = eng->K, F = eng->F, H = eng->iters + 1;

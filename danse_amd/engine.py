@@ -22,12 +22,14 @@ Control-byte derivation restates, per round i and node k:
 from __future__ import annotations
 
 import ctypes
+import warnings
 from dataclasses import dataclass
 
 import numpy as np
 
 from . import _lib as L
 from .scheduler import initialize_events, compile_rounds, compile_rounds_fs
+from .outputs import host_fields, stft_frames
 
 
 def beta_from_t50p(t50p, fs, Ns):
@@ -461,8 +463,38 @@ class DanseEngine:
                     full[:, :R + 1, :] = np.transpose(e[s], (1, 0, 2))
                 res[s].wTildeExt[k] = full
         diag = self.diagnostics()
+        if getattr(p, 'saveConditionNumber', False):
+            warnings.warn('saveConditionNumber: condition-number histories are not computed (dv.condNumbers = None)')
+        # yinSTFT / yCentrBatch (d_classes.py:915-930): the whole-signal STFT of
+        # the engine's inputs on the device, [S][F][nseg][Mtot]
+        nseg = stft_frames(self.T, self.N, self.Ns)
+        win = self.torch.from_numpy(np.asarray(p.winWOLAanalysis, dtype=np.float32)).to(self.y.device)
+        Y = self.torch.empty((S, F, nseg, self.Mtot, 2), dtype=self.torch.float32, device=self.y.device)
+        L.check_batch(self.lib.danse_stft(ctypes.c_void_p(self.y.data_ptr()), S, self.Mtot, self.T, self.N, self.Ns, nseg,
+                                    ctypes.c_void_p(win.data_ptr()), ctypes.c_void_p(Y.data_ptr()),
+                                    self.stream_ptr()))
+        self.torch.cuda.synchronize(self.y.device)
+        Yh = Y.cpu().numpy()
+        Yh = Yh[..., 0].astype(np.float64) + 1j * Yh[..., 1].astype(np.float64)
+        solveFlags = (self.flags[:, :, L.FAM_DANSE, :] & L.FLAG_SOLVE) != 0     # [R][S][K]
+        neighbors0 = [list(n.neighborsIdx) for n in self.scenes[0].wasn]
         for s in range(S):
             r = res[s]
+            kr = p.referenceSensor
+            fsr = -1
+            if kr < K and solveFlags[:, s, kr].any():
+                fsr = int(np.argmax(solveFlags[:, s, kr]))
+            for nm, v in host_fields(p, [n.sro for n in self.scenes[s].wasn], neighbors0, self.rt, nI, nseg,
+                                     fsr).items():
+                setattr(r, nm, v)
+            r.yCentrBatch = Yh[s]
+            r.yinSTFT = [Yh[s][:, :, self.base[k]:self.base[k] + self.M[k]] for k in range(K)]
+            r.computeCentralised = bool(p.computeCentralised)
+            r.computeLocal = bool(p.computeLocal)
+            r.computeSingleSensorBroadcast = bool(p.computeSingleSensorBroadcast)
+            # per-bin cond(Ryy) histories (d_classes.py:2127-2200, a debugging
+            # plot) are not computed on the device path
+            r.condNumbers = None
             r.startUpdates = self.startRound[s, 0] >= 0
             r.startRound = self.startRound[s, 0].copy()
             r.nInternalFilterUps = self.nSolves[s, 0].astype(np.float64)

@@ -1,0 +1,186 @@
+"""The ``dv`` output fields the reference's post-processing reads, and its
+output container.
+
+* ``host_fields``: the bookkeeping fields of ``DANSEvariables`` that follow
+  from the schedule alone (SRO estimates / residuals with Oracle SROs, buffer
+  flag iterations, the first-update instant, the never-filled online MSE
+  cost arrays), restating ``d_classes.py:810-846,959-964,1271-1274,
+  1955-1970,2364-2489,2562-2600``;
+* ``DANSEoutputs``: ``d_post.DANSEoutputs.from_variables`` /
+  ``from_snr_signals`` (``d_post.py:38-150``) field mapping.
+
+Every array here is small host bookkeeping; the signal-sized fields (``d``,
+``dhat``, filters, ``zFullTD``, ``yinSTFT``) come from the device
+(``engine.DanseEngine.outputs``).
+"""
+from __future__ import annotations
+
+import warnings
+
+import numpy as np
+
+# every attribute DANSEoutputs.from_variables (d_post.py:41-133) and
+# d_core.format_output (d_core.py:105-127) read from an online ``dv``
+ONLINE_DV_FIELDS = (
+    'yin', 'd', 'dhat', 'zFullTD', 'SROsppm', 'SROsEstimates', 'SROsResiduals', 'flagIterations',
+    'firstDANSEupdateRefSensor', 'wTilde', 'wTildeExt', 'yinSTFT', 'yCentrBatch', 'neighbors', 'fs',
+    'cleanSpeechSignalsAtNodes', 'mseCostOnline', 'expAvgBeta', 'oVADframes',
+    'computeCentralised', 'computeLocal', 'computeSingleSensorBroadcast',
+)
+# ... when the corresponding family is computed
+FAMILY_DV_FIELDS = {
+    'computeCentralised': ('dCentr', 'dHatCentr', 'wCentr', 'mseCostOnline_c'),
+    'computeLocal': ('dLocal', 'dHatLocal', 'wLocal', 'mseCostOnline_l'),
+    'computeSingleSensorBroadcast': ('dSSBC', 'dHatSSBC'),
+}
+
+
+def stft_frames(T: int, N: int, Ns: int) -> int:
+    """Frames of ``scipy.signal.stft(..., boundary=None, padded=True)``: the
+    signal is zero-padded at the end to a whole number of hops."""
+    nadd = (-(T - N) % Ns) % N
+    return (T + nadd - N) // Ns + 1
+
+
+def host_fields(p, sros, neighbors, rt, nIter, nFramesSTFT, firstSolveRound):
+    """Schedule-derived ``dv`` fields of one scene.
+
+    sros           node SROs [ppm] (``dv.SROsppm``)
+    neighbors      per node, its neighbour list
+    rt             scheduler.RoundTables (update instants ``t[r, k]`` and
+                   buffer flags ``flags[r, k, q]``)
+    nIter          the reference's iteration count (array rows)
+    nFramesSTFT    frames of ``yinSTFT`` (rows of the MSE cost arrays)
+    firstSolveRound  round of the first DANSE filter update of node
+                   ``p.referenceSensor`` (-1: none)
+    """
+    K, R = len(neighbors), rt.nRounds
+    sros = np.asarray(sros, dtype=np.float64)
+    out = {}
+    # update_sro_estimates / build_phase_shifts_for_srocomp (d_classes.py:
+    # 2364-2489, 2562-2600): with Oracle estimation every update writes the
+    # residual row; with compensation also the estimate row
+    est, res = [], []
+    for k in range(K):
+        nb = list(neighbors[k])
+        e = np.zeros((nIter, len(nb)))
+        s = np.zeros((nIter, len(nb)))
+        if p.estimateSROs == 'Oracle':
+            s[:R, :] = (sros[nb] - sros[k]) * 1e-6
+            if p.compensateSROs:
+                e[:R, :] = s[:R, :]
+        est.append(e)
+        res.append(s)
+    if p.estimateSROs != 'Oracle':
+        # CohDrift / DXCP-PhaT residuals come from the data (not on the device
+        # round path): reported as absent rather than as zeros
+        warnings.warn(f'estimateSROs={p.estimateSROs!r}: SROsEstimates / SROsResiduals are not computed')
+        est, res = None, None
+    out['SROsEstimates'], out['SROsResiduals'] = est, res
+    # compensate_sros (d_classes.py:1955-1970): one entry per neighbour whose
+    # buffer flag is nonzero at that update
+    flags = rt.flags
+    fi = [[] for _ in range(K)]
+    if flags is not None:
+        for k in range(K):
+            nb = list(neighbors[k])
+            for r in range(R):
+                for q in nb:
+                    if flags[r, k, q] != 0:
+                        fi[k].append(r)
+    out['flagIterations'] = fi
+    # update_and_estimate (d_classes.py:1271-1274) compares the NODE index
+    # with referenceSensor: the update instant of that node up to (and
+    # including) its first internal filter update
+    kr = p.referenceSensor
+    first = None
+    if kr < K and R > 0:
+        r = firstSolveRound if firstSolveRound >= 0 else R - 1
+        first = float(rt.t[r, kr])
+    out['firstDANSEupdateRefSensor'] = first
+    # d_classes.py:959-964: allocated, never filled (compute_batch_mse_cost is
+    # not called anywhere in the reference)
+    mse = np.full((nFramesSTFT, K), fill_value=None)
+    out['mseCostOnline'] = mse
+    out['mseCostOnline_c'] = mse.copy()
+    out['mseCostOnline_l'] = mse.copy()
+    return out
+
+
+class DANSEoutputs:
+    """``d_post.DANSEoutputs`` (``d_post.py:22-150``): the parameters plus
+    the output fields selected from ``dv``."""
+
+    def __init__(self):
+        self.initialised = False
+
+    def import_params(self, p):
+        self.__dict__.update(p.__dict__)
+        return self
+
+    def from_variables(self, dv):
+        for nm in ('TDdesiredSignals_est_c', 'STFTDdesiredSignals_est_c', 'TDdesiredSignals_est_l',
+                   'STFTDdesiredSignals_est_l', 'TDdesiredSignals_est_ssbc', 'STFTDdesiredSignals_est_ssbc',
+                   'TDfiltSpeech_c', 'STFTfiltSpeech_c', 'TDfiltNoise_c', 'STFTfiltNoise_c', 'TDfiltSpeech_l',
+                   'STFTfiltSpeech_l', 'TDfiltNoise_l', 'STFTfiltNoise_l', 'TDfiltSpeech_ssbc',
+                   'STFTfiltSpeech_ssbc', 'TDfiltNoise_ssbc', 'STFTfiltNoise_ssbc'):
+            setattr(self, nm, None)
+        self.micSignals = dv.yin
+        if self.simType == 'batch':
+            self.mmseCost = dv.mmseCost
+            self.mmseCostInit = dv.mmseCostInit
+            if self.computeLocal:
+                self.mmseCostLocal = dv.mmseCostLocal
+            if self.computeCentralised:
+                self.mmseCostCentr = dv.mmseCostCentr
+        self.TDdesiredSignals_est = dv.d
+        self.STFTDdesiredSignals_est = dv.dhat
+        if self.computeCentralised:
+            self.TDdesiredSignals_est_c = dv.dCentr
+            self.STFTDdesiredSignals_est_c = dv.dHatCentr
+        if self.computeLocal:
+            self.TDdesiredSignals_est_l = dv.dLocal
+            self.STFTDdesiredSignals_est_l = dv.dHatLocal
+        if self.computeSingleSensorBroadcast:
+            self.TDdesiredSignals_est_ssbc = dv.dSSBC
+            self.STFTDdesiredSignals_est_ssbc = dv.dHatSSBC
+        self.TDfusedSignals = dv.zFullTD
+        if hasattr(dv, 'etaMkFullTD'):
+            self.TDfusedSignalsTI = dv.etaMkFullTD
+        self.SROgroundTruth = dv.SROsppm
+        self.SROsEstimates = dv.SROsEstimates
+        self.SROsResiduals = dv.SROsResiduals
+        self.flagIterations = dv.flagIterations
+        self.firstUpRefSensor = dv.firstDANSEupdateRefSensor
+        self.filters = dv.wTilde
+        if self.simType == 'online':
+            self.filtersEXT = dv.wTildeExt
+            self.yinSTFT = dv.yinSTFT
+            self.yCentrBatch = dv.yCentrBatch
+            self.neighbors = dv.neighbors
+            self.fs = dv.fs
+            self.cleanTargets = dv.cleanSpeechSignalsAtNodes
+            self.mseCostOnline = dv.mseCostOnline
+            if self.computeCentralised:
+                self.mseCostOnline_c = dv.mseCostOnline_c
+            if self.computeLocal:
+                self.mseCostOnline_l = dv.mseCostOnline_l
+        self.filtersCentr = dv.wCentr if self.computeCentralised else None
+        self.filtersLocal = dv.wLocal if self.computeLocal else None
+        if getattr(self, 'saveConditionNumber', False):
+            self.condNumbers = dv.condNumbers
+        self.beta = dv.expAvgBeta
+        self.vadFrames = dv.oVADframes
+        self.initialised = True
+        return self
+
+    def from_snr_signals(self, snrSigs: dict):
+        self.TDfiltSpeech = snrSigs['s']
+        self.TDfiltNoise = snrSigs['n']
+        self.TDfiltSpeech_c = snrSigs['s_c']
+        self.TDfiltNoise_c = snrSigs['n_c']
+        self.TDfiltSpeech_l = snrSigs['s_l']
+        self.TDfiltNoise_l = snrSigs['n_l']
+        self.TDfiltSpeech_ssbc = snrSigs['s_ssbc']
+        self.TDfiltNoise_ssbc = snrSigs['n_ssbc']
+        return self

@@ -203,6 +203,14 @@ int danse_engine_output_bytes(danse_engine* eng, int32_t which, int32_t family, 
 int danse_wola_analysis(const float* x, int32_t C, int32_t T, const int32_t* ends,
                         const float* win, int32_t N, int32_t Ns, float* out, void* stream);
 
+/* Whole-signal STFT (the reference's yinSTFT / yCentrBatch, d_classes.py:
+ * 915-930: scipy.signal.stft(boundary=None, padded=True) times sum(win), i.e.
+ * raw windowed DFTs of frames t Ns .. t Ns + N, zero past the end):
+ * y: [S][C][T] float (device), win: [N] float (device),
+ * out: [S][F][nseg][C] complex float (device), F = N/2 + 1.  N = 1024. */
+int danse_stft(const float* y, int32_t S, int32_t C, int32_t T, int32_t N, int32_t Ns, int32_t nseg,
+               const float* win, float* out, void* stream);
+
 /* Batched filter update on full SCM pairs (update_w / update_w_gevd,
  * d_classes.py:3320-3387): Ryy, Rnn: [B][D][D] complex double (device), w:
  * [B][D] complex float.  The SCM the update factors (Rnn for GEVD, Ryy for

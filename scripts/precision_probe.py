@@ -71,6 +71,27 @@ def gevd_mix(Ryy, Rnn, refSensorIdx, rank=1, rq64=False):
     return out
 
 
+def gevd_planD(Ryy, Rnn, refSensorIdx, rank=1):
+    """planC with the triangular inverse in float32: fp64 Cholesky of Rnn,
+    L rounded to complex64, Li = L^-1 by complex64 substitution, then the
+    planC float32 congruence / eigen / back-transform."""
+    out = np.zeros((Ryy.shape[0], Ryy.shape[-1]), dtype=complex)
+    for f in range(Ryy.shape[0]):
+        L = np.linalg.cholesky(Rnn[f]).astype(np.complex64)
+        Li = sla.solve_triangular(L, np.eye(L.shape[0], dtype=np.complex64), lower=True).astype(np.complex64)
+        A32 = Ryy[f].astype(np.complex64)
+        C = Li @ A32 @ Li.conj().T
+        s, V = np.linalg.eigh(C)
+        idx = np.flip(np.argsort(s))
+        s, V = s[idx], V[:, idx]
+        g = L.conj().T[:, refSensorIdx]
+        for r in range(rank):
+            v = V[:, r]
+            x = Li.conj().T @ v
+            out[f] += (1 - 1 / float(s[r])) * x * complex(v.conj() @ g)
+    return out
+
+
 def gevd_planA(Ryy, Rnn, refSensorIdx, rank=1, li32=False, cong32=False):
     """The device plan: Ryy as stored (fp32), fp64 Cholesky of Rnn, fp64
     triangular inverse, C = Linv Ryy Linv^H in fp64 rounded to complex64,
@@ -101,8 +122,8 @@ def run(args):
     sc = make_case_scene(case)
     dp, wp = make_case_params(case)
     sc.get_vad_per_frame(dp.DFTsize, dp.Ns, wp.vadMinProportionActive)
-    fft32 = mode in ('fft32', 'state32', 'all32', 'mixC', 'mixD', 'ryy32', 'rnn32', 'planA', 'planB', 'planC')
-    ryyAcc32 = mode in ('planA', 'planB', 'planC')
+    fft32 = mode in ('fft32', 'state32', 'all32', 'mixC', 'mixD', 'ryy32', 'rnn32', 'planA', 'planB', 'planC', 'planD')
+    ryyAcc32 = mode in ('planA', 'planB', 'planC', 'planD')
     scm32 = mode in ('scm32', 'state32', 'all32')
     solve32 = mode in ('solve32', 'all32')
 
@@ -127,6 +148,8 @@ def run(args):
         O.update_w_gevd = gevd_planA
     elif mode == 'planC':
         O.update_w_gevd = lambda a, b, refSensorIdx, rank=1: gevd_planA(a, b, refSensorIdx, rank, li32=True, cong32=True)
+    elif mode == 'planD':
+        O.update_w_gevd = gevd_planD
     elif mode == 'planB':
         O.update_w_gevd = lambda a, b, refSensorIdx, rank=1: gevd_planA(a, b, refSensorIdx, rank, li32=True)
     elif mode == 'ryy32':

@@ -41,6 +41,10 @@ ONLINE_CASES = [
          danse=_d(SANDBOX, nodeUpdating='seq', performGEVD=False)),
     dict(name='online_mwf_asy_nobasis', M=[2, 2, 2], dur=2.0, seed=5,
          danse=_d(BATTERY, nodeUpdating='asy', performGEVD=False, use1stFrameAsBasis=False)),
+    # GEVD without the first-frame basis: the SCMs start from the eps-scaled
+    # random init (d_base.py:2446-2450, non-Hermitian; eigh reads the lower triangle)
+    dict(name='online_gevd_asy_nobasis', M=[2, 3, 2], dur=2.0, seed=12,
+         danse=_d(BATTERY, nodeUpdating='asy', use1stFrameAsBasis=False)),
     # config C shape (fewer nodes): SROs, Oracle SRO estimates, phase compensation with
     # full-sample-drift flags (d_classes.py:1936-2046, 2364-2621; quirks Q3, Q5, Q13)
     dict(name='online_C_sro_comp_asy', M=[2, 3, 2], dur=3.0, seed=8, sros=[0, 100, 200],
@@ -167,3 +171,11 @@ def tz_inputs(case):
     wPrev = np.zeros((2 * N - 1, M))
     wPrev[N, 0] = 1.0
     return wHat, yq, h, f, wPrev
+
+
+# online cases whose schedule-derived dv fields (SRO estimates / residuals,
+# flag iterations, first-update instant, MSE-cost arrays) and whole-signal
+# STFTs (yinSTFT, bins subsampled) are dumped as fields_<case>.npz
+FIELD_CASES = ['online_C_sro_comp_asy', 'online_C_sro_noflags_seq', 'online_B_k4m3_seq', 'online_ragged_asy_r2',
+               'online_E_fs_L64_asy']
+FIELD_STFT_BIN_STEP = 37

@@ -24,6 +24,7 @@ import _refharness as H  # noqa: E402
 from danse_amd.scene import make_scene, scene_digest  # noqa: E402
 from golden_cases import ONLINE_CASES, BATCH_CASES, SRO_EVENT_CASES, KAT_CASES, kat_inputs  # noqa: E402
 from golden_cases import DXCP_CASES, dxcp_inputs, TZ_CASES, tz_inputs  # noqa: E402
+from golden_cases import FIELD_CASES, FIELD_STFT_BIN_STEP  # noqa: E402
 
 
 def _run_online(ns, case):
@@ -62,6 +63,48 @@ def _run_online(ns, case):
         sigs = ns.core.generate_signals_for_snr_computation(p.danseParams, dv, w, ns.core.danse)
         for key in ['n', 's']:
             out[f'snr_{key}'] = sigs[key]
+    return out
+
+
+def _dv_fields_read():
+    """The dv attributes d_post.DANSEoutputs.from_variables and
+    d_core.format_output read (parsed from the reference source)."""
+    import ast
+    names = set()
+    for rel, fn in (('danse_toolbox/d_post.py', 'from_variables'), ('danse_toolbox/d_core.py', 'format_output')):
+        tree = ast.parse((H.REF / rel).read_text())
+        for node in ast.walk(tree):
+            if isinstance(node, ast.FunctionDef) and node.name == fn:
+                for sub in ast.walk(node):
+                    if isinstance(sub, ast.Attribute) and isinstance(sub.value, ast.Name) and sub.value.id == 'dv':
+                        names.add(sub.attr)
+    return sorted(names)
+
+
+def _run_fields(ns, name):
+    case = next(c for c in ONLINE_CASES if c['name'] == name)
+    sros = case.get('sros')
+    sc = make_scene(case['M'], sigDur=case['dur'], seed=case['seed'], SROperNode=sros)
+    p = H.make_params(ns, case['M'], **case['danse'])
+    if sros is not None:
+        p.wasnParams.SROperNode = np.array(sros, dtype=float)
+    w = H.to_ref_wasn(ns, sc)
+    p, w = H.prep(ns, p, w)
+    dv, w = ns.core.danse(w, p.danseParams)
+    K = len(case['M'])
+    out = {'digest': scene_digest(sc), 'dvFieldsRead': np.array(_dv_fields_read())}
+    for k in range(K):
+        out[f'SROsEstimates_{k}'] = np.asarray(dv.SROsEstimates[k])
+        out[f'SROsResiduals_{k}'] = np.asarray(dv.SROsResiduals[k])
+        out[f'flagIterations_{k}'] = np.asarray(dv.flagIterations[k], dtype=np.int64)
+        out[f'yinSTFT_{k}'] = dv.yinSTFT[k][::FIELD_STFT_BIN_STEP]
+    out['yCentrBatch_shape'] = np.array(dv.yCentrBatch.shape)
+    f = dv.firstDANSEupdateRefSensor
+    out['firstDANSEupdateRefSensor'] = np.array(np.nan if f is None else float(f))
+    for nm in ('mseCostOnline', 'mseCostOnline_c', 'mseCostOnline_l'):
+        m = getattr(dv, nm)
+        out[f'{nm}_shape'] = np.array(m.shape)
+        out[f'{nm}_allNone'] = np.array(all(x is None for x in np.ravel(m)))
     return out
 
 
@@ -133,7 +176,8 @@ def main():
            [('events', c, _run_sro_events) for c in SRO_EVENT_CASES] + \
            [('kat', c, _run_kat) for c in KAT_CASES] + \
            [('dxcp', c, _run_dxcp) for c in DXCP_CASES] + \
-           [('tz', c, _run_tz) for c in TZ_CASES]
+           [('tz', c, _run_tz) for c in TZ_CASES] + \
+           [('fields', dict(name=f'fields_{c}', src=c), lambda ns, c: _run_fields(ns, c['src'])) for c in FIELD_CASES]
     for kind, case, fn in jobs:
         name = case['name']
         if only and name not in only:

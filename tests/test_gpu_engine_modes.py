@@ -157,3 +157,84 @@ def test_headline_shape_K32x8_D39_vs_oracle():
     print(case['name'], 'rounds', R0, 'w', st, 'd', de)
     assert st['median'] <= 1e-5 and st['p99'] <= 1e-4, st
     assert de <= 1e-4
+
+
+@pytest.mark.parametrize('name', ['online_C_sro_comp_asy', 'online_ragged_asy_r2', 'online_E_fs_L64_asy'])
+def test_dv_fields_on_device(name):
+    """Every dv field the reference's post-processing reads is present; the
+    device STFT (danse_stft: yinSTFT / yCentrBatch) and the schedule fields
+    match the reference's (fields_* fixtures)."""
+    from pathlib import Path
+    from danse_amd.core import danse_multi
+    from danse_amd import outputs as OUT
+    from golden_cases import FIELD_STFT_BIN_STEP
+    case = _case(name)
+    sc, dp, wp = _scene_params(case)
+    dv = danse_multi([sc], dp)[0]
+    z = np.load(Path(__file__).parent / 'golden' / f'fields_{name}.npz')
+    for nm in OUT.ONLINE_DV_FIELDS:
+        assert hasattr(dv, nm), nm
+    for flag, names in OUT.FAMILY_DV_FIELDS.items():
+        if getattr(dp, flag):
+            for nm in names:
+                assert hasattr(dv, nm), nm
+    K = len(case['M'])
+    assert list(dv.yCentrBatch.shape) == list(z['yCentrBatch_shape'])
+    for k in range(K):
+        e = rel_err(dv.yinSTFT[k][::FIELD_STFT_BIN_STEP], z[f'yinSTFT_{k}'])
+        assert e <= 1e-5, (k, e)
+        assert np.array_equal(dv.SROsResiduals[k], z[f'SROsResiduals_{k}'])
+        assert np.array_equal(dv.SROsEstimates[k], z[f'SROsEstimates_{k}'])
+        assert list(dv.flagIterations[k]) == list(z[f'flagIterations_{k}'])
+    assert dv.firstDANSEupdateRefSensor == pytest.approx(float(z['firstDANSEupdateRefSensor']), abs=1e-12)
+    assert list(dv.mseCostOnline.shape) == list(z['mseCostOnline_shape'])
+
+
+def test_sandbox_main_random_ir():
+    """sandbox.main / danse_it_up end to end on a random-IR WASN: DANSE run,
+    noise-only and speech-only replays, format_output."""
+    from danse_amd import sandbox, params as P
+    tp = P.TestParameters(
+        wasnParams=P.WASNparameters(trueRoom=False, signalType='random', nSensorPerNode=[2, 3, 2], sigDur=2.0,
+                                    generateRandomWASNwithSeed=5,
+                                    topologyParams=P.TopologyParameters(topologyType='fully-connected')),
+        danseParams=P.DANSEparameters(simType='online', nodeUpdating='asy', performGEVD=True, computeLocal=True,
+                                      startComputeMetricsAt='after_200ms'),
+        exportParams=P.ExportParameters(bestPerfReference=False, conditionNumberPlot=False))
+    out = sandbox.main(tp)
+    K, T = 3, int(2.0 * 16000)
+    assert out.initialised
+    assert out.TDdesiredSignals_est.shape == (T, K) and out.TDdesiredSignals_est_l.shape == (T, K)
+    assert out.TDfiltSpeech.shape == (T, K) and out.TDfiltNoise.shape == (T, K)
+    assert np.all(np.isfinite(out.TDfiltSpeech)) and np.all(np.isfinite(out.TDfiltNoise))
+    assert np.max(np.abs(out.TDfiltSpeech)) > 0 and np.max(np.abs(out.TDdesiredSignals_est)) > 0
+    assert len(out.filters) == K and len(out.yinSTFT) == K
+
+
+def test_config_C_shape_K16_sro_vs_oracle():
+    """Config C's shape: K = 16 x 4 mics (D = 19, the wavefront class), SROs
+    linspace(0, 200, 16) ppm, Oracle SRO estimates, phase compensation with
+    full-sample-drift flags, asy, against the float64 oracle (the oracle's
+    SRO path is pinned by the online_C_sro_* reference fixtures)."""
+    from danse_amd.core import danse_multi
+    from oracle import danse_ref_cpu as O
+    case = dict(name='online_C_shape_K16_sro', M=[4] * 16, dur=4.0, seed=51, sros=list(np.linspace(0, 200, 16)),
+                danse=dict(BATTERY, nodeUpdating='asy', compensateSROs=True, includeFSDflags=True,
+                           estimateSROs='Oracle'))
+    sc, dp, wp = _scene_params(case)
+    dv = danse_multi([sc], dp)[0]
+    ov = O.danse(sc, dp, vadMinProp=wp.vadMinProportionActive)
+    assert np.array_equal(dv.startRound, ov.startRound)
+    assert np.array_equal(dv.nInternalFilterUps, ov.nInternalFilterUps)
+    assert int(np.sum(dv.diag)) == 0
+    errs = []
+    for k in range(16):
+        s0 = int(ov.startRound[k])
+        errs.append(_bin_rel(dv.wTilde[k][:, s0 + 1:dv.nRounds + 1], ov.wTilde[k][:, s0 + 1:dv.nRounds + 1]).ravel())
+    st = _stats(np.concatenate(errs))
+    de = rel_err(dv.d, ov.d)
+    print(case['name'], 'w', st, 'd', de)
+    assert st['median'] <= 1e-5 and st['p99'] <= 1e-4, st
+    assert de <= 1e-4
+    for k in range(16):
+        assert np.array_equal(dv.SROsEstimates[k][:dv.nRounds], ov.SROsEstimates[k][:dv.nRounds])
