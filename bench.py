@@ -86,6 +86,13 @@ def _wl_params(wl):
     return _battery_params(wl['M'], wl['nodeUpdating'], **wl.get('extra', {}))
 
 
+def update_kernel_name(Dmax, gevd=True):
+    """The update kernel a filter dimension runs on (danse_amd/csrc/update_class.hip)."""
+    if Dmax <= 12:
+        return 'update_kernel_lane'
+    return 'update_kernel_2d' if (gevd and Dmax <= 48) else 'update_kernel_big'
+
+
 def alg_bytes_update(D, opY, opN, solve):
     """Algorithmic HBM bytes of one node x bin x frame of update_kernel
     (in the engine's storage: packed Hermitian Ryy complex64 =
@@ -350,7 +357,7 @@ def run_online(args, wl, S, rank, world, local, dist, traffic=True, pmc_child=Fa
             'frac': tfs / FP32_VALU_PEAK_TFS if valu else gbs / HBM_PEAK_GBS,
             'traffic': (tr or {}).get('bytes_per_launch'),
             'traffic_detail': tr,
-            'kernel': 'update_kernel_' + ('big' if valu else 'lane'), 'avg_launch_ms': avg_ms,
+            'kernel': update_kernel_name(max(Dk), gevd=bool(wl.get('gevd', True))), 'avg_launch_ms': avg_ms,
             'alg_bytes_per_launch': float(byts.mean()), 'alg_flops_per_launch': float(flops.mean()),
             'hbm_GBs': gbs, 'hbm_frac': gbs / HBM_PEAK_GBS, 'valu_TFs': tfs, 'valu_frac': tfs / FP32_VALU_PEAK_TFS}
     return {

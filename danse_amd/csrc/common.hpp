@@ -50,6 +50,9 @@ DANSE_DEV cf cdiv_real(cf a, float s) {
 struct cd {
   double re, im;
 };
+// Component-wise select.  (A conditional operator on the struct values
+// makes clang emit a phi of temporaries' addresses, which keeps the
+// operands out of registers: scratch traffic.)
 DANSE_DEV cd cdk(cf a) { return cd{(double)a.re, (double)a.im}; }
 DANSE_DEV cf cfk(cd a) { return cf{(float)a.re, (float)a.im}; }
 DANSE_DEV cd conjg(cd a) { return cd{a.re, -a.im}; }
@@ -76,6 +79,9 @@ DANSE_DEV void fms_cc(cd& acc, cd a, cd b) {
   acc.re = fma(-a.re, b.re, fma(-a.im, b.im, acc.re));
   acc.im = fma(-a.im, b.re, fma(a.re, b.im, acc.im));
 }
+
+DANSE_DEV cf csel(bool c, cf a, cf b) { return cf{c ? a.re : b.re, c ? a.im : b.im}; }
+DANSE_DEV cd csel(bool c, cd a, cd b) { return cd{c ? a.re : b.re, c ? a.im : b.im}; }
 
 DANSE_DEV int lane_id() { return __lane_id(); }
 

@@ -1,5 +1,7 @@
 // update / filter kernels for large filter dimensions (16 < D <= 64): one
-// frequency bin per wavefront, rows in chunked vector registers
+// frequency bin per wavefront, rows in chunked vector registers.  Since the
+// two-dimensional layout (kernels_2d.hpp) took over the GEVD of D <= 48,
+// these serve the MWF filter of every large class and the GEVD of D > 48
 // (solver64m.hpp: Rnn in float64, mixed-precision filter update).  Same per-bin work as update_kernel in kernels.hpp:
 // SCM update (d_classes.py:2048-2267), filter update (d_classes.py:
 // 3320-3387), external filters (d_classes.py:1627-1694), dhat = w^H yhat.
@@ -9,7 +11,7 @@
 
 namespace danse {
 
-template <int DMAX, int RMAX>
+template <int DMAX, int RMAX, bool GEVD>
 __global__ void __launch_bounds__(64) update_kernel_big(const UpdateArgs a) {
   using namespace big;
   __shared__ LDSM<DMAX> lds;
@@ -93,7 +95,7 @@ __global__ void __launch_bounds__(64) update_kernel_big(const UpdateArgs a) {
     w = act ? wNext[rowc] : cf{0.0f, 0.0f};
   } else if (solve) {
     bool ok = true;
-    if (a.gevd) w = gevd_filter_mixed<DMAX, RMAX>(A, B, lds, li, D, a.rank, d.ref, ok);
+    if constexpr (GEVD) w = gevd_filter_mixed<DMAX, RMAX>(A, B, lds, li, D, a.rank, d.ref, ok);
     else w = mwf_filter_mixed<DMAX>(A, rgetd(B, d.ref), lds, li, D, d.ref, ok);
     if (!ok && li == 0) atomicOr(&a.diag[(s * a.K + d.k) * kMaxFam + d.fam], 1);
   } else {
@@ -103,7 +105,7 @@ __global__ void __launch_bounds__(64) update_kernel_big(const UpdateArgs a) {
   node_bin_tail(a, d, s, f, li, fl, pregiven, true, w, y, gsum<64>(act ? cmul(w, y) : cf{0.0f, 0.0f}));
 }
 
-template <int DMAX, int RMAX>
+template <int DMAX, int RMAX, bool GEVD>
 __global__ void __launch_bounds__(64) filter_update_kernel_big(const cd* Ryy, const cd* Rnn, int B, int D, int gevd,
                                                               int rank, int ref, cf* w, int* diag) {
   using namespace big;
@@ -127,7 +129,8 @@ __global__ void __launch_bounds__(64) filter_update_kernel_big(const cd* Ryy, co
   });
   bool ok = true;
   cf wv;
-  if (gevd) {
+  (void)gevd;
+  if constexpr (GEVD) {
     Row<DMAX> A;
     sfor<0, DMAX>([&](auto cc) { ws<decltype(cc)::value>(A, cfk(rsd<decltype(cc)::value>(Y))); });
     wv = gevd_filter_mixed<DMAX, RMAX>(A, N, lds, li, D, rank, ref, ok);

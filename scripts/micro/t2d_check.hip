@@ -1,0 +1,242 @@
+// Check + timing of the two-dimensional GEVD solver (solver2d.hpp) against
+// the row-per-lane wavefront solver (solver64m.hpp) on random Hermitian
+// positive-definite pairs: Rnn = X X^H / (2D), Ryy = Rnn + sigma h h^H
+// (one dominant source, as in the DANSE scenes) or Rnn + a full-rank term.
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include -I danse_amd/csrc
+//        -DPH_NB=5 scripts/micro/t2d_check.hip -o scripts/micro/bin/t2d_check5
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <vector>
+#include "kernels_2d.hpp"
+#include "kernels_big.hpp"
+
+using namespace danse;
+
+#ifndef PH_NB
+#define PH_NB 5
+#endif
+constexpr int NB = PH_NB;
+constexpr int DM = 8 * NB;
+
+// phase cost: the solver up to (and including) phase STOP
+//   0 load, 1 + float64 Cholesky, 2 + inverse (Li float32), 3 + congruence,
+//   4 + tridiagonalisation, 5 + eigen part / back-transform (full)
+template <int STOP>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
+phase2d(const cd* Ryy, const cd* Rnn, int D, cf* out) {
+  using namespace t2d;
+  __shared__ LDS2<NB> S;
+  const int li = threadIdx.x, p = li >> 3, q = li & 7, b = blockIdx.x;
+  BlkD<NB> M;
+  Blk<NB> Lf, A;
+  sfor<0, NB>([&](auto sc) {
+    constexpr int sb = decltype(sc)::value;
+    sfor<0, NB>([&](auto tc) {
+      constexpr int tb = decltype(tc)::value;
+      const int i = p + 8 * sb, c = q + 8 * tb;
+      const bool in = i < D && c < D;
+      M.v[sb][tb] = csel(in, Rnn[(long long)b * D * D + (in ? i * D + c : 0)], cd{0.0, 0.0});
+    });
+  });
+  auto loadA = [&]() {
+    sfor<0, NB>([&](auto sc) {
+      constexpr int sb = decltype(sc)::value;
+      sfor<0, NB>([&](auto tc) {
+        constexpr int tb = decltype(tc)::value;
+        const int i = p + 8 * sb, c = q + 8 * tb;
+        const bool in = i < D && c < D;
+        A.v[sb][tb] = csel(in, cfk(Ryy[(long long)b * D * D + (in ? i * D + c : 0)]), cf{0.0f, 0.0f});
+      });
+    });
+  };
+  cf res = cf{0.0f, 0.0f};
+  auto sumM = [&]() { sfor<0, NB>([&](auto sc) { sfor<0, NB>([&](auto tc) { res = res + cfk(M.v[decltype(sc)::value][decltype(tc)::value]); }); }); };
+  auto sumA = [&](const Blk<NB>& X) { sfor<0, NB>([&](auto sc) { sfor<0, NB>([&](auto tc) { res = res + X.v[decltype(sc)::value][decltype(tc)::value]; }); }); };
+  if constexpr (STOP == 0) {
+    sumM();
+  } else if constexpr (STOP == 1) {
+    chol2d<NB>(M, S, li, D);
+    sumM();
+  } else {
+    gevd2d_factor<NB>(M, Lf, S, li, D, 0);
+    loadA();
+    if constexpr (STOP == 2) {
+      sumA(Lf);
+      sumA(A);
+    } else {
+      congruence2d<NB>(A, Lf, S, li, D);
+      if constexpr (STOP == 3) {
+        sumA(A);
+        sumA(Lf);
+      } else {
+        tridiag2d<NB>(A, S, li, D);
+        if constexpr (STOP == 4) {
+          res = S.b[li] + cf{S.a[li < DM ? li : 0], 0.0f};
+          sumA(Lf);
+        } else {
+          res = eigen2d<NB, 1>(Lf, S, li, D, 1);
+        }
+      }
+    }
+  }
+  out[(long long)b * 64 + li] = res;
+}
+
+static void check(hipError_t e, const char* what) {
+  if (e != hipSuccess) {
+    printf("HIP error %s: %s\n", what, hipGetErrorString(e));
+    exit(1);
+  }
+}
+
+int main(int argc, char** argv) {
+  const int D = argc > 1 ? atoi(argv[1]) : DM - 1;
+  const int B = argc > 2 ? atoi(argv[2]) : 16416;
+  const int R = argc > 3 ? atoi(argv[3]) : 1;
+  const int ref = argc > 4 ? atoi(argv[4]) : 0;
+  if (D > DM || D <= DM - 8 || (R != 1 && R > kRMax) || ref >= D) {
+    printf("bad arguments\n");
+    return 2;
+  }
+  std::mt19937 rng(7);
+  std::normal_distribution<double> nd;
+  std::uniform_real_distribution<double> ud(0.0, 1.0);
+  const int NU = 256;
+  std::vector<cd> hY((size_t)B * D * D), hN((size_t)B * D * D);
+  for (int u = 0; u < NU; ++u) {
+    std::vector<cd> X((size_t)D * 2 * D), h(D), Z((size_t)D * 2 * D);
+    for (auto& v : X) v = cd{nd(rng), nd(rng)};
+    for (auto& v : Z) v = cd{nd(rng), nd(rng)};
+    for (auto& v : h) v = cd{nd(rng), nd(rng)};
+    const double sig = std::pow(10.0, 2.0 * ud(rng) - 1.0);
+    const bool full = (u % 4) == 3;
+    for (int i = 0; i < D; ++i)
+      for (int j = 0; j < D; ++j) {
+        cd n{0, 0}, z{0, 0};
+        for (int t = 0; t < 2 * D; ++t) {
+          const cd xi = X[i * 2 * D + t], xj = X[j * 2 * D + t];
+          n.re += xi.re * xj.re + xi.im * xj.im;
+          n.im += xi.im * xj.re - xi.re * xj.im;
+          const cd zi = Z[i * 2 * D + t], zj = Z[j * 2 * D + t];
+          z.re += zi.re * zj.re + zi.im * zj.im;
+          z.im += zi.im * zj.re - zi.re * zj.im;
+        }
+        n = cd{n.re / (2 * D), n.im / (2 * D)};
+        cd yv;
+        if (full) {
+          yv = cd{n.re + z.re / (2 * D), n.im + z.im / (2 * D)};
+        } else {
+          const cd hh{h[i].re * h[j].re + h[i].im * h[j].im, h[i].im * h[j].re - h[i].re * h[j].im};
+          yv = cd{n.re + sig * hh.re, n.im + sig * hh.im};
+        }
+        for (int b = u; b < B; b += NU) {
+          hN[((size_t)b * D + i) * D + j] = n;
+          hY[((size_t)b * D + i) * D + j] = yv;
+        }
+      }
+  }
+  cd *dY, *dN;
+  cf *dW0, *dW1;
+  int* dDiag;
+  check(hipMalloc(&dY, hY.size() * sizeof(cd)), "malloc");
+  check(hipMalloc(&dN, hN.size() * sizeof(cd)), "malloc");
+  check(hipMalloc(&dW0, (size_t)B * D * sizeof(cf)), "malloc");
+  check(hipMalloc(&dW1, (size_t)B * D * sizeof(cf)), "malloc");
+  check(hipMalloc(&dDiag, (size_t)B * sizeof(int)), "malloc");
+  check(hipMemcpy(dY, hY.data(), hY.size() * sizeof(cd), hipMemcpyHostToDevice), "h2d");
+  check(hipMemcpy(dN, hN.data(), hN.size() * sizeof(cd), hipMemcpyHostToDevice), "h2d");
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  auto run = [&](int which) {
+    if (which == 0) {
+      if (R == 1)
+        hipLaunchKernelGGL((filter_update_kernel_big<DM, 1, true>), dim3(B), dim3(64), 0, 0, dY, dN, B, D, 1, R, ref, dW0,
+                           dDiag);
+      else
+        hipLaunchKernelGGL((filter_update_kernel_big<DM, kRMax, true>), dim3(B), dim3(64), 0, 0, dY, dN, B, D, 1, R, ref,
+                           dW0, dDiag);
+    } else {
+      if (R == 1)
+        hipLaunchKernelGGL((filter_update_kernel_2d<NB, 1>), dim3(B), dim3(64), 0, 0, dY, dN, B, D, R, ref, dW1,
+                           dDiag);
+      else
+        hipLaunchKernelGGL((filter_update_kernel_2d<NB, kRMax>), dim3(B), dim3(64), 0, 0, dY, dN, B, D, R, ref, dW1,
+                           dDiag);
+    }
+  };
+  float best[2] = {1e30f, 1e30f};
+  for (int which = 0; which < 2; ++which) {
+    for (int rep = 0; rep < 4; ++rep) {
+      hipEventRecord(e0);
+      run(which);
+      hipEventRecord(e1);
+      check(hipEventSynchronize(e1), "sync");
+      float ms;
+      hipEventElapsedTime(&ms, e0, e1);
+      if (rep > 0) best[which] = std::min(best[which], ms);
+    }
+  }
+  check(hipGetLastError(), "launch");
+  {
+    cf* dOut;
+    check(hipMalloc(&dOut, (size_t)B * 64 * sizeof(cf)), "malloc");
+    const char* names[] = {"load", "+chol64", "+inv64", "+congruence", "+tridiag", "+eigen (full)"};
+    auto ph = [&](int st) {
+      switch (st) {
+        case 0: hipLaunchKernelGGL(phase2d<0>, dim3(B), dim3(64), 0, 0, dY, dN, D, dOut); break;
+        case 1: hipLaunchKernelGGL(phase2d<1>, dim3(B), dim3(64), 0, 0, dY, dN, D, dOut); break;
+        case 2: hipLaunchKernelGGL(phase2d<2>, dim3(B), dim3(64), 0, 0, dY, dN, D, dOut); break;
+        case 3: hipLaunchKernelGGL(phase2d<3>, dim3(B), dim3(64), 0, 0, dY, dN, D, dOut); break;
+        case 4: hipLaunchKernelGGL(phase2d<4>, dim3(B), dim3(64), 0, 0, dY, dN, D, dOut); break;
+        default: hipLaunchKernelGGL(phase2d<5>, dim3(B), dim3(64), 0, 0, dY, dN, D, dOut); break;
+      }
+    };
+    for (int st = 0; st <= 5; ++st) {
+      float bst = 1e30f;
+      for (int rep = 0; rep < 4; ++rep) {
+        hipEventRecord(e0);
+        ph(st);
+        hipEventRecord(e1);
+        check(hipEventSynchronize(e1), "sync");
+        float ms;
+        hipEventElapsedTime(&ms, e0, e1);
+        if (rep > 0) bst = std::min(bst, ms);
+      }
+      printf("  phase %d %-14s %8.3f ms\n", st, names[st], bst);
+    }
+    hipFree(dOut);
+  }
+  std::vector<cf> w0((size_t)B * D), w1((size_t)B * D);
+  check(hipMemcpy(w0.data(), dW0, w0.size() * sizeof(cf), hipMemcpyDeviceToHost), "d2h");
+  check(hipMemcpy(w1.data(), dW1, w1.size() * sizeof(cf), hipMemcpyDeviceToHost), "d2h");
+  std::vector<double> err(NU);
+  for (int u = 0; u < NU; ++u) {
+    double num = 0, den = 0;
+    for (int i = 0; i < D; ++i) {
+      const cf a = w0[(size_t)u * D + i], b = w1[(size_t)u * D + i];
+      num += (double)(a.re - b.re) * (a.re - b.re) + (double)(a.im - b.im) * (a.im - b.im);
+      den += (double)a.re * a.re + (double)a.im * a.im;
+    }
+    err[u] = std::sqrt(num / std::max(den, 1e-300));
+  }
+  // every tiled copy must equal its first instance (determinism across blocks)
+  double dmax = 0;
+  for (int b = NU; b < B; ++b)
+    for (int i = 0; i < D; ++i) {
+      const cf a = w1[(size_t)(b % NU) * D + i], c = w1[(size_t)b * D + i];
+      dmax = std::max(dmax, (double)std::fabs(a.re - c.re) + std::fabs(a.im - c.im));
+    }
+  std::sort(err.begin(), err.end());
+  printf("NB=%d D=%d B=%d R=%d ref=%d  old %.3f ms  2d %.3f ms  speedup %.2fx\n", NB, D, B, R, ref, best[0], best[1],
+         best[0] / best[1]);
+  printf("  rel err 2d vs old: median %.2e p99 %.2e max %.2e   tiled-copy max diff %.2e\n", err[NU / 2],
+         err[(NU * 99) / 100], err[NU - 1], dmax);
+  printf("  w0[0..2] = (%g,%g) (%g,%g)  w1 = (%g,%g) (%g,%g)\n", w0[0].re, w0[0].im, w0[1].re, w0[1].im, w1[0].re,
+         w1[0].im, w1[1].re, w1[1].im);
+  return 0;
+}
