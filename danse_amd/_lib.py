@@ -23,6 +23,7 @@ OP_KEEP, OP_SET, OP_AVG = 0, 1, 2
 FLAG_SOLVE = 0x10
 FLAG_EXT_TARGET = 0x20
 FLAG_PREGIVEN = 0x40
+FLAG_INITSLOT = 0x80
 EXT_COPY, EXT_RELAX, EXT_KEEP, EXT_REFONLY = 0, 1, 2, 3
 OUT_W, OUT_WEXT, OUT_D, OUT_DHAT, OUT_Z, OUT_DIAG = 0, 1, 2, 3, 4, 5
 
@@ -40,7 +41,7 @@ class DanseCfg(ctypes.Structure):
         ('w0', _p_f32), ('wExt0', _p_f32), ('wExtTarget0', _p_f32), ('scmInit', ctypes.POINTER(ctypes.c_double)),
         ('keepHistory', _c_i32),
         ('zLag', _p_u8), ('zPhase', ctypes.POINTER(ctypes.c_double)),
-        ('fsTab', _p_i32), ('zStreamLen', _c_i32),
+        ('fsTab', _p_i32), ('zStreamLen', _c_i32), ('scmInitPerBin', _c_i32),
     ]
 
 

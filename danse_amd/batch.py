@@ -72,6 +72,8 @@ class BatchEngine:
             doSolve[:] = 1
         self._doSolve = doSolve
         fi = dict(initType=p.filterInitType, fixedValue=p.filterInitFixedValue)
+        if p.filterInitType == 'random':
+            raise NotImplementedError("filterInitType 'random' in batch mode (the online engine supports it)")
         self._w0 = _cf32(np.concatenate([init_complex_filter((F, self.D[k]), p.referenceSensor, **fi).ravel()
                                          for k in range(K)]))
         self._wExt0 = _cf32(np.concatenate([init_complex_filter((F, self.M[k]), p.referenceSensor, **fi).ravel()

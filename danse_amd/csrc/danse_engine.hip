@@ -71,6 +71,7 @@ struct danse_engine {
   std::vector<long long> initW0Off, initScmOff, extSrcOff, tgtOff;
   cf *dW0 = nullptr, *dExt0 = nullptr, *dTgt0 = nullptr;
   cd* dScm0 = nullptr;
+  int scmPerBin = 0;   // dScm0 holds [F][D][D] per family-node (else [D][D])
   FamNode* dFnAll = nullptr;
   long long *dInitW0Off = nullptr, *dInitScmOff = nullptr, *dExtSrcOff = nullptr, *dTgtOff = nullptr;
   // fewSamples broadcasts (cfg.fsTab): T(z) IRs [S][K][Mmax][2N-1], schedule
@@ -109,7 +110,7 @@ static void pick_class(int D, int& G, int& DMAX) {
 // (scene, family-node): one block row per (scene, family-node).
 __global__ void reset_fam_kernel(const FamNode* fns, int nFN, const long long* w0Off, const long long* scmOff,
                                  const cf* w0, const cd* scm0, cf* wHist, long long wStride, cf* Ryy, cd* Rnn,
-                                 long long scmStride, int F) {
+                                 long long scmStride, int F, int perBin) {
   const int s = blockIdx.y / nFN;
   const int i = blockIdx.y % nFN;
   const FamNode fn = fns[i];
@@ -125,8 +126,9 @@ __global__ void reset_fam_kernel(const FamNode* fns, int nFN, const long long* w
       while (r * (r + 1) / 2 > t) --r;
       while ((r + 1) * (r + 2) / 2 <= t) ++r;
       src = (long long)r * D + (t - r * (r + 1) / 2);
+      if (perBin) src += (e % F) * D * D;
     } else {
-      src = e % ((long long)D * D);
+      src = perBin ? e : e % ((long long)D * D);
     }
     const cd v = scm0[scmOff[i] + src];
     Ryy[s * scmStride + fn.scmOff + e] = cfk(v);
@@ -238,7 +240,7 @@ int danse_engine_reset(danse_engine* eng, void* stream) {
   const int nFN = (int)eng->fns.size();
   hipLaunchKernelGGL(reset_fam_kernel, dim3(64, S * nFN), dim3(256), 0, st, eng->dFnAll, nFN, eng->dInitW0Off,
                      eng->dInitScmOff, eng->dW0, eng->dScm0, eng->wHist, eng->wStride, eng->Ryy, eng->Rnn,
-                     eng->scmStride, F);
+                     eng->scmStride, F, eng->scmPerBin);
   HIPCHK(hipGetLastError());
   hipLaunchKernelGGL(reset_ext_kernel, dim3(8, S * (eng->k1 - eng->k0)), dim3(256), 0, st, eng->dM, eng->k0, eng->k1,
                      eng->dExtSrcOff, eng->dWExtNodeOff, eng->dTgtOff, eng->dExt0, eng->dTgt0, eng->wExtHist,
@@ -469,6 +471,8 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
     std::vector<cf> w0h;
     std::vector<cd> scmh;
     long long w0Off = 0, scmInOff = 0;
+    eng->scmPerBin = c->scmInitPerBin ? 1 : 0;
+    const long long nSlice = eng->scmPerBin ? F : 1;
     for (int fam = 0; fam < kMaxFam; ++fam) {
       if (!((eng->families >> fam) & 1)) continue;
       for (int k = 0; k < K; ++k) {
@@ -479,13 +483,13 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
             eng->initScmOff.push_back((long long)scmh.size());
             for (long long e = 0; e < (long long)F * D; ++e)
               w0h.push_back(c->w0 ? cf{c->w0[2 * (w0Off + e)], c->w0[2 * (w0Off + e) + 1]} : cf{0.0f, 0.0f});
-            for (long long e = 0; e < (long long)D * D; ++e)
+            for (long long e = 0; e < nSlice * D * D; ++e)
               scmh.push_back(c->scmInit ? cd{c->scmInit[2 * (scmInOff + e)], c->scmInit[2 * (scmInOff + e) + 1]}
                                         : cd{0.0, 0.0});
           }
         }
         w0Off += (long long)F * D;
-        scmInOff += (long long)D * D;
+        scmInOff += nSlice * D * D;
       }
     }
     std::vector<cf> exth, tgth;

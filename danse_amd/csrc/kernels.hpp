@@ -91,7 +91,7 @@ DANSE_DEV cf load_y(const UpdateArgs& a, const FamNode& d, int s, int f, int li,
       v = v * cf{cs, sn};
     }
   }
-  return act ? v : cf{0.0f, 0.0f};
+  return csel(act, v, cf{0.0f, 0.0f});
 }
 
 // External filters (DANSE family, update_external_filters,

@@ -40,6 +40,7 @@ update_kernel_2d(const UpdateArgs a) {
   const int opY = fl & 3, opN = (fl >> 2) & 3;
   const bool pregiven = (fl & DANSE_FLAG_PREGIVEN) != 0;
   const bool solve = (fl & DANSE_FLAG_SOLVE) != 0 && !pregiven;
+  const bool initslot = (fl & DANSE_FLAG_INITSLOT) != 0;
 
   const cf y = load_y(a, d, s, f, li, act);
   S.vb[li] = y;
@@ -111,14 +112,14 @@ update_kernel_2d(const UpdateArgs a) {
   cf* wPrev = a.wHist + wBase + ((long long)slotPrev * F + f) * D;
   cf* wNext = a.wHist + wBase + ((long long)slotNext * F + f) * D;
   const int rowc = act ? li : 0;
-  if (pregiven) {
+  if (pregiven || initslot) {
     w = csel(act, wNext[rowc], cf{0.0f, 0.0f});
   } else if (solve) {
     if (!ok && li == 0) atomicOr(&a.diag[(s * a.K + d.k) * kMaxFam + d.fam], 1);
   } else {
     w = csel(act, wPrev[rowc], cf{0.0f, 0.0f});
   }
-  if (act && !pregiven) wNext[li] = w;
+  if (act && !pregiven && !initslot) wNext[li] = w;
   node_bin_tail(a, d, s, f, li, fl, pregiven, true, w, y, gsum<64>(csel(act, cmul(w, y), cf{0.0f, 0.0f})));
 }
 

@@ -89,10 +89,11 @@ __global__ void __launch_bounds__(64) update_kernel_big(const UpdateArgs a) {
   const int slotNext = a.wHistory ? r + 1 : ((r + 1) & 1);
   cf* wPrev = a.wHist + wBase + ((long long)slotPrev * F + f) * D;
   cf* wNext = a.wHist + wBase + ((long long)slotNext * F + f) * D;
-  cf w;
+  cf w = cf{0.0f, 0.0f};
   const bool pregiven = (fl & DANSE_FLAG_PREGIVEN) != 0;
-  if (pregiven) {
-    w = act ? wNext[rowc] : cf{0.0f, 0.0f};
+  const bool initslot = (fl & DANSE_FLAG_INITSLOT) != 0;
+  if (pregiven || initslot) {
+    w = csel(act, wNext[rowc], cf{0.0f, 0.0f});
   } else if (solve) {
     bool ok = true;
     if constexpr (GEVD) w = gevd_filter_mixed<DMAX, RMAX>(A, B, lds, li, D, a.rank, d.ref, ok);
@@ -101,7 +102,7 @@ __global__ void __launch_bounds__(64) update_kernel_big(const UpdateArgs a) {
   } else {
     w = act ? wPrev[rowc] : cf{0.0f, 0.0f};
   }
-  if (act && !pregiven) wNext[li] = w;
+  if (act && !pregiven && !initslot) wNext[li] = w;
   node_bin_tail(a, d, s, f, li, fl, pregiven, true, w, y, gsum<64>(act ? cmul(w, y) : cf{0.0f, 0.0f}));
 }
 

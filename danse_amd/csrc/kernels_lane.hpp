@@ -72,7 +72,7 @@ __global__ void __launch_bounds__(64) update_kernel_lane(const UpdateArgs a) {
       sfor<0, i + 1>([&](auto jc) {
         constexpr int j = decltype(jc)::value;
         const cf yy = cy * mulc(y[i], y[j]);
-        A.a[P(i, j)] = (opY == DANSE_OP_SET) ? yy : by * A.a[P(i, j)] + yy;
+        A.a[P(i, j)] = csel(opY == DANSE_OP_SET, yy, by * A.a[P(i, j)] + yy);
         if constexpr (i == j) A.a[P(i, j)].im = 0.0f;
       });
     });
@@ -163,6 +163,8 @@ __global__ void __launch_bounds__(64) update_kernel_lane(const UpdateArgs a) {
       gevd_filter_mixed<D, RMAX>(A, Li, g, a.rank, w);
     }
     if (valid) sfor<0, D>([&](auto ic) { wNext[decltype(ic)::value] = w[decltype(ic)::value]; });
+  } else if (fl & DANSE_FLAG_INITSLOT) {
+    sfor<0, D>([&](auto ic) { w[decltype(ic)::value] = wNext[decltype(ic)::value]; });
   } else {
     sfor<0, D>([&](auto ic) { w[decltype(ic)::value] = wPrev[decltype(ic)::value]; });
     if (valid) sfor<0, D>([&](auto ic) { wNext[decltype(ic)::value] = w[decltype(ic)::value]; });

@@ -49,7 +49,7 @@ DANSE_DEV void tridiag(PTri<D>& A, cf (&u0)[D], cf (&b)[D]) {
     const float nx = fsqrt(nrm2);
     const float ax0 = fsqrt(ax02);
     const float iax0 = frsq(ax02);
-    const cf e = (ax02 > 0.0f) ? cf{x0.re * iax0, x0.im * iax0} : cf{1.0f, 0.0f};
+    const cf e = csel(ax02 > 0.0f, cf{x0.re * iax0, x0.im * iax0}, cf{1.0f, 0.0f});
     const float invn = (nrm2 > 1e-30f) ? frsq(2.0f * nx * (nx + ax0)) : 0.0f;
     cf u[D];
     sfor<j + 1, D>([&](auto ic) {

@@ -248,6 +248,21 @@ DANSE_DEV bool gevd2d_factor(BlkD<NB>& M, Blk<NB>& Lf, LDS2<NB>& S, int li, int 
 template <int NB>
 DANSE_DEV void congruence2d(Blk<NB>& A, const Blk<NB>& Lf, LDS2<NB>& S, int li, int D) {
   const int p = li >> 3, q = li & 7;
+  // scipy.linalg.eigh reads the lower triangle: A[i][c] = conj(A[c][i]) for
+  // i < c (the SCMs are Hermitian except for the random init's residue).
+  // Element (c, i) lives on lane (q, p), register [t][s], and is never one
+  // that this loop rewrites.
+  {
+    const int tl = 8 * q + p;
+    sfor<0, NB>([&](auto sc) {
+      constexpr int s = decltype(sc)::value;
+      sfor<0, NB>([&](auto tc) {
+        constexpr int t = decltype(tc)::value;
+        const cf v = cf{__shfl(A.v[t][s].re, tl), __shfl(A.v[t][s].im, tl)};
+        A.v[s][t] = csel(p + 8 * s < q + 8 * t, conjg(v), A.v[s][t]);
+      });
+    });
+  }
   // Li -> LDS (row-major, pitch DM + 1)
   sfor<0, NB>([&](auto sc) {
     constexpr int s = decltype(sc)::value;

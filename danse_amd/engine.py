@@ -38,39 +38,60 @@ def beta_from_t50p(t50p, fs, Ns):
 
 
 def init_complex_filter(size, refIdx, initType, fixedValue):
-    """``init_complex_filter`` (``d_base.py:2367-2414``) for the
-    deterministic init types (``random`` is not supported on the device)."""
+    """``init_complex_filter`` (``d_base.py:2367-2414``).  ``random`` draws
+    with the reference's default seed 0 over the whole ``size`` (the caller
+    passes the reference's ``(F, nIter + 1, D)`` so the first iteration's
+    slice holds the same numbers)."""
     if initType == 'selectFirstSensor':
         w = np.zeros(size, dtype=np.complex128)
         w[..., refIdx] = 1
+    elif initType == 'random':
+        rng = np.random.default_rng(0)
+        w = (rng.random(size) - 0.5) + 1j * (rng.random(size) - 0.5)
     elif initType == 'fixedValue':
         w = np.full(size, fixedValue, dtype=np.complex128)
     elif initType == 'selectFirstSensor_andFixedValue':
         w = np.full(size, fixedValue, dtype=np.complex128)
         w[..., refIdx] = 1
     else:
-        raise NotImplementedError(f'filterInitType {initType!r} on the device path')
+        raise ValueError(f'filterInitType {initType!r}')
     return w
 
 
-def init_scm_slice(p, Mtot):
-    """``init_covmats`` (``d_base.py:2417-2470``) with the seed of
-    ``init_from_wasn`` (``d_classes.py:553-571``), same-for-all-bins slice."""
+def init_filter_history(F, nIter, D, refIdx, initType, fixedValue):
+    """Initial filter history ``(F, nIter + 1, D)`` of one family-node
+    (``init_from_wasn``, ``d_classes.py:392-410,660-700``); deterministic
+    init types broadcast one ``(F, D)`` slice (no copy)."""
+    if initType == 'random':
+        return init_complex_filter((F, nIter + 1, D), refIdx, initType, fixedValue)
+    return np.broadcast_to(init_complex_filter((F, D), refIdx, initType, fixedValue)[:, None, :], (F, nIter + 1, D))
+
+
+def init_scm_slices(p, Mtot, K, F):
+    """``init_covmats`` (``d_base.py:2417-2470``) in the draw order of
+    ``init_from_wasn`` (``d_classes.py:553-651``): one ``fullSlice`` for all
+    nodes or one per node (drawn node by node from the same generator), each
+    ``(Mtot, Mtot)`` or per bin ``(F, Mtot, Mtot)``.  Returns the K slices."""
     if p.covMatInitType == 'batch_estimates':
-        raise NotImplementedError('covMatInitType batch_estimates')
-    if not p.covMatSameInitForAllFreqs or not p.covMatSameInitForAllNodes:
-        raise NotImplementedError('per-bin / per-node random SCM init on the device path')
+        raise NotImplementedError('covMatInitType batch_estimates (batch-mode SCM estimates as the online init)')
     rng = np.random.default_rng(p.seed)
-    dims = (Mtot, Mtot)
-    rand = 2 * rng.random(dims) - 1 + 1j * (2 * rng.random(dims) - 1)
-    if p.covMatInitType == 'fully_random':
-        return p.covMatRandomInitScaling * rand
-    eye = np.eye(Mtot) * p.covMatEyeInitScaling
-    if p.covMatInitType == 'eye_and_random':
-        return eye + p.covMatRandomInitScaling * rand
-    if p.covMatInitType == 'eye':
-        return eye
-    raise ValueError(p.covMatInitType)
+    dims = (Mtot, Mtot) if p.covMatSameInitForAllFreqs else (F, Mtot, Mtot)
+
+    def draw():
+        rand = 2 * rng.random(dims) - 1 + 1j * (2 * rng.random(dims) - 1)
+        if p.covMatInitType == 'fully_random':
+            return p.covMatRandomInitScaling * rand
+        eye = np.eye(Mtot) * p.covMatEyeInitScaling
+        if p.covMatInitType == 'eye_and_random':
+            return eye + p.covMatRandomInitScaling * rand
+        if p.covMatInitType == 'eye':
+            return np.broadcast_to(eye, dims).copy()
+        raise ValueError(p.covMatInitType)
+
+    if p.covMatSameInitForAllNodes:
+        one = draw()
+        return [one] * K
+    return [draw() for _ in range(K)]
 
 
 def _cf32(a):
@@ -178,6 +199,7 @@ class DanseEngine:
                 if min(self.Dfam[f]) < p.GEVDrank:
                     raise ValueError('GEVD rank larger than a filter dimension')
         self.pregiven = pregiven
+        self._ran = False
         self._build_flags()
         self._build_cfg()
         # inputs [S][Mtot][T] float32 on the device
@@ -190,6 +212,21 @@ class DanseEngine:
         L.check(self.lib.danse_engine_set_inputs(self.eng, ctypes.c_void_p(self.y.data_ptr())), self.eng)
         if pregiven is not None:
             self._load_pregiven(pregiven)
+        self._load_init_history()
+
+    def _load_init_history(self):
+        """filterInitType 'random': the whole init history (F, nIter + 1, D)
+        of every family-node goes to the device, since a node that has not
+        started updating uses the init slot of each iteration (INITSLOT)."""
+        if self.p.filterInitType != 'random' or self.pregiven is not None:
+            return
+        if not self.keepHistory:
+            raise NotImplementedError("filterInitType 'random' needs keepHistory=True (per-iteration init slots)")
+        R = self.R
+        for f in self.fams:
+            for k in range(self.k0, self.k1):
+                h = np.transpose(self._winit(f, k)[:, :R + 1, :], (1, 0, 2)).astype(np.complex64)
+                self._put(L.OUT_W, f, k, np.broadcast_to(h[None], (self.S,) + h.shape))
 
     # ------------------------------------------------------------------ #
     def _build_sro_tables(self, sc0):
@@ -269,10 +306,16 @@ class DanseEngine:
                     if started.any():
                         self.startRound[s, f, k] = int(np.argmax(started))
                     solve = started & doSolve[k]
+                    # not yet started: perform_update leaves the init slot
+                    # wTilde[:, i + 1] in place (d_classes.py:2290-2362); it
+                    # differs from w[i] only for random init (flag INITSLOT)
+                    initslot = (~started) & doSolve[k] & (p.filterInitType == 'random')
                     if p.bypassUpdates:
                         solve[:] = False
+                        initslot[:] = False
                     self.nSolves[s, f, k] = int(solve.sum())
                     b = opY.astype(np.uint8) | (opN.astype(np.uint8) << 2) | (solve.astype(np.uint8) * L.FLAG_SOLVE)
+                    b = b | (initslot.astype(np.uint8) * L.FLAG_INITSLOT)
                     if f == L.FAM_DANSE:
                         b = b | (extT[:, k].astype(np.uint8) * L.FLAG_EXT_TARGET)
                     if self.pregiven is not None:
@@ -280,29 +323,36 @@ class DanseEngine:
                     fl[:, s, f, k] = b
         self.flags = fl
 
+    def _winit(self, f, k):
+        """Initial filter history (F, nIter + 1, D) of family f ('ext': the
+        external filters) at node k."""
+        p = self.p
+        if f == 'ext':
+            D, ref = self.M[k], p.referenceSensor
+        else:
+            D, ref = self.Dfam[f][k], self.refFam[f][k]
+        return init_filter_history(self.F, self.nIter, D, ref, p.filterInitType, p.filterInitFixedValue)
+
     def _build_cfg(self):
         p, S, K, F = self.p, self.S, self.K, self.F
         fi = dict(initType=p.filterInitType, fixedValue=p.filterInitFixedValue)
         w0 = []
         scm = []
-        sl = init_scm_slice(p, self.Mtot)
+        sls = init_scm_slices(p, self.Mtot, K, F)
         for f in [0, 1, 2, 3]:
             if f not in self.fams:
                 continue
             for k in range(K):
                 D = self.Dfam[f][k]
-                w0.append(init_complex_filter((F, D), self.refFam[f][k], **fi).ravel())
-                if f == L.FAM_LOCAL:
-                    scm.append(sl[:self.M[k], :self.M[k]].ravel())
-                elif f == L.FAM_CENTR:
-                    scm.append(sl.ravel())
-                else:
-                    scm.append(sl[:D, :D].ravel())
+                w0.append(np.ascontiguousarray(self._winit(f, k)[:, 0, :]).ravel())
+                scm.append(np.ascontiguousarray(sls[k][..., :D, :D]).ravel())
         self._w0 = _cf32(np.concatenate(w0))
         self._scm = np.ascontiguousarray(np.concatenate(scm).astype(np.complex128)).view(np.float64)
-        ext = [init_complex_filter((F, self.M[k]), p.referenceSensor, **fi).ravel() for k in range(K)]
+        ext = [np.ascontiguousarray(self._winit('ext', k)[:, 0, :]).ravel() for k in range(K)]
         self._wExt0 = _cf32(np.concatenate(ext))
-        self._tgt0 = self._wExt0.copy()
+        # wTildeExtTarget: its own (F, M) draw (d_classes.py:687-691)
+        tgt = [init_complex_filter((F, self.M[k]), p.referenceSensor, **fi).ravel() for k in range(K)]
+        self._tgt0 = _cf32(np.concatenate(tgt))
         extMode = []
         for k in range(K):
             if p.onlyBroadcastRefSensorSigs:
@@ -348,6 +398,7 @@ class DanseEngine:
         c.zPhase = _ptr(self._zPhase, ctypes.c_double)
         self._fsTab = np.ascontiguousarray(self.rt.fsTab, dtype=np.int32) if self.fewSamples else None
         c.fsTab = _ptr(self._fsTab, ctypes.c_int32)
+        c.scmInitPerBin = 0 if p.covMatSameInitForAllFreqs else 1
         c.zStreamLen = int(self.rt.zStreamLen) if self.fewSamples else 0
         self.zLen = c.zStreamLen if self.fewSamples else self.R * self.Ns
         self._cfg = c
@@ -388,6 +439,9 @@ class DanseEngine:
         return ctypes.c_void_p(st.cuda_stream)
 
     def run(self, graph=True, stream=None):
+        if self._ran:
+            self._load_init_history()   # the solves of the previous run overwrote init slots
+        self._ran = True
         L.check(self.lib.danse_engine_run(self.eng, 0, self.R, self.stream_ptr(stream), int(bool(graph))), self.eng)
         return self
 
@@ -440,10 +494,10 @@ class DanseEngine:
             for k in range(self.k0, self.k1):
                 D = self.Dfam[f][k]
                 w = self._get(L.OUT_W, f, k, shape=(S, hist, F, D))
-                init = init_complex_filter((F, D), self.refFam[f][k], **fi)
+                init = self._winit(f, k)
                 for s in range(S):
                     full = np.empty((F, nI + 1, D), dtype=np.complex128)
-                    full[:] = init[:, None, :]
+                    full[:] = init
                     if self.keepHistory:
                         full[:, :R + 1, :] = np.transpose(w[s], (1, 0, 2))
                     getattr(res[s], wn)[k] = full
@@ -455,10 +509,10 @@ class DanseEngine:
         for k in range(self.k0, self.k1):
             M = self.M[k]
             e = self._get(L.OUT_WEXT, 0, k, shape=(S, hist, F, M))
-            init = init_complex_filter((F, M), p.referenceSensor, **fi)
+            init = self._winit('ext', k)
             for s in range(S):
                 full = np.empty((F, nI + 1, M), dtype=np.complex128)
-                full[:] = init[:, None, :]
+                full[:] = init
                 if self.keepHistory:
                     full[:, :R + 1, :] = np.transpose(e[s], (1, 0, 2))
                 res[s].wTildeExt[k] = full

@@ -55,6 +55,11 @@ enum danse_family {
 #define DANSE_FLAG_EXT_TARGET 0x20
 #define DANSE_FLAG_PREGIVEN 0x40   /* w[i+1], wExt[i+1] pre-loaded (danse_engine_put):
                                       update_using_pregiven_filters, d_classes.py:1338-1352 */
+#define DANSE_FLAG_INITSLOT 0x80   /* the family-node has not started updating: its filter
+                                      for this round is the (pre-loaded) init slot w[i+1]
+                                      (perform_update leaves wTilde[:, i+1] untouched,
+                                      d_classes.py:2290-2362; differs from w[i] only for
+                                      filterInitType 'random') */
 
 /* External-filter update mode per node (update_external_filters,
  * d_classes.py:1627-1694). */
@@ -118,6 +123,9 @@ typedef struct danse_cfg {
   const int32_t* fsTab;     /* [R*K*DANSE_FS_FIELDS]: DANSE_FS_BCEND, _LEN, _POS,
                                _IRSRC, _ZEND (see enum danse_fs_field)          */
   int32_t zStreamLen;       /* samples per node stream with fsTab (else R*Ns)  */
+  int32_t scmInitPerBin;    /* 1: scmInit holds one slice per bin, [F][D][D] per
+                               family-node (covMatSameInitForAllFreqs = False,
+                               init_from_wasn, d_classes.py:553-651); 0: [D][D] */
 } danse_cfg;
 
 /* Fields of one fsTab entry (round r, node k). */

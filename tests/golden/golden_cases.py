@@ -45,6 +45,15 @@ ONLINE_CASES = [
     # random init (d_base.py:2446-2450, non-Hermitian; eigh reads the lower triangle)
     dict(name='online_gevd_asy_nobasis', M=[2, 3, 2], dur=2.0, seed=12,
          danse=_d(BATTERY, nodeUpdating='asy', use1stFrameAsBasis=False)),
+    # init variants (d_base.py:2367-2470, d_classes.py:553-700): random filters
+    # (seed 0 over the whole (F, nIter + 1, D) history), per-bin and per-node
+    # eye + eps-scaled random SCMs (non-Hermitian at eps scale; eigh reads the
+    # lower triangle), no first-frame basis so the init stays in the recursion
+    dict(name='online_init_random_asy', M=[2, 3, 2], dur=2.0, seed=13,
+         danse=_d(BATTERY, nodeUpdating='asy', filterInitType='random', covMatInitType='eye_and_random',
+                  covMatSameInitForAllFreqs=False,
+                  covMatSameInitForAllNodes=False, use1stFrameAsBasis=False, computeLocal=True,
+                  computeCentralised=True)),
     # config C shape (fewer nodes): SROs, Oracle SRO estimates, phase compensation with
     # full-sample-drift flags (d_classes.py:1936-2046, 2364-2621; quirks Q3, Q5, Q13)
     dict(name='online_C_sro_comp_asy', M=[2, 3, 2], dur=3.0, seed=8, sros=[0, 100, 200],

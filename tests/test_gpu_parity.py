@@ -166,6 +166,10 @@ BIG_CASES = [
          danse=dict(ONLINE_CASES[1]['danse'], nodeUpdating='seq', GEVDrank=2)),
     dict(name='online_big_D20_mwf', M=[17, 4, 4, 5], dur=4.0, seed=23,
          danse=dict(ONLINE_CASES[1]['danse'], nodeUpdating='asy', performGEVD=False)),
+    # random filters + per-bin / per-node non-Hermitian SCM init on the 2D
+    # classes (D = 15, centralised 24): the lower-triangle reading of eigh
+    dict(name='online_big_init_random', M=[12, 6, 3, 3], dur=3.0, seed=24,
+         danse=dict(next(c for c in ONLINE_CASES if c['name'] == 'online_init_random_asy')['danse'])),
 ]
 
 
