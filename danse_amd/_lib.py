@@ -74,6 +74,13 @@ SIGNATURES = {
     'danse_engine_finish': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p]),
     'danse_engine_set_zspec': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p]),
     'danse_engine_zspec': (_c_i32, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t)]),
+    'danse_engine_gate': (_c_i32, [ctypes.c_void_p, _c_i32, _c_i32, _p_i32, _p_i32, _p_i32,
+                                   ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), _p_i32,
+                                   ctypes.c_void_p]),
+    'danse_engine_set_flags': (_c_i32, [ctypes.c_void_p, _p_u8, ctypes.c_void_p]),
+    'danse_engine_set_gate': (_c_i32, [ctypes.c_void_p, _c_i32, _p_i32, _p_i32, _p_i32, _p_i32,
+                                       ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
+    'danse_engine_gate_verdicts': (_c_i32, [ctypes.c_void_p, _p_i32, ctypes.c_void_p]),
     'danse_engine_get': (_c_i32, [ctypes.c_void_p, _c_i32, _c_i32, _c_i32, ctypes.c_void_p, ctypes.c_size_t,
                                   ctypes.c_void_p]),
     'danse_engine_put': (_c_i32, [ctypes.c_void_p, _c_i32, _c_i32, _c_i32, ctypes.c_void_p, ctypes.c_size_t,

@@ -11,6 +11,7 @@
 
 #include "bcast.hpp"
 #include "classes.hpp"
+#include "gate.hpp"
 #include "tzconv.hpp"
 
 using namespace danse;
@@ -71,6 +72,15 @@ struct danse_engine {
   std::vector<long long> initW0Off, initScmOff, extSrcOff, tgtOff;
   cf *dW0 = nullptr, *dExt0 = nullptr, *dTgt0 = nullptr;
   cd* dScm0 = nullptr;
+  cf* liCache = nullptr;     // GEVD factor cache of the lane classes (kernels.hpp li_reusable)
+  // speculative gate schedule (danse_engine_set_gate): candidates sorted by
+  // round, gateOff[r] .. gateOff[r + 1] checked between bcast(r) and update(r)
+  GateCand* dGateCand = nullptr;
+  int* dGateVerdict = nullptr;
+  std::vector<int> gateOff;
+  std::vector<int> gateDmax;   // per round: largest candidate D (LDS size)
+  int nGate = 0;
+  long long liStride = 0;
   int scmPerBin = 0;   // dScm0 holds [F][D][D] per family-node (else [D][D])
   FamNode* dFnAll = nullptr;
   long long *dInitW0Off = nullptr, *dInitScmOff = nullptr, *dExtSrcOff = nullptr, *dTgtOff = nullptr;
@@ -298,7 +308,7 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
     if (c->ref >= eng->M[k]) return fail(eng, "referenceSensor must be < M_k for every node");
 
   // ---- family-node table (owned nodes), channel lists
-  long long scmOff = 0, wOff = 0;
+  long long scmOff = 0, wOff = 0, liOff = 0;
   const long long histW = c->keepHistory ? (long long)R + 1 : 2;
   for (int fam = 0; fam < kMaxFam; ++fam) {
     if (!((eng->families >> fam) & 1)) continue;
@@ -328,11 +338,15 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
       scmOff += fn.packed ? (long long)F * fn.D * (fn.D + 1) / 2 : (long long)F * fn.D * fn.D;
       fn.wOff = wOff;
       wOff += histW * F * fn.D;
+      fn.liOff = liOff;
+      if (c->gevd && fn.packed) liOff += (long long)F * (fn.D * (fn.D + 1) / 2 + fn.D);
+      else if (c->gevd && class_dmax(fn.D) <= 48) liOff += (long long)F * (64 * (class_dmax(fn.D) / 8) * (class_dmax(fn.D) / 8) + 64);
       eng->fns.push_back(fn);
     }
   }
   eng->scmStride = scmOff;
   eng->wStride = wOff;
+  eng->liStride = liOff;
   eng->wExtNodeOff.assign(K, 0);
   long long eo = 0, to = 0;
   for (int k = 0; k < K; ++k) {
@@ -452,6 +466,7 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
   HIPCHK(dalloc(&eng->dhat, (size_t)kMaxFam * S * K * R * F));
   HIPCHK(dalloc(&eng->d, (size_t)kMaxFam * S * K * c->T));
   HIPCHK(dalloc(&eng->diag, (size_t)S * K * kMaxFam));
+  if (eng->liStride > 0) HIPCHK(dalloc(&eng->liCache, (size_t)S * eng->liStride));
   HIPCHK(hipMemset(eng->Yspec, 0, 2 * S * MT * F * sizeof(cf)));
   HIPCHK(hipMemset(eng->Zspec, 0, (size_t)2 * K * S * F * sizeof(cf)));
   HIPCHK(hipMemset(eng->zPrev, 0, (size_t)S * K * c->N * sizeof(float)));
@@ -545,7 +560,8 @@ void danse_engine_destroy(danse_engine* eng) {
                   eng->ownZspec ? eng->Zspec : nullptr, eng->Ryy,
                   eng->Rnn, eng->wHist, eng->wExtHist, eng->wExtTarget, eng->dhat, eng->zPrev, eng->zStream, eng->d,
                   eng->diag, eng->dW0, eng->dScm0, eng->dExt0, eng->dTgt0, eng->dFnAll, eng->dInitW0Off,
-                  eng->dInitScmOff, eng->dExtSrcOff, eng->dTgtOff, eng->dFsTab, eng->wIR, eng->dSn};
+                  eng->dInitScmOff, eng->dExtSrcOff, eng->dTgtOff, eng->dFsTab, eng->wIR, eng->dSn, eng->liCache,
+                  eng->dGateCand, eng->dGateVerdict};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (auto& cl : eng->classes) {
@@ -586,6 +602,7 @@ static UpdateArgs make_update(danse_engine* e, int r) {
   a.wHistory = e->keepHistory; a.wExtHist = e->wExtHist; a.wExtStride = e->wExtStride; a.wExtHistory = e->keepHistory;
   a.wExtTarget = e->wExtTarget; a.tgtStride = e->tgtStride; a.dhat = e->dhat; a.beta = e->dBeta;
   a.betaExt = e->dBetaExt; a.alphaExt = e->alphaExt; a.gevd = e->gevd; a.rank = e->rank; a.diag = e->diag;
+  a.liCache = e->liCache; a.liStride = e->liStride;
   return a;
 }
 
@@ -659,8 +676,16 @@ int danse_engine_run(danse_engine* eng, int32_t r0, int32_t r1, void* stream, in
   HIPCHK(hipSetDevice(eng->dev));
   hipStream_t st = (hipStream_t)stream;
   auto seq = [&](hipStream_t s) {
+    if (eng->nGate > 0 && r0 == 0) (void)hipMemsetAsync(eng->dGateVerdict, 0xff, eng->nGate * sizeof(int), s);
     for (int r = r0; r < r1; ++r) {
       launch_bcast(eng, r, r > 0, 1, s);
+      if (eng->nGate > 0 && eng->gateOff[r + 1] > eng->gateOff[r]) {
+        const int n = eng->gateOff[r + 1] - eng->gateOff[r];
+        const size_t lds = (size_t)eng->gateDmax[r] * (eng->gateDmax[r] + 1) * sizeof(cd);
+        hipLaunchKernelGGL(gate_kernel, dim3(eng->F, n), dim3(64), lds, s, make_update(eng, r), eng->dFnAll,
+                           eng->dGateCand + eng->gateOff[r], eng->dInitScmOff, eng->dScm0, eng->scmPerBin,
+                           eng->dGateVerdict + eng->gateOff[r]);
+      }
       launch_update(eng, r, s);
     }
     if (r1 == eng->R) launch_bcast(eng, eng->R, 1, 0, s);
@@ -706,6 +731,101 @@ int danse_engine_set_zspec(danse_engine* eng, void* ptr) {
     eng->graphExec = nullptr;
     eng->graphR0 = eng->graphR1 = -1;
   }
+  return 0;
+}
+
+int danse_engine_gate(danse_engine* eng, int32_t r, int32_t n, const int32_t* family, const int32_t* node,
+                      const int32_t* scene, const double* qY, const double* qN, int32_t* verdict, void* stream) {
+  if (!eng || !eng->y) return fail(eng, "inputs not set");
+  if (r < 0 || r >= eng->R || n < 0) return fail(eng, "bad gate arguments");
+  if (n == 0) return 0;
+  HIPCHK(hipSetDevice(eng->dev));
+  hipStream_t st = (hipStream_t)stream;
+  std::vector<GateCand> h(n);
+  int dmax = 1;
+  for (int i = 0; i < n; ++i) {
+    int fni = -1;
+    for (size_t x = 0; x < eng->fns.size(); ++x)
+      if (eng->fns[x].fam == family[i] && eng->fns[x].k == node[i]) fni = (int)x;
+    if (fni < 0 || scene[i] < 0 || scene[i] >= eng->S) return fail(eng, "gate candidate not on this engine");
+    h[i] = GateCand{fni, scene[i], qY[i], qN[i]};
+    dmax = std::max(dmax, eng->fns[fni].D);
+  }
+  GateCand* dC = nullptr;
+  int* dV = nullptr;
+  HIPCHK(dalloc(&dC, (size_t)n));
+  HIPCHK(dalloc(&dV, (size_t)n));
+  std::vector<int> ones(n, 1);
+  HIPCHK(hipMemcpyAsync(dC, h.data(), n * sizeof(GateCand), hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(dV, ones.data(), n * sizeof(int), hipMemcpyHostToDevice, st));
+  UpdateArgs a = make_update(eng, r);
+  const size_t lds = (size_t)dmax * (dmax + 1) * sizeof(cd);
+  hipLaunchKernelGGL(gate_kernel, dim3(eng->F, n), dim3(64), lds, st, a, eng->dFnAll, dC, eng->dInitScmOff,
+                     eng->dScm0, eng->scmPerBin, dV);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(verdict, dV, n * sizeof(int), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  (void)hipFree(dC);
+  (void)hipFree(dV);
+  return 0;
+}
+
+int danse_engine_set_gate(danse_engine* eng, int32_t n, const int32_t* round, const int32_t* family,
+                          const int32_t* node, const int32_t* scene, const double* qY, const double* qN) {
+  if (!eng || n < 0) return fail(eng, "bad gate schedule");
+  HIPCHK(hipSetDevice(eng->dev));
+  if (eng->graphExec) {   // the captured run changes with the schedule
+    (void)hipGraphExecDestroy(eng->graphExec);
+    eng->graphExec = nullptr;
+  }
+  if (eng->dGateCand) (void)hipFree(eng->dGateCand);
+  if (eng->dGateVerdict) (void)hipFree(eng->dGateVerdict);
+  eng->dGateCand = nullptr;
+  eng->dGateVerdict = nullptr;
+  eng->nGate = 0;
+  eng->gateOff.assign(eng->R + 1, 0);
+  eng->gateDmax.assign(eng->R, 1);
+  if (n == 0) return 0;
+  std::vector<std::pair<int, GateCand>> v;
+  for (int i = 0; i < n; ++i) {
+    int fni = -1;
+    for (size_t x = 0; x < eng->fns.size(); ++x)
+      if (eng->fns[x].fam == family[i] && eng->fns[x].k == node[i]) fni = (int)x;
+    if (fni < 0 || scene[i] < 0 || scene[i] >= eng->S || round[i] < 0 || round[i] >= eng->R)
+      return fail(eng, "gate candidate not on this engine");
+    v.push_back({round[i], GateCand{fni, scene[i], qY[i], qN[i]}});
+  }
+  std::stable_sort(v.begin(), v.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+  std::vector<GateCand> h;
+  for (auto& x : v) {
+    h.push_back(x.second);
+    eng->gateOff[x.first + 1]++;
+    eng->gateDmax[x.first] = std::max(eng->gateDmax[x.first], eng->fns[x.second.fni].D);
+  }
+  for (int r = 0; r < eng->R; ++r) eng->gateOff[r + 1] += eng->gateOff[r];
+  eng->nGate = n;
+  HIPCHK(dalloc(&eng->dGateCand, (size_t)n));
+  HIPCHK(dalloc(&eng->dGateVerdict, (size_t)n));
+  HIPCHK(hipMemcpy(eng->dGateCand, h.data(), n * sizeof(GateCand), hipMemcpyHostToDevice));
+  return 0;
+}
+
+int danse_engine_gate_verdicts(danse_engine* eng, int32_t* verdict, void* stream) {
+  if (!eng || !verdict) return fail(eng, "null argument");
+  if (eng->nGate == 0) return 0;
+  HIPCHK(hipSetDevice(eng->dev));
+  HIPCHK(hipMemcpyAsync(verdict, eng->dGateVerdict, eng->nGate * sizeof(int), hipMemcpyDeviceToHost,
+                        (hipStream_t)stream));
+  HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  return 0;
+}
+
+int danse_engine_set_flags(danse_engine* eng, const uint8_t* flags, void* stream) {
+  if (!eng || !flags) return fail(eng, "null argument");
+  HIPCHK(hipSetDevice(eng->dev));
+  const size_t nb = (size_t)eng->R * eng->S * kMaxFam * eng->K;
+  HIPCHK(hipMemcpyAsync(eng->dFlags, flags, nb, hipMemcpyHostToDevice, (hipStream_t)stream));
+  HIPCHK(hipStreamSynchronize((hipStream_t)stream));
   return 0;
 }
 

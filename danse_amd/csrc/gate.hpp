@@ -1,0 +1,121 @@
+// The reference's start-of-updates gate (check_covariance_matrices,
+// danse_toolbox/d_classes.py:1430-1540): once the frame counters allow it,
+// a family-node starts updating only if, over ALL bins,
+//   GEVD: Rnn and Ryy are Hermitian (np.allclose(X^H, X): |X^H - X| <=
+//         1e-8 + 1e-5 |X| elementwise), eigvalsh >= 0 and full rank;
+//   MWF:  Rnn and Ryy are full rank.
+// Evaluated on the device for one round, on the SCMs as the reference holds
+// them after that round's recursion (the kernel applies the round's update
+// to a private copy; the update kernel then repeats it for real).
+//
+// Storage: the engine keeps the LOWER triangle (eigh reads it).  The
+// reference matrix is X = H + Q with Q anti-Hermitian; Q = q Q0, Q0 = (R0 -
+// R0^H) / 2 from the init slice R0, q = beta^m (m recursion steps since the
+// init, 0 after a first-frame SET) -- the recursion adds only Hermitian terms.
+// So conj(X_ji) - X_ij = -2 Q_ij, and X_ji = conj(X_ij - 2 Q_ij).
+//
+// eigvalsh >= 0 and the rank test become one float64 Cholesky of the
+// lower-triangle Hermitian matrix with every pivot above D eps trace(X) (the
+// matrix_rank tolerance sigma_max max(M, N) eps with sigma_max <= trace).
+// One (candidate, bin) per wavefront, the matrix in LDS, lane i owns row i.
+#pragma once
+#include "kernels.hpp"
+
+namespace danse {
+
+struct GateCand {
+  int fni;      // index into the engine's family-node table
+  int s;        // scene
+  double qY;    // beta^m of Ryy's init residue (0: a SET wiped it)
+  double qN;    // ... of Rnn's
+};
+
+__global__ void __launch_bounds__(64) gate_kernel(const UpdateArgs a, const FamNode* fns, const GateCand* cand,
+                                                 const long long* initOff, const cd* scm0, int perBin, int* verdict) {
+  extern __shared__ cd gX[];   // [D][D + 1]
+  const int li = threadIdx.x;
+  const int f = blockIdx.x;
+  const GateCand c = cand[blockIdx.y];
+  const FamNode d = fns[c.fni];
+  const int D = d.D, s = c.s, F = a.F;
+  const int P = D + 1;
+  const bool act = li < D;
+  const uint8_t fl = a.flags[(((long long)a.r * a.S + s) * kMaxFam + d.fam) * a.K + d.k];
+  __shared__ cf gy[64];
+  const cf y = load_y(a, d, s, f, li, act);
+  gy[li] = y;
+  __syncthreads();
+  const double beta = a.beta[s * a.K + d.k];
+  const cd* R0 = scm0 + initOff[c.fni] + (perBin ? (long long)f * D * D : 0ll);
+  bool pass = true;
+  for (int which = 0; which < 2; ++which) {   // 0: Ryy, 1: Rnn
+    const int op = which == 0 ? (fl & 3) : ((fl >> 2) & 3);
+    const double q = which == 0 ? c.qY : c.qN;
+    const double cy = (op == DANSE_OP_SET) ? 1.0 / D : (1.0 - beta) / D;
+    const double cx = (op == DANSE_OP_SET) ? 0.0 : beta;
+    bool herm = true;
+    double diag = 0.0;
+    if (act) {
+      const int i = li;
+      for (int j = 0; j <= i; ++j) {
+        long long e;
+        if (d.packed) e = (long long)s * a.scmStride + d.scmOff + (long long)(i * (i + 1) / 2 + j) * F + f;
+        else e = (long long)s * a.scmStride + d.scmOff + ((long long)f * D + i) * D + j;
+        cd x = which == 0 ? cdk(a.Ryy[e]) : a.Rnn[e];
+        if (i == j) x.im = 0.0;   // the stored diagonal is real; its init residue is Q_ii
+        if (op != DANSE_OP_KEEP) {
+          const cf yj = gy[j];
+          cd yy = cd{0.0, 0.0};
+          fma_cc(yy, cdk(y), cdk(yj));
+          x = cx * x;
+          x.re = fma(cy, yy.re, x.re);
+          x.im = fma(cy, (i == j) ? 0.0 : yy.im, x.im);
+        }
+        const cd r0ij = R0[i * D + j], r0ji = R0[j * D + i];
+        const cd Q = cd{0.5 * q * (r0ij.re - r0ji.re), 0.5 * q * (r0ij.im + r0ji.im)};   // q (R0 - R0^H)_ij / 2
+        if (i == j) {
+          const double qi = q * r0ij.im;   // X_ii = x.re + i qi
+          herm = herm && (2.0 * fabs(qi) <= 1e-8 + 1e-5 * sqrt(x.re * x.re + qi * qi));
+          diag = x.re;
+          gX[i * P + j] = cd{x.re, 0.0};
+        } else {
+          const double aq = 2.0 * sqrt(Q.re * Q.re + Q.im * Q.im);
+          const double xr = x.re, xi = x.im;                        // X_ij = H_ij + Q_ij (stored)
+          const double mr = xr - 2.0 * Q.re, mi = xi - 2.0 * Q.im;   // conj(X_ji) = X_ij - 2 Q_ij
+          herm = herm && (aq <= 1e-8 + 1e-5 * sqrt(xr * xr + xi * xi)) && (aq <= 1e-8 + 1e-5 * sqrt(mr * mr + mi * mi));
+          gX[i * P + j] = cd{xr, xi};
+        }
+      }
+    }
+    // GEVD: Hermitian over every entry of every bin
+    if (a.gevd && __ballot(act && !herm) != 0ull) pass = false;
+    // full rank (+ positive definite): float64 Cholesky of the lower triangle
+    double tr = diag;
+    for (int o = 32; o >= 1; o >>= 1) tr += __shfl_xor(tr, o);
+    const double tol = (double)D * 2.220446049250313e-16 * fabs(tr);
+    __syncthreads();
+    for (int j = 0; j < D; ++j) {
+      const double pj = gX[j * P + j].re;
+      if (!(pj > tol)) {
+        pass = false;
+        break;
+      }
+      const double inv = 1.0 / sqrt(pj);
+      if (li > j && li < D) {
+        const cd v = gX[li * P + j];
+        gX[li * P + j] = inv * v;
+      }
+      __syncthreads();
+      if (li > j && li < D) {
+        const cd lij = gX[li * P + j];
+        for (int k = j + 1; k <= li; ++k) fms_cc(gX[li * P + k], lij, gX[k * P + j]);
+      }
+      __syncthreads();
+    }
+    __syncthreads();
+    if (!pass) break;
+  }
+  if (li == 0 && !pass) atomicAnd(&verdict[blockIdx.y], 0);
+}
+
+}  // namespace danse

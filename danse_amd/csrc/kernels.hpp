@@ -36,6 +36,7 @@ struct FamNode {
   long long wOff;     // complex-element offset within one scene's w-history block
   long long wExtOff;  // DANSE only: offset within one scene's wExt-history block
   long long tgtOff;   // DANSE only: offset within one scene's target block
+  long long liOff;    // lane classes, GEVD: offset of the factor cache (Li, g) within one scene's block
 };
 
 struct UpdateArgs {
@@ -66,7 +67,25 @@ struct UpdateArgs {
   float alphaExt;
   int gevd, rank;
   int* diag;               // [S*K*kMaxFam]
+  cf* liCache;             // GEVD factor cache per family-node [NT + D][F] (Li = L^-1 packed, g = L^H e_ref)
+  long long liStride;      // per scene; null cache = always refactor
 };
+
+// The factor of Rnn cached by the last solve of this (scene, family-node) is
+// still the factor of the current Rnn: no Rnn update since that solve (the
+// flags of the rounds in between; Rnn changes only on VAD-inactive frames,
+// and the cached factor was taken after that round's own update).
+// Wave-uniform scan over at most kLiScan earlier rounds of the flag table.
+constexpr int kLiScan = 64;
+DANSE_DEV bool li_reusable(const UpdateArgs& a, const FamNode& d, int s, int opN) {
+  if (!a.liCache || opN != DANSE_OP_KEEP) return false;
+  for (int rr = a.r - 1; rr >= 0 && rr >= a.r - kLiScan; --rr) {
+    const uint8_t f2 = a.flags[(((long long)rr * a.S + s) * kMaxFam + d.fam) * a.K + d.k];
+    if ((f2 & DANSE_FLAG_SOLVE) && !(f2 & DANSE_FLAG_PREGIVEN)) return true;
+    if (((f2 >> 2) & 3) != DANSE_OP_KEEP) return false;
+  }
+  return false;
+}
 
 // Observation vector entry of lane li (channel chanList[chanOff + li]) for
 // bin f: a local spectrum, or the fused spectrum of sender q (the frame of

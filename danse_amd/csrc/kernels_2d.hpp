@@ -41,6 +41,10 @@ update_kernel_2d(const UpdateArgs a) {
   const bool pregiven = (fl & DANSE_FLAG_PREGIVEN) != 0;
   const bool solve = (fl & DANSE_FLAG_SOLVE) != 0 && !pregiven;
   const bool initslot = (fl & DANSE_FLAG_INITSLOT) != 0;
+  // factor cache (kernels.hpp li_reusable): per bin the float32 Li blocks in
+  // lane order [NB * NB][64] and g [64]
+  const bool reuse = solve && li_reusable(a, d, s, opN);
+  cf* liC = a.liCache ? a.liCache + (long long)s * a.liStride + d.liOff + (long long)f * (64 * NB * NB + 64) : nullptr;
 
   const cf y = load_y(a, d, s, f, li, act);
   S.vb[li] = y;
@@ -58,7 +62,7 @@ update_kernel_2d(const UpdateArgs a) {
   // ---- Rnn (float64): recursion, store, factor --------------------------
   Blk<NB> Lf;
   bool ok = true;
-  if (opN || solve) {
+  if (opN || (solve && !reuse)) {
     BlkD<NB> M;
     const double cy = (opN == DANSE_OP_SET) ? 1.0 / D : (1.0 - beta) / D;
     const double cx = (opN == DANSE_OP_SET) ? 0.0 : beta;
@@ -80,7 +84,28 @@ update_kernel_2d(const UpdateArgs a) {
         M.v[sb][tb] = x;
       });
     });
-    if (solve) ok = gevd2d_factor<NB>(M, Lf, S, li, D, d.ref);
+    if (solve && !reuse) {
+      ok = gevd2d_factor<NB>(M, Lf, S, li, D, d.ref);
+      if (liC) {
+        sfor<0, NB>([&](auto sc) {
+          sfor<0, NB>([&](auto tc) {
+            constexpr int sb = decltype(sc)::value, tb = decltype(tc)::value;
+            liC[(sb * NB + tb) * 64 + li] = Lf.v[sb][tb];
+          });
+        });
+        liC[64 * NB * NB + li] = S.g[li];
+      }
+    }
+  }
+  if (reuse) {
+    sfor<0, NB>([&](auto sc) {
+      sfor<0, NB>([&](auto tc) {
+        constexpr int sb = decltype(sc)::value, tb = decltype(tc)::value;
+        Lf.v[sb][tb] = liC[(sb * NB + tb) * 64 + li];
+      });
+    });
+    S.g[li] = liC[64 * NB * NB + li];
+    t2d::wsync();
   }
 
   // ---- Ryy (float32): recursion, store, filter ---------------------------

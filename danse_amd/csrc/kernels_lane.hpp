@@ -51,6 +51,10 @@ __global__ void __launch_bounds__(64) update_kernel_lane(const UpdateArgs a) {
   const uint8_t fl = a.flags[(((long long)r * a.S + s) * kMaxFam + d.fam) * a.K + d.k];
   const int opY = fl & 3, opN = (fl >> 2) & 3;
   const bool solve = (fl & DANSE_FLAG_SOLVE) != 0 && (fl & DANSE_FLAG_PREGIVEN) == 0;
+  // GEVD: reuse the cached float32 Li / g when Rnn has not changed since the
+  // last factorisation (skips the float64 load, Cholesky and inverse)
+  const bool reuse = GEVD && solve && li_reusable(a, d, s, opN);
+  cf* liC = a.liCache ? a.liCache + (long long)s * a.liStride + d.liOff + f : nullptr;
   __shared__ cf Ls[NT][64];
   __shared__ cf Gs[D][64];
 
@@ -82,7 +86,7 @@ __global__ void __launch_bounds__(64) update_kernel_lane(const UpdateArgs a) {
   }
   asm volatile("" ::: "memory");   // the Ryy work above is done before the float64 triangle loads
   PTriD<D> N;
-  if (opN || solve) {
+  if (opN || (solve && !reuse)) {
     sfor<0, NT>([&](auto ec) { N.a[decltype(ec)::value] = a.Rnn[base + (long long)decltype(ec)::value * F]; });
     sfor<0, D>([&](auto ic) { N.a[P(decltype(ic)::value, decltype(ic)::value)].im = 0.0; });
   }
@@ -109,14 +113,27 @@ __global__ void __launch_bounds__(64) update_kernel_lane(const UpdateArgs a) {
   bool ok = true;
   if (solve) {
   if constexpr (GEVD) {
-    // float64 Cholesky + inverse of Rnn; hand-over in float32
-    double invd[D];
-    ok = chol64<D>(N, invd);
-    cf g[D];
-    ref_row<D>(N, d.ref, g);
-    tri_inv64<D>(N, invd);
-    store_tri<D>(N, Ls, threadIdx.x);
-    sfor<0, D>([&](auto ic) { Gs[decltype(ic)::value][threadIdx.x] = g[decltype(ic)::value]; });
+    if (reuse) {
+      sfor<0, NT>([&](auto ec) { Ls[decltype(ec)::value][threadIdx.x] = liC[(long long)decltype(ec)::value * F]; });
+      sfor<0, D>([&](auto ic) { Gs[decltype(ic)::value][threadIdx.x] = liC[(long long)(NT + decltype(ic)::value) * F]; });
+    } else {
+      // float64 Cholesky + inverse of Rnn; hand-over in float32 (LDS, and
+      // the factor cache for later solves on the same Rnn)
+      double invd[D];
+      ok = chol64<D>(N, invd);
+      {
+        cf g[D];   // out of the registers before the inverse
+        ref_row<D>(N, d.ref, g);
+        sfor<0, D>([&](auto ic) { Gs[decltype(ic)::value][threadIdx.x] = g[decltype(ic)::value]; });
+        if (liC && valid) sfor<0, D>([&](auto ic) { liC[(long long)(NT + decltype(ic)::value) * F] = g[decltype(ic)::value]; });
+      }
+      asm volatile("" ::: "memory");
+      tri_inv64<D>(N, invd);
+      store_tri<D>(N, Ls, threadIdx.x);
+      if (liC && valid) {
+        sfor<0, NT>([&](auto ec) { liC[(long long)decltype(ec)::value * F] = cfk(N.a[decltype(ec)::value]); });
+      }
+    }
   } else {
     // MWF, float64 throughout: w = Ryy^-1 (Ryy - Rnn) e_ref
     cd ncol[D];

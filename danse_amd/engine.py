@@ -200,6 +200,9 @@ class DanseEngine:
                     raise ValueError('GEVD rank larger than a filter dimension')
         self.pregiven = pregiven
         self._ran = False
+        self._gateMoved = False
+        self._gateSpecFailed = False
+        self._gateInstalled = None
         self._build_flags()
         self._build_cfg()
         # inputs [S][Mtot][T] float32 on the device
@@ -261,9 +264,36 @@ class DanseEngine:
                 phi[nb] -= est * self.Ns
         self._zPhase = ph
 
+    def _flags_for(self, s, f, k, start):
+        """Control bytes of one (scene, family, node) for a start round
+        (-1: not started within the run); records startRound / nSolves."""
+        p, R = self.p, self.R
+        g = self._gateState[(s, f, k)]
+        started = np.zeros(R, dtype=bool)
+        if start >= 0:
+            started[start:] = True
+        self.startRound[s, f, k] = start
+        solve = started & g['doSolve']
+        # not yet started: perform_update leaves the init slot
+        # wTilde[:, i + 1] in place (d_classes.py:2290-2362); it
+        # differs from w[i] only for random init (flag INITSLOT)
+        initslot = (~started) & g['doSolve'] & (p.filterInitType == 'random')
+        if p.bypassUpdates:
+            solve[:] = False
+            initslot[:] = False
+        self.nSolves[s, f, k] = int(solve.sum())
+        b = g['opY'].astype(np.uint8) | (g['opN'].astype(np.uint8) << 2) | (solve.astype(np.uint8) * L.FLAG_SOLVE)
+        b = b | (initslot.astype(np.uint8) * L.FLAG_INITSLOT)
+        if g['extT'] is not None:
+            b = b | (g['extT'].astype(np.uint8) * L.FLAG_EXT_TARGET)
+        if self.pregiven is not None:
+            b = np.full(R, L.FLAG_PREGIVEN, dtype=np.uint8)
+        return b
+
     def _build_flags(self):
         p, S, K, R = self.p, self.S, self.K, self.R
         fl = np.zeros((R, S, 4, K), dtype=np.uint8)
+        self._gateState = {}
         self.startRound = np.full((S, 4, K), -1, dtype=np.int64)
         self.nSolves = np.zeros((S, 4, K), dtype=np.int64)
         vad = np.zeros((S, K, R), dtype=bool)
@@ -301,26 +331,12 @@ class DanseEngine:
                     else:
                         opY = np.where(v, L.OP_AVG, L.OP_KEEP)
                         opN = np.where(~v, L.OP_AVG, L.OP_KEEP)
-                    gate = (ny > D) & (nn > D) & tOK[:, k]
-                    started = np.maximum.accumulate(gate)
-                    if started.any():
-                        self.startRound[s, f, k] = int(np.argmax(started))
-                    solve = started & doSolve[k]
-                    # not yet started: perform_update leaves the init slot
-                    # wTilde[:, i + 1] in place (d_classes.py:2290-2362); it
-                    # differs from w[i] only for random init (flag INITSLOT)
-                    initslot = (~started) & doSolve[k] & (p.filterInitType == 'random')
-                    if p.bypassUpdates:
-                        solve[:] = False
-                        initslot[:] = False
-                    self.nSolves[s, f, k] = int(solve.sum())
-                    b = opY.astype(np.uint8) | (opN.astype(np.uint8) << 2) | (solve.astype(np.uint8) * L.FLAG_SOLVE)
-                    b = b | (initslot.astype(np.uint8) * L.FLAG_INITSLOT)
-                    if f == L.FAM_DANSE:
-                        b = b | (extT[:, k].astype(np.uint8) * L.FLAG_EXT_TARGET)
-                    if self.pregiven is not None:
-                        b = np.full(R, L.FLAG_PREGIVEN, dtype=np.uint8)
-                    fl[:, s, f, k] = b
+                    elig = (ny > D) & (nn > D) & tOK[:, k]
+                    self._gateState[(s, f, k)] = dict(elig=elig, opY=opY, opN=opN, doSolve=doSolve[k],
+                                                      extT=extT[:, k] if f == L.FAM_DANSE else None)
+                    # compiled assuming the reference gate passes at the first
+                    # round the counters allow (run() checks it on the device)
+                    fl[:, s, f, k] = self._flags_for(s, f, k, int(np.argmax(elig)) if elig.any() else -1)
         self.flags = fl
 
     def _winit(self, f, k):
@@ -438,12 +454,153 @@ class DanseEngine:
         st = stream if stream is not None else t.cuda.current_stream(self.device)
         return ctypes.c_void_p(st.cuda_stream)
 
-    def run(self, graph=True, stream=None):
+    def run(self, graph=True, stream=None, gate=True):
+        """The whole run.  ``gate``: the reference's start gate (Hermitian /
+        positive definite / full rank over every bin, ``check_covariance_
+        matrices``, ``d_classes.py:1430-1540``) is evaluated on the device at
+        each family-node's first counter-eligible round.  Speculatively first:
+        the checks run inside the (graph-captured) run, whose solve flags
+        assume every check passes, and the verdicts are read back once; if
+        one failed, the run is repeated exactly with the host loop
+        (``_run_gated``: un-graphed up to the last decision, the start and
+        the solve flags moved to the first round that passes)."""
         if self._ran:
             self._load_init_history()   # the solves of the previous run overwrote init slots
+            self._reset_gate()
         self._ran = True
-        L.check(self.lib.danse_engine_run(self.eng, 0, self.R, self.stream_ptr(stream), int(bool(graph))), self.eng)
+        st = self.stream_ptr(stream)
+        gating = gate and self.pregiven is None and not self.p.bypassUpdates
+        if gating and not self._gateSpecFailed:
+            n = self._install_gate()
+            L.check(self.lib.danse_engine_run(self.eng, 0, self.R, st, int(bool(graph))), self.eng)
+            if n == 0:
+                return self
+            ver = np.zeros(n, dtype=np.int32)
+            L.check(self.lib.danse_engine_gate_verdicts(self.eng, _ptr(ver, ctypes.c_int32), st), self.eng)
+            if np.all(ver != 0):
+                return self
+            # a start is delayed: repeat the run exactly on the host loop
+            self._gateSpecFailed = True
+            L.check(self.lib.danse_engine_reset(self.eng, st), self.eng)
+            self._load_init_history()
+        if gating:
+            self._uninstall_gate()
+            r0 = self._run_gated(st)
+        else:
+            r0 = 0
+        if r0 < self.R:
+            L.check(self.lib.danse_engine_run(self.eng, r0, self.R, st, int(bool(graph))), self.eng)
+        else:
+            L.check(self.lib.danse_engine_finish(self.eng, st), self.eng)
         return self
+
+    def _gate_candidates(self):
+        """(round, (s, f, k)) of every owned family-node's first counter-eligible round."""
+        out = []
+        for key, g in self._gateState.items():
+            if key[2] < self.k0 or key[2] >= self.k1:
+                continue
+            e = np.flatnonzero(g['elig'])
+            if e.size:
+                out.append((int(e[0]), key))
+        return out
+
+    def _install_gate(self):
+        if self._gateInstalled is not None:
+            return self._gateInstalled
+        cands = self._gate_candidates()
+        n = len(cands)
+        rnd = np.array([c[0] for c in cands], dtype=np.int32)
+        scn = np.array([c[1][0] for c in cands], dtype=np.int32)
+        fam = np.array([c[1][1] for c in cands], dtype=np.int32)
+        node = np.array([c[1][2] for c in cands], dtype=np.int32)
+        qY = np.array([self._gate_q(s, k, self._gateState[(s, f, k)]['opY'], r) for r, (s, f, k) in cands])
+        qN = np.array([self._gate_q(s, k, self._gateState[(s, f, k)]['opN'], r) for r, (s, f, k) in cands])
+        L.check(self.lib.danse_engine_set_gate(self.eng, n, _ptr(rnd, ctypes.c_int32), _ptr(fam, ctypes.c_int32),
+                                               _ptr(node, ctypes.c_int32), _ptr(scn, ctypes.c_int32),
+                                               _ptr(qY, ctypes.c_double), _ptr(qN, ctypes.c_double)), self.eng)
+        self._gateInstalled = n
+        return n
+
+    def _uninstall_gate(self):
+        if self._gateInstalled:
+            z = np.zeros(1, dtype=np.int32)
+            d = np.zeros(1)
+            L.check(self.lib.danse_engine_set_gate(self.eng, 0, _ptr(z, ctypes.c_int32), _ptr(z, ctypes.c_int32),
+                                                   _ptr(z, ctypes.c_int32), _ptr(z, ctypes.c_int32),
+                                                   _ptr(d, ctypes.c_double), _ptr(d, ctypes.c_double)), self.eng)
+        self._gateInstalled = None
+
+    def _reset_gate(self):
+        if not self._gateMoved:
+            return
+        self._gateMoved = False
+        fl = self.flags
+        for (s, f, k), g in self._gateState.items():
+            fl[:, s, f, k] = self._flags_for(s, f, k, int(np.argmax(g['elig'])) if g['elig'].any() else -1)
+        self._flags = np.ascontiguousarray(fl)
+        L.check(self.lib.danse_engine_set_flags(self.eng, _ptr(self._flags, ctypes.c_uint8), None), self.eng)
+
+    def _gate_q(self, s, k, ops, r):
+        """beta^m of the init slice's anti-Hermitian residue after round r
+        (0 once a first-frame SET replaced the init)."""
+        o = ops[:r + 1]
+        if np.any(o == L.OP_SET):
+            return 0.0
+        return float(self._beta[s, k]) ** int(np.sum(o == L.OP_AVG))
+
+    def _run_gated(self, st):
+        R = self.R
+        pending = {}
+        for key, g in self._gateState.items():
+            if key[2] < self.k0 or key[2] >= self.k1:
+                continue
+            e = np.flatnonzero(g['elig'])
+            if e.size:
+                pending[key] = int(e[0])
+        r0 = 0
+        while pending:
+            rc = min(pending.values())
+            if rc > r0:
+                L.check(self.lib.danse_engine_run(self.eng, r0, rc, st, 0), self.eng)
+            L.check(self.lib.danse_engine_bcast(self.eng, rc, st), self.eng)
+            cands = sorted(key for key, r in pending.items() if r == rc)
+            fam = np.array([c[1] for c in cands], dtype=np.int32)
+            node = np.array([c[2] for c in cands], dtype=np.int32)
+            scn = np.array([c[0] for c in cands], dtype=np.int32)
+            qY = np.array([self._gate_q(c[0], c[2], self._gateState[c]['opY'], rc) for c in cands])
+            qN = np.array([self._gate_q(c[0], c[2], self._gateState[c]['opN'], rc) for c in cands])
+            ver = np.zeros(len(cands), dtype=np.int32)
+            L.check(self.lib.danse_engine_gate(self.eng, rc, len(cands), _ptr(fam, ctypes.c_int32),
+                                               _ptr(node, ctypes.c_int32), _ptr(scn, ctypes.c_int32),
+                                               _ptr(qY, ctypes.c_double), _ptr(qN, ctypes.c_double),
+                                               _ptr(ver, ctypes.c_int32), st), self.eng)
+            changed = False
+            for c, v in zip(cands, ver):
+                s, f, k = c
+                if v:
+                    del pending[c]
+                    if self.startRound[s, f, k] != rc:
+                        self.flags[:, s, f, k] = self._flags_for(s, f, k, rc)
+                        changed = True
+                else:
+                    nxt = np.flatnonzero(self._gateState[c]['elig'][rc + 1:])
+                    if nxt.size:
+                        pending[c] = rc + 1 + int(nxt[0])
+                    else:
+                        del pending[c]
+                    if self.startRound[s, f, k] != -1:
+                        self.flags[:, s, f, k] = self._flags_for(s, f, k, -1)
+                        changed = True
+            if changed:
+                self._gateMoved = True
+                self._flags = np.ascontiguousarray(self.flags)
+                L.check(self.lib.danse_engine_set_flags(self.eng, _ptr(self._flags, ctypes.c_uint8), st), self.eng)
+            L.check(self.lib.danse_engine_update(self.eng, rc, st), self.eng)
+            r0 = rc + 1
+            if r0 >= R:
+                break
+        return r0
 
     def bcast(self, r, stream=None):
         L.check(self.lib.danse_engine_bcast(self.eng, r, self.stream_ptr(stream)), self.eng)

@@ -186,6 +186,27 @@ int danse_engine_finish(danse_engine* eng, void* stream);   /* synthesis of the 
  * node range is one contiguous block); an update may read slot (r-1) & 1
  * (zLag). */
 int danse_engine_zspec(danse_engine* eng, void** ptr, size_t* bytes);
+/* The reference's start-of-updates gate (check_covariance_matrices,
+ * d_classes.py:1430-1540) for n candidate (family, node, scene) triples at
+ * round r, after danse_engine_bcast(r) and before danse_engine_update(r):
+ * Hermitian (GEVD), positive definite and full rank over every bin, on the
+ * SCMs after round r's recursion.  qY / qN: beta^m of the init slice's
+ * anti-Hermitian residue in Ryy / Rnn (0 after a first-frame SET).
+ * verdict[i] = 1 pass / 0 fail.  Synchronous (the host decides the flags).  */
+int danse_engine_gate(danse_engine* eng, int32_t r, int32_t n, const int32_t* family, const int32_t* node,
+                      const int32_t* scene, const double* qY, const double* qN, int32_t* verdict, void* stream);
+/* Replace the round control table (same layout as danse_cfg.flags); the host
+ * re-derives the solve flags when the gate delays a node's start.        */
+int danse_engine_set_flags(danse_engine* eng, const uint8_t* flags, void* stream);
+/* Speculative form of the gate for graph-captured runs: the n candidates
+ * (round, family, node, scene, qY, qN) are checked inside danse_engine_run
+ * (between bcast and update of their round) while the run proceeds on the
+ * flags compiled for "every gate passes"; danse_engine_gate_verdicts
+ * (synchronous) returns the verdicts in the order given, sorted stably by
+ * round.  If one failed, the host re-runs with danse_engine_gate.          */
+int danse_engine_set_gate(danse_engine* eng, int32_t n, const int32_t* round, const int32_t* family,
+                          const int32_t* node, const int32_t* scene, const double* qY, const double* qN);
+int danse_engine_gate_verdicts(danse_engine* eng, int32_t* verdict, void* stream);
 /* Use a caller-owned buffer (same size and layout) for the fused spectra,
  * e.g. a torch tensor that an RCCL all-gather fills in place. */
 int danse_engine_set_zspec(danse_engine* eng, void* ptr);

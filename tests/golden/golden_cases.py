@@ -54,6 +54,13 @@ ONLINE_CASES = [
                   covMatSameInitForAllFreqs=False,
                   covMatSameInitForAllNodes=False, use1stFrameAsBasis=False, computeLocal=True,
                   computeCentralised=True)),
+    # the reference gate delays the start (check_covariance_matrices,
+    # d_classes.py:1430-1540): a 1e-6 non-Hermitian init residue decays with
+    # beta^m until np.allclose(X^H, X) holds -- nodes start at iterations 29,
+    # 28 and 54 although the frame counters allow 26
+    dict(name='online_gate_delay_asy', M=[2, 2, 2], dur=3.0, seed=14,
+         danse=_d(BATTERY, nodeUpdating='asy', covMatInitType='eye_and_random', covMatRandomInitScaling=1e-6,
+                  use1stFrameAsBasis=False, t_expAvg50p=0.1)),
     # config C shape (fewer nodes): SROs, Oracle SRO estimates, phase compensation with
     # full-sample-drift flags (d_classes.py:1936-2046, 2364-2621; quirks Q3, Q5, Q13)
     dict(name='online_C_sro_comp_asy', M=[2, 3, 2], dur=3.0, seed=8, sros=[0, 100, 200],
