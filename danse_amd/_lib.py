@@ -42,6 +42,8 @@ class DanseCfg(ctypes.Structure):
         ('keepHistory', _c_i32),
         ('zLag', _p_u8), ('zPhase', ctypes.POINTER(ctypes.c_double)),
         ('fsTab', _p_i32), ('zStreamLen', _c_i32), ('scmInitPerBin', _c_i32),
+        ('cohDrift', _c_i32), ('cdSegLength', _c_i32), ('cdStart', _c_i32), ('cdEvery', _c_i32),
+        ('cdCompensate', _c_i32), ('cdNIter', _c_i32), ('cdAlpha', ctypes.c_double), ('cdAlphaEps', ctypes.c_double),
     ]
 
 
@@ -81,6 +83,8 @@ SIGNATURES = {
     'danse_engine_set_gate': (_c_i32, [ctypes.c_void_p, _c_i32, _p_i32, _p_i32, _p_i32, _p_i32,
                                        ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
     'danse_engine_gate_verdicts': (_c_i32, [ctypes.c_void_p, _p_i32, ctypes.c_void_p]),
+    'danse_engine_sro_estimates': (_c_i32, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
+                                            ctypes.POINTER(ctypes.c_double)]),
     'danse_engine_get': (_c_i32, [ctypes.c_void_p, _c_i32, _c_i32, _c_i32, ctypes.c_void_p, ctypes.c_size_t,
                                   ctypes.c_void_p]),
     'danse_engine_put': (_c_i32, [ctypes.c_void_p, _c_i32, _c_i32, _c_i32, ctypes.c_void_p, ctypes.c_size_t,

@@ -12,6 +12,7 @@
 #include "bcast.hpp"
 #include "classes.hpp"
 #include "gate.hpp"
+#include "cohdrift.hpp"
 #include "tzconv.hpp"
 
 using namespace danse;
@@ -80,6 +81,11 @@ struct danse_engine {
   std::vector<int> gateOff;
   std::vector<int> gateDmax;   // per round: largest candidate D (LDS size)
   int nGate = 0;
+  // CohDrift (cohdrift.hpp)
+  int cohDrift = 0, cdLd = 0, cdStart = 0, cdEvery = 1, cdComp = 0, cdNIter = 0;
+  double cdAlpha = 0.0, cdAlphaEps = 0.0;
+  cd *cdRing = nullptr, *cdAvg = nullptr;
+  double *cdPhase = nullptr, *cdEst = nullptr, *cdRes = nullptr;
   long long liStride = 0;
   int scmPerBin = 0;   // dScm0 holds [F][D][D] per family-node (else [D][D])
   FamNode* dFnAll = nullptr;
@@ -237,6 +243,11 @@ int danse_engine_reset(danse_engine* eng, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   const int S = eng->S, K = eng->K, F = eng->F, R = eng->R;
   HIPCHK(hipMemsetAsync(eng->zPrev, 0, (size_t)S * K * eng->N * sizeof(float), st));
+  if (eng->cohDrift) {
+    HIPCHK(hipMemsetAsync(eng->cdPhase, 0, (size_t)S * K * K * sizeof(double), st));
+    HIPCHK(hipMemsetAsync(eng->cdEst, 0, (size_t)S * K * (K - 1) * R * sizeof(double), st));
+    HIPCHK(hipMemsetAsync(eng->cdRes, 0, (size_t)S * K * (K - 1) * R * sizeof(double), st));
+  }
   HIPCHK(hipMemsetAsync(eng->Zspec, 0, (size_t)2 * K * S * F * sizeof(cf), st));
   HIPCHK(hipMemsetAsync(eng->zStream, 0, (size_t)S * K * eng->zLen * sizeof(float), st));
   if (eng->wIR) {
@@ -467,6 +478,18 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
   HIPCHK(dalloc(&eng->d, (size_t)kMaxFam * S * K * c->T));
   HIPCHK(dalloc(&eng->diag, (size_t)S * K * kMaxFam));
   if (eng->liStride > 0) HIPCHK(dalloc(&eng->liCache, (size_t)S * eng->liStride));
+  if (c->cohDrift) {
+    if (c->cdSegLength < 1 || c->cdEvery < 1 || c->cdStart < c->cdSegLength) return fail(eng, "bad CohDrift parameters");
+    eng->cohDrift = 1;
+    eng->cdLd = c->cdSegLength; eng->cdStart = c->cdStart; eng->cdEvery = c->cdEvery; eng->cdComp = c->cdCompensate;
+    eng->cdNIter = c->cdNIter; eng->cdAlpha = c->cdAlpha; eng->cdAlphaEps = c->cdAlphaEps;
+    const size_t nq = (size_t)S * K * (K - 1);
+    HIPCHK(dalloc(&eng->cdRing, (size_t)(c->cdSegLength + 1) * nq * F));
+    HIPCHK(dalloc(&eng->cdAvg, nq * F));
+    HIPCHK(dalloc(&eng->cdPhase, (size_t)S * K * K));
+    HIPCHK(dalloc(&eng->cdEst, nq * R));
+    HIPCHK(dalloc(&eng->cdRes, nq * R));
+  }
   HIPCHK(hipMemset(eng->Yspec, 0, 2 * S * MT * F * sizeof(cf)));
   HIPCHK(hipMemset(eng->Zspec, 0, (size_t)2 * K * S * F * sizeof(cf)));
   HIPCHK(hipMemset(eng->zPrev, 0, (size_t)S * K * c->N * sizeof(float)));
@@ -561,7 +584,8 @@ void danse_engine_destroy(danse_engine* eng) {
                   eng->Rnn, eng->wHist, eng->wExtHist, eng->wExtTarget, eng->dhat, eng->zPrev, eng->zStream, eng->d,
                   eng->diag, eng->dW0, eng->dScm0, eng->dExt0, eng->dTgt0, eng->dFnAll, eng->dInitW0Off,
                   eng->dInitScmOff, eng->dExtSrcOff, eng->dTgtOff, eng->dFsTab, eng->wIR, eng->dSn, eng->liCache,
-                  eng->dGateCand, eng->dGateVerdict};
+                  eng->dGateCand, eng->dGateVerdict, eng->cdRing, eng->cdAvg, eng->cdPhase, eng->cdEst,
+                  eng->cdRes};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (auto& cl : eng->classes) {
@@ -603,6 +627,7 @@ static UpdateArgs make_update(danse_engine* e, int r) {
   a.wExtTarget = e->wExtTarget; a.tgtStride = e->tgtStride; a.dhat = e->dhat; a.beta = e->dBeta;
   a.betaExt = e->dBetaExt; a.alphaExt = e->alphaExt; a.gevd = e->gevd; a.rank = e->rank; a.diag = e->diag;
   a.liCache = e->liCache; a.liStride = e->liStride;
+  a.cdPhase = e->cdPhase;
   return a;
 }
 
@@ -613,6 +638,14 @@ static void launch_update(danse_engine* e, int r, hipStream_t st) {
     a.fn = cl.dev;
     a.famNodeId = cl.devIds;
     launch_update_class(cl.DMAX, a, st);   // D > kMaxDMax rejected at create time
+  }
+  if (e->cohDrift) {
+    CohDriftArgs c{};
+    c.S = e->S; c.K = e->K; c.MT = e->MT; c.F = e->F; c.r = r; c.ld = e->cdLd; c.start = e->cdStart;
+    c.every = e->cdEvery; c.nIter = e->cdNIter; c.compensate = e->cdComp; c.alpha = e->cdAlpha;
+    c.alphaEps = e->cdAlphaEps; c.Ns = (double)e->Ns; c.base = e->dBase; c.ring = e->cdRing; c.avgTail = e->cdAvg;
+    c.phase = e->cdPhase; c.est = e->cdEst; c.res = e->cdRes; c.R = e->R;
+    hipLaunchKernelGGL(cohdrift_kernel, dim3(e->S * e->K * (e->K - 1)), dim3(kCdThreads), 0, st, make_update(e, r), c);
   }
 }
 
@@ -817,6 +850,21 @@ int danse_engine_gate_verdicts(danse_engine* eng, int32_t* verdict, void* stream
   HIPCHK(hipMemcpyAsync(verdict, eng->dGateVerdict, eng->nGate * sizeof(int), hipMemcpyDeviceToHost,
                         (hipStream_t)stream));
   HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  return 0;
+}
+
+int danse_engine_sro_estimates(danse_engine* eng, double* est, double* res) {
+  if (!eng || !est || !res) return fail(eng, "null argument");
+  const size_t n = (size_t)eng->S * eng->K * eng->R * (eng->K - 1);
+  if (!eng->cohDrift) {
+    std::fill(est, est + n, 0.0);
+    std::fill(res, res + n, 0.0);
+    return 0;
+  }
+  HIPCHK(hipSetDevice(eng->dev));
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(est, eng->cdEst, n * sizeof(double), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(res, eng->cdRes, n * sizeof(double), hipMemcpyDeviceToHost));
   return 0;
 }
 

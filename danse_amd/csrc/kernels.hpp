@@ -68,6 +68,7 @@ struct UpdateArgs {
   int gevd, rank;
   int* diag;               // [S*K*kMaxFam]
   cf* liCache;             // GEVD factor cache per family-node [NT + D][F] (Li = L^-1 packed, g = L^H e_ref)
+  const double* cdPhase;   // CohDrift phase accumulator [S][K][K] (adds to zPhase), or null
   long long liStride;      // per scene; null cache = always refactor
 };
 
@@ -103,7 +104,9 @@ DANSE_DEV cf load_y(const UpdateArgs& a, const FamNode& d, int s, int f, int li,
     const int lag = a.zLag ? a.zLag[lk] : 0;
     v = a.Zspec[((((long long)((r - lag) & 1)) * a.K + q) * a.S + s) * F + f];
     if (a.zPhase) {
-      double t = (double)f * a.zPhase[lk] / (double)(2 * (F - 1));
+      double ph = a.zPhase[lk];
+      if (a.cdPhase) ph += a.cdPhase[((long long)s * a.K + d.k) * a.K + q];
+      double t = (double)f * ph / (double)(2 * (F - 1));
       t -= rint(t);
       float sn, cs;
       sincospif(-2.0f * (float)t, &sn, &cs);

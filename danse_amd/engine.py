@@ -244,10 +244,17 @@ class DanseEngine:
         self._zLag = (None if self.rt.synchronous or self.fewSamples
                       else np.ascontiguousarray(self.rt.zLag[:R], dtype=np.uint8))
         self._zPhase = None
+        self.cohDrift = p.estimateSROs == 'CohDrift'
+        if self.cohDrift:
+            cd = p.cohDrift
+            if cd.loop != 'closed' or cd.estimationMethod != 'ls':
+                raise NotImplementedError("CohDrift on the device path: closed loop, estimationMethod 'ls'")
+            if 'asy' not in p.nodeUpdating or self.fewSamples or p.computeCentralised:
+                raise NotImplementedError('CohDrift on the device path: asy node updating, wholeChunk, no centralised')
+        elif p.estimateSROs != 'Oracle':
+            raise NotImplementedError(f'estimateSROs={p.estimateSROs!r} (the reference raises for DXCP-PhaT in DANSE)')
         if not p.compensateSROs:
             return
-        if p.estimateSROs != 'Oracle':
-            raise NotImplementedError(f'estimateSROs={p.estimateSROs!r} on the device path (Oracle only)')
         sro = np.array([nd.sro for nd in sc0.wasn], dtype=np.float64)
         for sc in self.scenes:
             if not np.array_equal(np.array([nd.sro for nd in sc.wasn], dtype=np.float64), sro):
@@ -256,7 +263,9 @@ class DanseEngine:
         for k in range(K):
             phi = np.zeros(K, dtype=np.float64)
             nb = [q for q in range(K) if q != k]
-            est = (sro[nb] - sro[k]) * 1e-6
+            # CohDrift: the estimates accumulate on the device (cohdrift.hpp);
+            # the table keeps the full-sample-drift flags only
+            est = np.zeros(len(nb)) if self.cohDrift else (sro[nb] - sro[k]) * 1e-6
             for r in range(R):
                 if p.includeFSDflags:
                     phi[nb] += self.rt.flags[r, k, nb]
@@ -415,6 +424,13 @@ class DanseEngine:
         self._fsTab = np.ascontiguousarray(self.rt.fsTab, dtype=np.int32) if self.fewSamples else None
         c.fsTab = _ptr(self._fsTab, ctypes.c_int32)
         c.scmInitPerBin = 0 if p.covMatSameInitForAllFreqs else 1
+        if self.cohDrift:
+            cd = p.cohDrift
+            c.cohDrift, c.cdSegLength, c.cdEvery = 1, int(cd.segLength), int(cd.estEvery)
+            c.cdStart = int(cd.startAfterNups + cd.estEvery)
+            c.cdCompensate = int(bool(p.compensateSROs))
+            c.cdNIter = int(self.nIter)
+            c.cdAlpha, c.cdAlphaEps = float(cd.alpha), float(cd.alphaEps)
         c.zStreamLen = int(self.rt.zStreamLen) if self.fewSamples else 0
         self.zLen = c.zStreamLen if self.fewSamples else self.R * self.Ns
         self._cfg = c
@@ -689,6 +705,11 @@ class DanseEngine:
         Yh = Yh[..., 0].astype(np.float64) + 1j * Yh[..., 1].astype(np.float64)
         solveFlags = (self.flags[:, :, L.FAM_DANSE, :] & L.FLAG_SOLVE) != 0     # [R][S][K]
         neighbors0 = [list(n.neighborsIdx) for n in self.scenes[0].wasn]
+        if self.cohDrift:
+            cdE = np.zeros((S, K, self.R, K - 1))
+            cdR = np.zeros((S, K, self.R, K - 1))
+            L.check(self.lib.danse_engine_sro_estimates(self.eng, _ptr(cdE, ctypes.c_double),
+                                                        _ptr(cdR, ctypes.c_double)), self.eng)
         for s in range(S):
             r = res[s]
             kr = p.referenceSensor
@@ -698,6 +719,12 @@ class DanseEngine:
             for nm, v in host_fields(p, [n.sro for n in self.scenes[s].wasn], neighbors0, self.rt, nI, nseg,
                                      fsr).items():
                 setattr(r, nm, v)
+            if self.cohDrift:
+                r.SROsEstimates = [np.zeros((nI, K - 1)) for _ in range(K)]
+                r.SROsResiduals = [np.zeros((nI, K - 1)) for _ in range(K)]
+                for k in range(K):
+                    r.SROsEstimates[k][:self.R] = cdE[s, k]
+                    r.SROsResiduals[k][:self.R] = cdR[s, k]
             r.yCentrBatch = Yh[s]
             r.yinSTFT = [Yh[s][:, :, self.base[k]:self.base[k] + self.M[k]] for k in range(K)]
             r.computeCentralised = bool(p.computeCentralised)

@@ -71,11 +71,11 @@ def host_fields(p, sros, neighbors, rt, nIter, nFramesSTFT, firstSolveRound):
                 e[:R, :] = s[:R, :]
         est.append(e)
         res.append(s)
-    if p.estimateSROs != 'Oracle':
-        # CohDrift / DXCP-PhaT residuals come from the data (not on the device
-        # round path): reported as absent rather than as zeros
+    if p.estimateSROs not in ('Oracle', 'CohDrift'):
+        # DXCP-PhaT inside DANSE raises in the reference itself (quirk Q12)
         warnings.warn(f'estimateSROs={p.estimateSROs!r}: SROsEstimates / SROsResiduals are not computed')
         est, res = None, None
+    # (CohDrift: the engine overwrites both with the device estimates)
     out['SROsEstimates'], out['SROsResiduals'] = est, res
     # compensate_sros (d_classes.py:1955-1970): one entry per neighbour whose
     # buffer flag is nonzero at that update

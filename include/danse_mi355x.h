@@ -126,6 +126,20 @@ typedef struct danse_cfg {
   int32_t scmInitPerBin;    /* 1: scmInit holds one slice per bin, [F][D][D] per
                                family-node (covMatSameInitForAllFreqs = False,
                                init_from_wasn, d_classes.py:553-651); 0: [D][D] */
+  /* CohDrift SRO estimation (estimateSROs 'CohDrift', closed loop, 'ls':
+   * update_sro_estimates + build_phase_shifts_for_srocomp, d_classes.py:
+   * 2364-2621; cohdrift_sro_estimation, d_sros.py:19-95).  The device keeps
+   * the coherence ring, the averaged residual products and a per-(scene,
+   * node, sender) phase accumulator that adds to zPhase (which then holds the
+   * full-sample-drift flags only).  0 = off.                               */
+  int32_t cohDrift;         /* 1: closed loop                                   */
+  int32_t cdSegLength;      /* segLength (ld)                                   */
+  int32_t cdStart;          /* startAfterNups + estEvery (first estimate)       */
+  int32_t cdEvery;          /* estEvery                                         */
+  int32_t cdCompensate;     /* compensateSROs: accumulate the phase             */
+  int32_t cdNIter;          /* the reference's nIter (estimation stops there)   */
+  double cdAlpha;           /* alpha                                            */
+  double cdAlphaEps;        /* alphaEps                                         */
 } danse_cfg;
 
 /* Fields of one fsTab entry (round r, node k). */
@@ -198,6 +212,9 @@ int danse_engine_gate(danse_engine* eng, int32_t r, int32_t n, const int32_t* fa
 /* Replace the round control table (same layout as danse_cfg.flags); the host
  * re-derives the solve flags when the gate delays a node's start.        */
 int danse_engine_set_flags(danse_engine* eng, const uint8_t* flags, void* stream);
+/* CohDrift outputs (SROsEstimates / SROsResiduals of the reference, rows of
+ * the rounds run): est, res [S][K][R][K-1] double, host memory.           */
+int danse_engine_sro_estimates(danse_engine* eng, double* est, double* res);
 /* Speculative form of the gate for graph-captured runs: the n candidates
  * (round, family, node, scene, qY, qN) are checked inside danse_engine_run
  * (between bcast and update of their round) while the run proceeds on the

@@ -209,6 +209,18 @@ def update_covmats_batch(yAllFrames, vadAllFrames):
     return Ryy, Rnn
 
 
+def cohdrift_sro_estimation_ls(wPos, wPri, avgResProd, Ns, ld, alpha, first, bufferFlagPos, bufferFlagPri):
+    """``cohdrift_sro_estimation`` with ``method='ls'`` (``d_sros.py:19-95``)."""
+    res = wPos * wPri.conj()
+    res = np.concatenate([res[:-1], np.conj(res)[::-1][:-1]], -1)
+    res *= np.exp(1j * 2 * np.pi / len(res) * np.arange(len(res)) * (bufferFlagPos - bufferFlagPri))
+    avg = res if first else alpha * avgResProd + (1 - alpha) * res
+    kappa = np.arange(0, len(wPri))
+    b = np.pi * kappa * (ld * Ns) / (len(kappa) * 2)
+    sro = - b.T @ np.angle(avg[-len(kappa):]) / (b.T @ b)
+    return sro, avg
+
+
 def _is_hermitian_and_posdef(x):
     x = np.real_if_close(x)
     b1 = np.allclose(np.transpose(x, axes=(0, 2, 1)).conj(), x)
@@ -386,6 +398,12 @@ class OnlineDANSE:
         self.SROsppm = np.array([nd.sro for nd in self.scene.wasn])
         self.SROsEstimates = [np.zeros((self.nIter, len(self.neighbors[k]))) for k in range(K)]
         self.SROsResiduals = [np.zeros((self.nIter, len(self.neighbors[k]))) for k in range(K)]
+        # CohDrift (d_classes.py:2364-2470, d_sros.py:19-95): per-iteration
+        # coherences yyH[0, q] / sqrt(yyH[0, 0] yyH[q, q]) and the averaged
+        # residual products (2 (F - 1) bins, the reference's full-spectrum layout)
+        self.cohHist = [np.zeros((self.nIter, self.F, len(self.neighbors[k])), dtype=complex) for k in range(K)]
+        self.avgProdResiduals = [np.zeros((2 * (self.F - 1), len(self.neighbors[k])), dtype=complex)
+                                 for k in range(K)]
         self.nInternalFilterUps = np.zeros(K)
         self.lastExtFiltUp = np.zeros(K)
         self.nSensorsNeighborsCentr = [[self.M[q] for q in range(K) if q != k] for k in range(K)]
@@ -610,11 +628,21 @@ class OnlineDANSE:
                 extra[self.M[k] + q] = fl
             else:
                 skipUpdate = True
+        yUncomp = yTHat.copy()
         if p.compensateSROs:
             if p.includeFSDflags:
                 self.phaseShiftFactors[k] += extra
             psf = np.exp(-1 * 1j * 2 * np.pi / N * np.outer(np.arange(self.F), self.phaseShiftFactors[k]))
             yTHat *= psf
+        if p.estimateSROs == 'CohDrift':
+            yc = yTHat if p.cohDrift.loop == 'closed' else yUncomp
+            D = yc.shape[1]
+            for q in range(len(self.neighbors[k])):
+                iq = self.M[k] + q
+                yy0q = yc[:, 0] * yc[:, iq].conj() / D
+                yy00 = yc[:, 0] * yc[:, 0].conj() / D
+                yyqq = yc[:, iq] * yc[:, iq].conj() / D
+                self.cohHist[k][i, :, q] = yy0q / np.sqrt(yy00 * yyqq)
         skipUpdateCentr = None
         if p.computeCentralised:
             skipUpdateCentr = False
@@ -679,10 +707,17 @@ class OnlineDANSE:
             sroOut = (self.SROsppm[self.neighbors[k]] - self.SROsppm[k]) * 1e-6
             self.SROsResiduals[k][i, :] = sroOut
         elif p.estimateSROs == 'CohDrift':
-            raise NotImplementedError('CohDrift SRO estimation in the oracle')
+            self._cohdrift(k, i)
         if p.compensateSROs:
             for q in range(len(self.neighbors[k])):
-                self.SROsEstimates[k][i, q] = (self.SROsppm[self.neighbors[k][q]] - self.SROsppm[k]) * 1e-6
+                if p.estimateSROs == 'CohDrift':
+                    res = self.SROsResiduals[k][i, q]
+                    if p.cohDrift.loop == 'closed':
+                        self.SROsEstimates[k][i, q] += res / (1 + res) * p.cohDrift.alphaEps
+                    else:
+                        self.SROsEstimates[k][i, q] = res / (1 + res)
+                else:
+                    self.SROsEstimates[k][i, q] = (self.SROsppm[self.neighbors[k][q]] - self.SROsppm[k]) * 1e-6
                 self.phaseShiftFactors[k][self.M[k] + q] -= self.SROsEstimates[k][i, q] * self.Ns
             if p.computeCentralised:
                 for q in range(self.K):
@@ -775,6 +810,31 @@ class OnlineDANSE:
             self.local[k].w[:, i + 1, :] = fn(self.local[k].Ryy, self.local[k].Rnn, refSensorIdx=p.referenceSensor, rank=rank)
         if p.computeSingleSensorBroadcast and self.ssbc[k].start and p.simType != 'batch':
             self.ssbc[k].w[:, i + 1, :] = fn(self.ssbc[k].Ryy, self.ssbc[k].Rnn, refSensorIdx=p.referenceSensor, rank=rank)
+
+    # ---- update_sro_estimates, CohDrift branch (2364-2470) ----
+    def _cohdrift(self, k, i):
+        p = self.p
+        cd = p.cohDrift
+        if p.computeCentralised:
+            raise NotImplementedError('CohDrift with centralised estimates')
+        if cd.estimationMethod != 'ls':
+            raise NotImplementedError("CohDrift estimationMethod 'gs' (paderwasn max_time_lag_search)")
+        idx = np.arange(cd.startAfterNups + cd.estEvery, self.nIter, cd.estEvery)
+        if i not in idx:
+            return
+        first = i == np.amin(idx)
+        ld = cd.segLength
+        bfPos = p.broadcastLength * np.sum(self.bufferFlags[k][:(i + 1), :], axis=0)
+        bfPri = p.broadcastLength * np.sum(self.bufferFlags[k][:(i - ld + 1), :], axis=0)
+        if cd.loop == 'closed':
+            bfPos = np.zeros_like(bfPos)
+            bfPri = np.zeros_like(bfPri)
+        for q in range(len(self.neighbors[k])):
+            sro, apr = cohdrift_sro_estimation_ls(self.cohHist[k][i, :, q], self.cohHist[k][i - ld, :, q],
+                                                  self.avgProdResiduals[k][:, q], self.Ns, ld, cd.alpha, first,
+                                                  bfPos[q], bfPri[q])
+            self.SROsResiduals[k][i, q] = sro
+            self.avgProdResiduals[k][:, q] = apr
 
     # ---- update_external_filters (1627-1694) ----
     def _update_external_filters(self, k, t):

@@ -10,7 +10,10 @@ from danse_amd.scene import make_scene
 def make_case_params(case, SROperNode=None):
     if SROperNode is None:
         SROperNode = case.get('sros')
-    dp = P.DANSEparameters(**case['danse'])
+    kw = dict(case['danse'])
+    if isinstance(kw.get('cohDrift'), dict):
+        kw['cohDrift'] = P.CohDriftParameters(**kw['cohDrift'])
+    dp = P.DANSEparameters(**kw)
     wp = P.WASNparameters(trueRoom=False, signalType='random', nSensorPerNode=list(case['M']),
                           SROperNode=np.zeros(len(case['M'])) if SROperNode is None else np.asarray(SROperNode),
                           topologyParams=P.TopologyParameters(topologyType='fully-connected', seed=12348))

@@ -155,6 +155,8 @@ def make_params(ns, nSensorPerNode, fs=16000.0, **danse_overrides):
     for k, v in danse_overrides.items():
         if not hasattr(p.danseParams, k):
             raise KeyError(k)
+        if k == 'cohDrift' and isinstance(v, dict):
+            v = ns.base.CohDriftParameters(**v)
         setattr(p.danseParams, k, v)
     p.danseParams.__post_init__()
     p.exportParams = ns.cl.ExportParameters(bypassAllExports=True, conditionNumberPlot=False)

@@ -66,6 +66,12 @@ ONLINE_CASES = [
     dict(name='online_C_sro_comp_asy', M=[2, 3, 2], dur=3.0, seed=8, sros=[0, 100, 200],
          danse=_d(BATTERY, nodeUpdating='asy', compensateSROs=True, includeFSDflags=True, estimateSROs='Oracle',
                   computeLocal=True)),
+    # CohDrift SRO estimation (d_sros.py:19-95, d_classes.py:2364-2621): closed
+    # loop, least-squares fit over bins, estimates feeding the phase
+    # compensation from iteration startAfterNups + estEvery on
+    dict(name='online_C_cohdrift_asy', M=[2, 3, 2], dur=3.0, seed=15, sros=[0, 60, 120],
+         danse=_d(BATTERY, nodeUpdating='asy', compensateSROs=True, includeFSDflags=True, estimateSROs='CohDrift',
+                  cohDrift=dict(estimationMethod='ls'))),
     dict(name='online_C_sro_noflags_seq', M=[2, 2, 2, 2], dur=3.0, seed=9, sros=[50, 0, 200, 120],
          danse=_d(BATTERY, nodeUpdating='seq', compensateSROs=True, includeFSDflags=False, estimateSROs='Oracle')),
     # config E shape (tests/battery20230919_perf_asfctofL.py:14-110): MK = [2, 3],

@@ -238,3 +238,29 @@ def test_config_C_shape_K16_sro_vs_oracle():
     assert de <= 1e-4
     for k in range(16):
         assert np.array_equal(dv.SROsEstimates[k][:dv.nRounds], ov.SROsEstimates[k][:dv.nRounds])
+
+
+def test_cohdrift_sro_estimates_vs_oracle():
+    """CohDrift SRO estimation (closed loop, 'ls'; d_sros.py:19-95,
+    d_classes.py:2364-2621) on the device: the per-update residual SRO
+    estimates and the compensated estimates they feed match the float64
+    oracle (itself pinned to the reference by online_C_cohdrift_asy)."""
+    from danse_amd.core import danse_multi
+    from oracle import danse_ref_cpu as O
+    case = _case('online_C_cohdrift_asy')
+    sc, dp, wp = _scene_params(case)
+    dv = danse_multi([sc], dp)[0]
+    ov = O.OnlineDANSE(sc, dp, vadMinProp=wp.vadMinProportionActive)
+    ov.run()
+    for k in range(len(case['M'])):
+        rd = np.asarray(dv.SROsResiduals[k])
+        ro = np.asarray(ov.SROsResiduals[k])[:rd.shape[0]]
+        scale = max(float(np.max(np.abs(ro))), 1e-12)
+        err = float(np.max(np.abs(rd - ro))) / scale
+        nz = int(np.count_nonzero(ro))
+        print('node', k, 'residual SRO rel err', err, 'estimates', nz, 'max |res|', scale)
+        assert nz > 0
+        assert err <= 2e-3, err
+        ed = np.asarray(dv.SROsEstimates[k])
+        eo = np.asarray(ov.SROsEstimates[k])[:ed.shape[0]]
+        assert float(np.max(np.abs(ed - eo))) <= 2e-3 * max(float(np.max(np.abs(eo))), 1e-12)
