@@ -65,6 +65,12 @@ WORKLOADS = {
     # north_star headline shape: online, 32 nodes x 8 mics (D = 39), 513 bins, one WASN per GPU
     'N2': dict(M=[8] * 32, dur=10.0, nodeUpdating='asy', scenes=1,
                desc='N2: online GEVD-DANSE r1, K=32 x 8 mics (D=39), N=1024, asy, 10 s, single WASN'),
+    # BASELINE.json configs[2]: online, K = 16 x 4 (D = 19), SROs up to 200 ppm with
+    # data-driven SRO estimation (CohDrift, closed loop, least squares) and
+    # phase compensation; 8 WASNs per GPU
+    'C': dict(M=[4] * 16, dur=10.0, nodeUpdating='asy', scenes=8, sros=[float(x) for x in np.linspace(0, 200, 16)],
+              extra=dict(compensateSROs=True, includeFSDflags=True, estimateSROs='CohDrift', cohdrift_ls=True),
+              desc='C: GEVD-DANSE r1, K=16 x 4 mics (D=19), SROs 0..200 ppm, CohDrift estimation + compensation, asy, 10 s'),
     'B_seq': dict(M=[4] * 8, dur=10.0, nodeUpdating='seq', scenes=31, desc='B (seq): GEVD-DANSE r1, K=8 x 4 mics, seq, 10 s'),
     'small': dict(M=[2] * 4, dur=3.0, nodeUpdating='asy', desc='small smoke workload K=4 x 2, 3 s'),
     # BASELINE.json configs[4] scene shape (tests/battery20230919_perf_asfctofL.py:14-88):
@@ -83,7 +89,11 @@ for _n, _w in WORKLOADS.items():
 
 
 def _wl_params(wl):
-    return _battery_params(wl['M'], wl['nodeUpdating'], **wl.get('extra', {}))
+    extra = dict(wl.get('extra', {}))
+    if extra.pop('cohdrift_ls', False):
+        from danse_amd import params as P
+        extra['cohDrift'] = P.CohDriftParameters(estimationMethod='ls')
+    return _battery_params(wl['M'], wl['nodeUpdating'], **extra)
 
 
 def update_kernel_name(Dmax, gevd=True):
@@ -265,7 +275,7 @@ def run_online(args, wl, S, rank, world, local, dist, traffic=True, pmc_child=Fa
     t0 = time.time()
     scenes = []
     for i, sd in enumerate(seeds):
-        sc = make_scene(M, sigDur=wl['dur'], seed=1000 + sd, nodes=nodes)
+        sc = make_scene(M, sigDur=wl['dur'], seed=1000 + sd, nodes=nodes, SROperNode=wl.get('sros'))
         sc.get_vad_per_frame(dp.DFTsize, dp.Ns, wp.vadMinProportionActive)
         scenes.append(sc)
         if (i + 1) % 64 == 0:
@@ -528,7 +538,7 @@ def cpu_baseline(M, wl, dp, wp, seconds, rounds=None):
     rate is, if anything, over-stated."""
     from danse_amd.scene import make_scene
     from oracle import danse_ref_cpu as O
-    sc = make_scene(M, sigDur=wl['dur'], seed=1000)
+    sc = make_scene(M, sigDur=wl['dur'], seed=1000, SROperNode=wl.get('sros'))
     sc.get_vad_per_frame(dp.DFTsize, dp.Ns, wp.vadMinProportionActive)
     K, F = len(M), dp.DFTsize // 2 + 1
     D = max(M) + K - 1

@@ -211,16 +211,20 @@ def test_sandbox_main_random_ir():
     assert len(out.filters) == K and len(out.yinSTFT) == K
 
 
-def test_config_C_shape_K16_sro_vs_oracle():
-    """Config C's shape: K = 16 x 4 mics (D = 19, the wavefront class), SROs
-    linspace(0, 200, 16) ppm, Oracle SRO estimates, phase compensation with
-    full-sample-drift flags, asy, against the float64 oracle (the oracle's
-    SRO path is pinned by the online_C_sro_* reference fixtures)."""
+@pytest.mark.parametrize('est', ['Oracle', 'CohDrift'])
+def test_config_C_shape_K16_sro_vs_oracle(est):
+    """Config C's shape: K = 16 x 4 mics (D = 19, the 2D class), SROs
+    linspace(0, 200, 16) ppm, phase compensation with full-sample-drift
+    flags, asy, Oracle or data-driven CohDrift SRO estimates, against the
+    float64 oracle (pinned by the online_C_sro_* / online_C_cohdrift_asy
+    reference fixtures)."""
     from danse_amd.core import danse_multi
     from oracle import danse_ref_cpu as O
+    from danse_amd.params import CohDriftParameters
+    extra = dict(cohDrift=CohDriftParameters(estimationMethod='ls')) if est == 'CohDrift' else {}
     case = dict(name='online_C_shape_K16_sro', M=[4] * 16, dur=4.0, seed=51, sros=list(np.linspace(0, 200, 16)),
                 danse=dict(BATTERY, nodeUpdating='asy', compensateSROs=True, includeFSDflags=True,
-                           estimateSROs='Oracle'))
+                           estimateSROs=est, **extra))
     sc, dp, wp = _scene_params(case)
     dv = danse_multi([sc], dp)[0]
     ov = O.danse(sc, dp, vadMinProp=wp.vadMinProportionActive)
@@ -233,11 +237,21 @@ def test_config_C_shape_K16_sro_vs_oracle():
         errs.append(_bin_rel(dv.wTilde[k][:, s0 + 1:dv.nRounds + 1], ov.wTilde[k][:, s0 + 1:dv.nRounds + 1]).ravel())
     st = _stats(np.concatenate(errs))
     de = rel_err(dv.d, ov.d)
-    print(case['name'], 'w', st, 'd', de)
-    assert st['median'] <= 1e-5 and st['p99'] <= 1e-4, st
+    print(case['name'], est, 'w', st, 'd', de)
+    # CohDrift closes a loop: each estimate comes from the coherence phase of
+    # the float32 spectra (differences ~1e-7 rad from the float64 oracle's)
+    # and moves the compensation phase of every later frame, so the filter
+    # differences grow with the run instead of staying at the per-frame
+    # level; measured p99 1.1e-4 over 125 rounds at K = 16
+    p99tol = 1e-4 if est == 'Oracle' else 3e-4
+    assert st['median'] <= 1e-5 and st['p99'] <= p99tol, st
     assert de <= 1e-4
     for k in range(16):
-        assert np.array_equal(dv.SROsEstimates[k][:dv.nRounds], ov.SROsEstimates[k][:dv.nRounds])
+        if est == 'Oracle':
+            assert np.array_equal(dv.SROsEstimates[k][:dv.nRounds], ov.SROsEstimates[k][:dv.nRounds])
+        else:
+            eo = ov.SROsEstimates[k][:dv.nRounds]
+            assert np.max(np.abs(dv.SROsEstimates[k][:dv.nRounds] - eo)) <= 2e-3 * max(np.max(np.abs(eo)), 1e-12)
 
 
 def test_cohdrift_sro_estimates_vs_oracle():
