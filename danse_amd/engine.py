@@ -163,6 +163,9 @@ class DanseEngine:
             # local spectra and the centralised VAD averages every node's VAD;
             # a node-sharded engine only analyses (and only has) its own nodes
             raise NotImplementedError('centralised / single-sensor-broadcast estimates on a node-sharded engine')
+        if (self.k0, self.k1) != (0, K) and p.estimateSROs == 'CohDrift':
+            # the CohDrift kernel runs for every (node, sender) pair of the engine
+            raise NotImplementedError('CohDrift SRO estimation on a node-sharded engine')
         if not self.rt.synchronous and (p.computeCentralised or p.computeSingleSensorBroadcast):
             raise NotImplementedError('centralised / single-sensor-broadcast estimates with asynchronous (SRO) '
                                       'clocks are not on the device path')
