@@ -144,6 +144,9 @@ def main():
                          '~2 full rounds of the 1024 wave slots the update kernel can hold; N2 default 1)')
     ap.add_argument('--workload', default='B', choices=sorted(WORKLOADS))
     ap.add_argument('--shard', default='nodes', choices=['nodes', 'scenes'])
+    ap.add_argument('--batch-shard', default='replicas', choices=['replicas', 'nodes'],
+                    help='config D on N>1 GPUs: independent WASNs per GPU (weak scaling) or every GPU owning a '
+                         'node block of the same WASNs, external filters all-gathered per iteration (strong)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
     ap.add_argument('--no-graph', action='store_true')
@@ -397,22 +400,31 @@ def bench_batch(args, wl, S, rank, world, local, dist):
     dp.simType = 'batch'
     dp.maxBatchUpdates = wl['iters']
     t0 = time.time()
+    byNodes = dist is not None and world > 1 and args.batch_shard == 'nodes'
     scenes = []
-    for sd in range(rank * S, (rank + 1) * S):
+    for sd in (range(S) if byNodes else range(rank * S, (rank + 1) * S)):
         sc = make_scene(M, sigDur=wl['dur'], seed=2000 + sd)
         sc.get_vad_per_frame(dp.DFTsize, dp.Ns, wp.vadMinProportionActive)
         scenes.append(sc)
     tScene = time.time() - t0
-    eng = BatchEngine(scenes, dp, device=local)
+    if byNodes:
+        from danse_amd.batch import node_ranges, run_node_sharded, allgather_exchange
+        rngs, blk = node_ranges(K, world)
+        eng = BatchEngine(scenes, dp, device=local, nodeRange=rngs[rank])
+        ex = allgather_exchange(dist, world)
+        step = lambda: run_node_sharded(eng, ex, blk)   # noqa: E731
+    else:
+        eng = BatchEngine(scenes, dp, device=local)
+        step = eng.run
     for _ in range(args.warmup):
-        eng.run()
+        step()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     for _ in range(args.steps):
-        eng.run()
+        step()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -423,19 +435,20 @@ def bench_batch(args, wl, S, rank, world, local, dist):
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
     F = eng.F
-    fu_per_step = S * world * K * eng.nseg * F * eng.iters
+    fu_per_step = S * (1 if byNodes else world) * K * eng.nseg * F * eng.iters
     D = M[0] + K - 1
-    herk_flops = S * K * eng.iters * 4.0 * F * D * (D + 1) * eng.nseg   # SURVEY §8d (Hermitian half)
+    herk_flops = S * (eng.k1 - eng.k0) * eng.iters * 4.0 * F * D * (D + 1) * eng.nseg   # SURVEY §8d (Hermitian half)
     if rank == 0:
         line = {
             'metric': 'DANSE frame-updates/sec (nodes x bins)', 'value': fu_per_step * args.steps / el,
             'unit': 'frame-updates/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
-            'ms_per_step': el / args.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak',
-            'vs_baseline': None, 'dtype': 'c64',
-            'data': f'synthetic random-IR scenes (seeded), {S * world} WASNs x {K} nodes x {eng.nseg} frames x {F} '
+            'ms_per_step': el / args.steps * 1e3, 'higher_is_better': True,
+            'scaling': 'strong' if byNodes else 'weak', 'vs_baseline': None, 'dtype': 'c64',
+            'data': f'synthetic random-IR scenes (seeded), {S * (1 if byNodes else world)} WASNs x {K} nodes x {eng.nseg} frames x {F} '
                     f'bins x {eng.iters} iterations per step',
             'config': {'workload': wl['desc'], 'wasns_per_gpu': S, 'K': K, 'M': M[0], 'D': D, 'bins': F,
-                       'frames': eng.nseg, 'iterations': eng.iters, 'shard': 'replicas'},
+                       'frames': eng.nseg, 'iterations': eng.iters,
+                       'shard': 'nodes' if byNodes else 'replicas'},
             'roofline': None,
             'herk_alg_flops_per_step_per_gpu': herk_flops,
             'cpu_baseline': None,

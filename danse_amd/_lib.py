@@ -58,6 +58,8 @@ class DanseBatchCfg(ctypes.Structure):
         ('vad', _p_u8), ('doSolve', _p_u8),
         ('w0', _p_f32), ('wExt0', _p_f32),
         ('costTrim', _c_i32),
+        ('k0', _c_i32),
+        ('k1', _c_i32),
     ]
 
 
@@ -103,6 +105,9 @@ SIGNATURES = {
     'danse_batch_last_error': (ctypes.c_char_p, [ctypes.c_void_p]),
     'danse_batch_set_inputs': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     'danse_batch_run': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p]),
+    'danse_batch_run_iters': (_c_i32, [ctypes.c_void_p, _c_i32, _c_i32, ctypes.c_void_p]),
+    'danse_batch_pack_wext': (_c_i32, [ctypes.c_void_p, _c_i32, ctypes.c_void_p, ctypes.c_void_p]),
+    'danse_batch_unpack_wext': (_c_i32, [ctypes.c_void_p, _c_i32, ctypes.c_void_p, ctypes.c_void_p]),
     'danse_batch_output_bytes': (_c_i32, [ctypes.c_void_p, _c_i32, _c_i32, ctypes.POINTER(ctypes.c_size_t)]),
     'danse_batch_get': (_c_i32, [ctypes.c_void_p, _c_i32, _c_i32, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
     'danse_dxcp_create': (_c_i32, [_c_i32, _c_i32, ctypes.POINTER(ctypes.c_void_p)]),

@@ -23,7 +23,12 @@ from .outputs import stft_frames  # noqa: F401  (re-exported)
 class BatchEngine:
     """S same-shape scenes of one WASN shape, batch DANSE on one device."""
 
-    def __init__(self, scenes, p, device=0, costTrim=1000):
+    def __init__(self, scenes, p, device=0, costTrim=1000, nodeRange=None):
+        """``nodeRange=(k0, k1)``: node-sharded batch DANSE -- this engine
+        computes z for every node but SCMs, solves, external filters,
+        estimates and costs only for nodes k0..k1-1; the other nodes'
+        external filters arrive through :meth:`unpack_wext` (see
+        :func:`run_node_sharded`)."""
         import torch
         self.torch = torch
         self.lib = L.load_library()
@@ -48,6 +53,12 @@ class BatchEngine:
             if sorted(sc0.wasn[k].neighborsIdx) != [q for q in range(K) if q != k]:
                 raise NotImplementedError('device path covers fully connected WASNs')
         self.device = device
+        if nodeRange is None:
+            nodeRange = (0, K)
+        self.k0, self.k1 = int(nodeRange[0]), int(nodeRange[1])
+        if not 0 <= self.k0 < self.k1 <= K:
+            raise ValueError(f'nodeRange {nodeRange} is not a non-empty range of the {K} nodes')
+        self.Mmax = max(self.M)
         self.iters = int(p.maxBatchUpdates)
         self.nIter = int((T - self.N) / self.Ns) + 1
         self.nseg = nseg = stft_frames(T, self.N, self.Ns)
@@ -110,6 +121,7 @@ class BatchEngine:
         c.doSolve = _ptr(self._doSolve, ctypes.c_uint8)
         c.w0, c.wExt0 = _ptr(self._w0, ctypes.c_float), _ptr(self._wExt0, ctypes.c_float)
         c.costTrim = int(costTrim)
+        c.k0, c.k1 = self.k0, self.k1
         self._cfg = c
         eng = ctypes.c_void_p()
         L.check_batch(self.lib.danse_batch_create(ctypes.byref(c), int(device), ctypes.byref(eng)))
@@ -132,6 +144,36 @@ class BatchEngine:
 
     def run(self, stream=None):
         L.check_batch(self.lib.danse_batch_run(self.eng, self.stream_ptr(stream)), self.eng)
+        return self
+
+    def run_iters(self, it0, it1, stream=None):
+        """Batch iterations [it0, it1) (it0 == 0 also sets the initial state
+        and computes the STFT of the inputs)."""
+        L.check_batch(self.lib.danse_batch_run_iters(self.eng, int(it0), int(it1), self.stream_ptr(stream)), self.eng)
+        return self
+
+    def wext_chunk(self):
+        """Complex64 elements of one (node, scene) chunk of the exchange buffers."""
+        return self.F * self.Mmax
+
+    def pack_wext(self, slot, out, stream=None):
+        """Own nodes' external filters of history slot ``slot`` into the device
+        tensor ``out`` (complex64, >= (k1 - k0) * S * F * Mmax elements)."""
+        n = (self.k1 - self.k0) * self.S * self.wext_chunk()
+        if out.dtype != self.torch.complex64 or out.numel() < n or not out.is_contiguous():
+            raise ValueError('pack_wext needs a contiguous complex64 tensor of (k1-k0)*S*F*Mmax elements')
+        L.check_batch(self.lib.danse_batch_pack_wext(self.eng, int(slot), ctypes.c_void_p(out.data_ptr()),
+                                                     self.stream_ptr(stream)), self.eng)
+        return out
+
+    def unpack_wext(self, slot, src, stream=None):
+        """Other nodes' external filters of slot ``slot`` from ``src``
+        ([K][S][F * Mmax] complex64, node order)."""
+        n = self.K * self.S * self.wext_chunk()
+        if src.dtype != self.torch.complex64 or src.numel() < n or not src.is_contiguous():
+            raise ValueError('unpack_wext needs a contiguous complex64 tensor of K*S*F*Mmax elements')
+        L.check_batch(self.lib.danse_batch_unpack_wext(self.eng, int(slot), ctypes.c_void_p(src.data_ptr()),
+                                                       self.stream_ptr(stream)), self.eng)
         return self
 
     def _get(self, which, node=0, dtype=np.complex64, shape=None):
@@ -177,6 +219,50 @@ class BatchEngine:
             self.close()
         except Exception:
             pass
+
+
+def node_ranges(K, world):
+    """Contiguous node blocks of ceil(K / world) nodes per rank, so that the
+    all-gathered exchange buffer [world * c][S][F * Mmax] lists the nodes in
+    order.  Every rank must own at least one node."""
+    c = -(-K // world)
+    rngs = [(r * c, min(K, (r + 1) * c)) for r in range(world)]
+    if any(a >= b for a, b in rngs):
+        raise ValueError(f'{K} nodes do not split into {world} non-empty blocks of {c}')
+    return rngs, c
+
+
+def run_node_sharded(eng, exchange, blockNodes, stream=None, device=None):
+    """One batch-DANSE run of a node-sharded engine.  After every iteration
+    the engine's own nodes' new external filters are packed into a
+    [blockNodes][S][F * Mmax] buffer and ``exchange(buf)`` returns the
+    gathered [>= K][S][F * Mmax] buffer of all ranks in node order (an RCCL
+    all_gather_into_tensor across ranks, see :func:`allgather_exchange`);
+    the other nodes' slots are filled from it before the next iteration's z.
+    This is the one data exchange of batch DANSE: node k's estimate needs
+    z_q = wExt_q^H y_q of every neighbour q (d_core.py:286-326)."""
+    torch = eng.torch
+    dev = device if device is not None else f'cuda:{eng.device}'
+    buf = torch.zeros(blockNodes * eng.S * eng.wext_chunk(), dtype=torch.complex64, device=dev)
+    for it in range(eng.iters):
+        eng.run_iters(it, it + 1, stream)
+        eng.pack_wext(it + 1, buf, stream)
+        eng.unpack_wext(it + 1, exchange(buf), stream)
+    return eng
+
+
+def allgather_exchange(dist, world):
+    """exchange() for run_node_sharded over torch.distributed (RCCL on the
+    GPU; gloo would need host tensors)."""
+    cache = {}
+
+    def ex(buf):
+        out = cache.get(buf.numel())
+        if out is None:
+            out = cache[buf.numel()] = buf.new_empty(world * buf.numel())
+        dist.all_gather_into_tensor(out, buf)
+        return out
+    return ex
 
 
 class BatchOutputs:

@@ -209,7 +209,7 @@ __global__ void batch_ext_kernel(int S, int K, int it, const int* __restrict__ M
                                  long long wStride, int hist, cf* __restrict__ wExtHist,
                                  const long long* __restrict__ wExtOff, long long wExtStride,
                                  cf* __restrict__ tgt, const long long* __restrict__ tgtOff, long long tgtStride,
-                                 int Mmax) {
+                                 int Mmax, int k0, int nOwn) {
   constexpr int F = 513;
   const long long n = (long long)S * K * F * Mmax;
   for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
@@ -218,7 +218,7 @@ __global__ void batch_ext_kernel(int S, int K, int it, const int* __restrict__ M
     const int k = (int)((e / ((long long)Mmax * F)) % K);
     const int s = (int)(e / ((long long)Mmax * F * K));
     const int Mq = M[k];
-    if (m >= Mq) continue;
+    if (m >= Mq || k < k0 || k >= k0 + nOwn) continue;   // other ranks' nodes arrive by unpack
     const cf* w = wHist + (long long)s * wStride + wOff[k] + ((long long)(it + 1) * F + f) * Dk[k];
     cf* eprev = wExtHist + (long long)s * wExtStride + wExtOff[k] + ((long long)it * F + f) * Mq;
     cf* enext = eprev + (long long)F * Mq;
@@ -247,16 +247,16 @@ __global__ void __launch_bounds__(256) batch_est_kernel(const cf* __restrict__ Y
                                                         const cf* __restrict__ wHist, const long long* __restrict__ wOff,
                                                         long long wStride, int slot, const float* __restrict__ win,
                                                         const cf* __restrict__ tw, cf* __restrict__ dhat,
-                                                        float* __restrict__ frames) {
+                                                        float* __restrict__ frames, int k0, int nOwn) {
   __shared__ cf lds[4][wfft::kLdsElems];
   constexpr int F = 513;
   const int nfr = nseg - 1;
   const int wv = threadIdx.x >> 6;
   const long long job = (long long)blockIdx.x * 4 + wv;
-  if (job >= (long long)S * K * nfr) return;
+  if (job >= (long long)S * nOwn * nfr) return;
   const int t = (int)(job % nfr);
-  const int k = (int)((job / nfr) % K);
-  const int s = (int)(job / ((long long)nfr * K));
+  const int k = k0 + (int)((job / nfr) % nOwn);
+  const int s = (int)(job / ((long long)nfr * nOwn));
   const int Mk = M[k], D = Dk[k];
   const cf* w = wHist + (long long)s * wStride + wOff[k] + (long long)slot * F * D;
   const int l = __lane_id();
@@ -310,13 +310,14 @@ __global__ void __launch_bounds__(256) batch_est_kernel(const cf* __restrict__ Y
 // Overlap-add of the windowed frames, normalised by the overlap-add of win^2
 // where that exceeds 1e-10 (scipy istft); zero beyond the last frame.
 __global__ void batch_ola_kernel(const float* __restrict__ frames, int S, int K, int T, int Ns, int nseg,
-                                 const float* __restrict__ win, float* __restrict__ d) {
+                                 const float* __restrict__ win, float* __restrict__ d, int k0, int nOwn) {
   const int nfr = nseg - 1;
-  const long long n = (long long)S * K * T;
+  const long long n = (long long)S * nOwn * T;
   const int outLen = 1024 + (nfr - 1) * Ns;
   for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
     const int x = (int)(e % T);
-    const long long sk = e / T;
+    const long long so = e / T;   // (scene, owned node)
+    const long long sk = (so / nOwn) * K + k0 + so % nOwn;
     float acc = 0.0f, nrm = 0.0f;
     if (x < outLen) {
       int tLo = (x - 1024) / Ns + 1;
@@ -330,7 +331,7 @@ __global__ void batch_ola_kernel(const float* __restrict__ frames, int S, int K,
       }
       if (nrm > 1e-10f) acc /= nrm;
     }
-    d[e] = acc;
+    d[sk * T + x] = acc;
   }
 }
 
@@ -357,9 +358,9 @@ __global__ void batch_wstore_kernel(const cf* __restrict__ wTmp, int nRun, int S
 constexpr int kCostThr = 1024;
 __global__ void __launch_bounds__(kCostThr) batch_cost_kernel(const float* __restrict__ clean,
                                                               const float* __restrict__ d, int T, int trim,
-                                                              double* __restrict__ cost) {
+                                                              double* __restrict__ cost, int K, int k0, int nOwn) {
   __shared__ double red[kCostThr];
-  const long long sk = blockIdx.x;
+  const long long sk = (long long)(blockIdx.x / nOwn) * K + k0 + blockIdx.x % nOwn;
   const float* c = clean + sk * T;
   const float* dd = d + sk * T;
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
@@ -393,6 +394,7 @@ struct danse_batch {
   int dev = 0;
   std::string err;
   int S, K, MT, N, Ns, T, F, iters, nseg, gevd, rank, ref, trim;
+  int k0 = 0, k1 = 0;   // owned nodes (node-sharded batch DANSE across GPUs)
   float alphaExt;
   std::vector<int> M, base, D, extMode;
   std::vector<long long> scmOff, wOff, wExtOff, tgtOff;
@@ -453,6 +455,9 @@ int danse_batch_create(const danse_batch_cfg* c, int device, danse_batch** out) 
   eng->S = c->S; eng->K = c->K; eng->N = c->N; eng->Ns = c->Ns; eng->T = c->T; eng->F = c->N / 2 + 1;
   eng->iters = c->iters; eng->nseg = c->nseg; eng->gevd = c->gevd; eng->rank = c->rank; eng->ref = c->ref;
   eng->alphaExt = c->alphaExt; eng->trim = c->costTrim;
+  eng->k0 = c->k1 > c->k0 ? c->k0 : 0;
+  eng->k1 = c->k1 > c->k0 ? c->k1 : c->K;
+  if (eng->k0 < 0 || eng->k1 > c->K) return bfail(eng, "bad owned node range");
   const int S = c->S, K = c->K, F = eng->F, nseg = c->nseg, H = c->iters + 1;
   eng->M.assign(c->M, c->M + K);
   eng->extMode.assign(c->extMode, c->extMode + K);
@@ -583,13 +588,13 @@ static void launch_herk(danse_batch* e, hipStream_t st) {
   for (int nt = 1; nt <= 4; ++nt) {
     std::vector<HerkNode> grp;
     for (auto& n : e->nodes)
-      if ((n.D + 15) / 16 == nt) grp.push_back(n);
+      if ((n.D + 15) / 16 == nt && n.k >= e->k0 && n.k < e->k1) grp.push_back(n);
     if (grp.empty()) continue;
-    // contiguous groups only when all nodes share nt (the common case); else per node
-    const bool all = (int)grp.size() == e->K;
+    // contiguous groups only when all owned nodes share nt (the common case); else per node
+    const bool all = (int)grp.size() == e->k1 - e->k0;
     for (size_t g = 0; g < (all ? 1 : grp.size()); ++g) {
-      const HerkNode* dn = e->dNodes + (all ? 0 : grp[g].k);
-      const int nN = all ? e->K : 1;
+      const HerkNode* dn = e->dNodes + (all ? e->k0 : grp[g].k);
+      const int nN = all ? e->k1 - e->k0 : 1;
       const unsigned grid = (unsigned)(e->S * nN * e->F);
 #define DANSE_HERK(NTV)                                                                                             \
   hipLaunchKernelGGL((herk_kernel<NTV, cd>), dim3(grid), dim3(64), 0, st, e->Y, e->Z, e->S, e->K, e->MT, e->nseg, e->dBase, \
@@ -604,12 +609,19 @@ static void launch_herk(danse_batch* e, hipStream_t st) {
 }
 
 int danse_batch_run(danse_batch* eng, void* stream) {
+  if (!eng) return bfail(eng, "null engine");
+  return danse_batch_run_iters(eng, 0, eng->iters, stream);
+}
+
+int danse_batch_run_iters(danse_batch* eng, int32_t it0, int32_t it1, void* stream) {
   if (!eng || !eng->y) return bfail(eng, "inputs not set");
+  if (it0 < 0 || it1 > eng->iters || it0 >= it1) return bfail(eng, "bad iteration range");
   BCHK(hipSetDevice(eng->dev));
   hipStream_t st = (hipStream_t)stream;
   const int S = eng->S, K = eng->K, F = eng->F, nseg = eng->nseg, H = eng->iters + 1;
+  const int k0 = eng->k0, nOwn = eng->k1 - eng->k0;
   // initial state: w / wExt slot 0 and the external-filter targets
-  for (int s = 0; s < S; ++s) {
+  if (it0 == 0) for (int s = 0; s < S; ++s) {
     long long a = 0, b = 0;
     for (int k = 0; k < K; ++k) {
       BCHK(hipMemcpyAsync(eng->wHist + (long long)s * eng->wStride + eng->wOff[k], eng->w0.data() + a,
@@ -622,7 +634,7 @@ int danse_batch_run(danse_batch* eng, void* stream) {
       b += (long long)F * eng->M[k];
     }
   }
-  {
+  if (it0 == 0) {
     const long long jobs = (long long)S * eng->MT * nseg;
     hipLaunchKernelGGL(batch_stft_kernel, dim3((unsigned)((jobs + 3) / 4)), dim3(256), 0, st, eng->y, S, eng->MT,
                        eng->T, eng->Ns, nseg, eng->dWin, eng->dTw, eng->Y);
@@ -630,7 +642,7 @@ int danse_batch_run(danse_batch* eng, void* stream) {
   }
   int Mmax = 0;
   for (int k = 0; k < K; ++k) Mmax = std::max(Mmax, eng->M[k]);
-  for (int it = 0; it < eng->iters; ++it) {
+  for (int it = it0; it < it1; ++it) {
     hipLaunchKernelGGL(batch_z_kernel, dim3(2048), dim3(256), 0, st, eng->Y, S, K, eng->MT, nseg, eng->dM, eng->dBase,
                        eng->wExtHist, eng->dWExtOff, eng->wExtStride, it, eng->Z);
     BCHK(hipGetLastError());
@@ -641,7 +653,7 @@ int danse_batch_run(danse_batch* eng, void* stream) {
     // launch covers the whole run (K*S*F bins for equal D: a full chip
     // instead of S*F bins per launch).
     const size_t pitch = (size_t)eng->wStride * sizeof(cf);
-    for (int k = 0; k < K;) {
+    for (int k = eng->k0; k < eng->k1;) {
       const int D = eng->D[k];
       const size_t rowB = (size_t)F * D * sizeof(cf);
       if (!eng->doSolve[(size_t)it * K + k]) {
@@ -651,7 +663,7 @@ int danse_batch_run(danse_batch* eng, void* stream) {
         continue;
       }
       int k1 = k + 1;
-      while (k1 < K && eng->D[k1] == D && eng->doSolve[(size_t)it * K + k1]) ++k1;
+      while (k1 < eng->k1 && eng->D[k1] == D && eng->doSolve[(size_t)it * K + k1]) ++k1;
       const cd* Ry = eng->Ryy + eng->scmOff[k];
       const cd* Rn = eng->Rnn + eng->scmOff[k];
       if (!launch_filter_update_class(class_dmax(D), Ry, Rn, (k1 - k) * S * F, D, eng->gevd, eng->rank, eng->ref,
@@ -664,21 +676,63 @@ int danse_batch_run(danse_batch* eng, void* stream) {
     }
     hipLaunchKernelGGL(batch_ext_kernel, dim3(512), dim3(256), 0, st, S, K, it, eng->dM, eng->dD, eng->dExtMode,
                        eng->ref, eng->dBetaExt, eng->alphaExt, eng->wHist, eng->dWOff, eng->wStride, H, eng->wExtHist,
-                       eng->dWExtOff, eng->wExtStride, eng->tgt, eng->dTgtOff, eng->tgtStride, Mmax);
+                       eng->dWExtOff, eng->wExtStride, eng->tgt, eng->dTgtOff, eng->tgtStride, Mmax, k0,
+                       nOwn);
     BCHK(hipGetLastError());
-    const long long jobs = (long long)S * K * (nseg - 1);
+    const long long jobs = (long long)S * nOwn * (nseg - 1);
     hipLaunchKernelGGL(batch_est_kernel, dim3((unsigned)((jobs + 3) / 4)), dim3(256), 0, st, eng->Y, eng->Z, S, K,
                        eng->MT, nseg, eng->dM, eng->dBase, eng->dD, eng->wHist, eng->dWOff, eng->wStride, it + 1,
-                       eng->dWin, eng->dTw, eng->dhat, eng->dFramesTD);
+                       eng->dWin, eng->dTw, eng->dhat, eng->dFramesTD, k0, nOwn);
     BCHK(hipGetLastError());
     hipLaunchKernelGGL(batch_ola_kernel, dim3(2048), dim3(256), 0, st, eng->dFramesTD, S, K, eng->T, eng->Ns, nseg,
-                       eng->dWin, eng->dD_);
+                       eng->dWin, eng->dD_, k0, nOwn);
     BCHK(hipGetLastError());
     if (eng->clean) {
-      hipLaunchKernelGGL(batch_cost_kernel, dim3(S * K), dim3(kCostThr), 0, st, eng->clean, eng->dD_, eng->T, eng->trim,
-                         eng->dCost + (size_t)it * S * K);
+      hipLaunchKernelGGL(batch_cost_kernel, dim3(S * nOwn), dim3(kCostThr), 0, st, eng->clean, eng->dD_, eng->T,
+                         eng->trim, eng->dCost + (size_t)it * S * K, K, k0, nOwn);
       BCHK(hipGetLastError());
     }
+  }
+  return 0;
+}
+
+// Node-sharded batch DANSE: the external filters of slot `slot` (written by
+// the iteration slot - 1) of every node travel between ranks; every rank
+// computes z for all nodes, SCMs / solves / estimates for its own.
+//   pack:   own nodes k0..k1-1 -> dst [k1 - k0][S][F * Mmax] (zero padded)
+//   unpack: src [K][S][F * Mmax] -> the other nodes' slots
+int danse_batch_pack_wext(danse_batch* eng, int32_t slot, void* dst, void* stream) {
+  if (!eng || !dst) return bfail(eng, "null argument");
+  if (slot < 0 || slot > eng->iters) return bfail(eng, "slot out of range");
+  BCHK(hipSetDevice(eng->dev));
+  int Mmax = 0;
+  for (int k = 0; k < eng->K; ++k) Mmax = std::max(Mmax, eng->M[k]);
+  const size_t chunk = (size_t)eng->F * Mmax;
+  cf* d = (cf*)dst;
+  for (int k = eng->k0; k < eng->k1; ++k) {
+    cf* o = d + (size_t)(k - eng->k0) * eng->S * chunk;
+    if (eng->M[k] < Mmax) BCHK(hipMemsetAsync(o, 0, (size_t)eng->S * chunk * sizeof(cf), (hipStream_t)stream));
+    BCHK(hipMemcpy2DAsync(o, chunk * sizeof(cf), eng->wExtHist + eng->wExtOff[k] + (long long)slot * eng->F * eng->M[k],
+                          (size_t)eng->wExtStride * sizeof(cf), (size_t)eng->F * eng->M[k] * sizeof(cf), eng->S,
+                          hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  }
+  return 0;
+}
+
+int danse_batch_unpack_wext(danse_batch* eng, int32_t slot, const void* src, void* stream) {
+  if (!eng || !src) return bfail(eng, "null argument");
+  if (slot < 0 || slot > eng->iters) return bfail(eng, "slot out of range");
+  BCHK(hipSetDevice(eng->dev));
+  int Mmax = 0;
+  for (int k = 0; k < eng->K; ++k) Mmax = std::max(Mmax, eng->M[k]);
+  const size_t chunk = (size_t)eng->F * Mmax;
+  const cf* sp = (const cf*)src;
+  for (int k = 0; k < eng->K; ++k) {
+    if (k >= eng->k0 && k < eng->k1) continue;
+    BCHK(hipMemcpy2DAsync(eng->wExtHist + eng->wExtOff[k] + (long long)slot * eng->F * eng->M[k],
+                          (size_t)eng->wExtStride * sizeof(cf), sp + (size_t)k * eng->S * chunk, chunk * sizeof(cf),
+                          (size_t)eng->F * eng->M[k] * sizeof(cf), eng->S, hipMemcpyDeviceToDevice,
+                          (hipStream_t)stream));
   }
   return 0;
 }

@@ -294,6 +294,9 @@ typedef struct danse_batch_cfg {
   const float* w0;         /* initial filters, node blocks [F][D_k] complex        */
   const float* wExt0;      /* initial external filters (and targets), [F][M_k]     */
   int32_t costTrim;        /* samples trimmed at both ends in the MMSE cost (1000) */
+  int32_t k0, k1;          /* owned nodes [k0, k1) (node-sharded batch DANSE across
+                              GPUs: z for every node, SCMs / solves / estimates /
+                              cost for the owned ones); k1 <= k0: all nodes     */
 } danse_batch_cfg;
 
 typedef struct danse_batch danse_batch;
@@ -317,6 +320,16 @@ const char* danse_batch_last_error(const danse_batch* eng);
  * clean speech at each node's reference sensor) or NULL (no MMSE cost). */
 int danse_batch_set_inputs(danse_batch* eng, const float* y, const float* clean);
 int danse_batch_run(danse_batch* eng, void* stream);
+/* Iterations [it0, it1) (it0 == 0 also sets the initial state and the STFT);
+ * between two calls a node-sharded run exchanges the external filters of
+ * slot it1 (written by iteration it1 - 1):
+ *   danse_batch_pack_wext(own nodes -> dst [k1-k0][S][F*Mmax] complex),
+ *   all-gather over ranks into [K][S][F*Mmax],
+ *   danse_batch_unpack_wext(the other nodes' slots <- src).
+ * (update_external_filters_batch + batch z, d_core.py:286-326)          */
+int danse_batch_run_iters(danse_batch* eng, int32_t it0, int32_t it1, void* stream);
+int danse_batch_pack_wext(danse_batch* eng, int32_t slot, void* dst, void* stream);
+int danse_batch_unpack_wext(danse_batch* eng, int32_t slot, const void* src, void* stream);
 int danse_batch_output_bytes(danse_batch* eng, int32_t which, int32_t node, size_t* bytes);
 int danse_batch_get(danse_batch* eng, int32_t which, int32_t node, void* dst, size_t bytes, void* stream);
 

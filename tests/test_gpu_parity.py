@@ -345,3 +345,44 @@ def test_snr_replay_vs_oracle():
         e = rel_err(sig_g[key], sig_o[key])
         print('replay', key, e)
         assert e < 1e-5
+
+
+@pytest.mark.parametrize('case', BATCH_CASES, ids=lambda c: c['name'])
+def test_batch_node_sharded_equals_full(case):
+    """Node-sharded batch DANSE (two engines of one device, each owning a
+    node block, exchanging the external filters after every iteration as
+    the RCCL all-gather would) against the single-engine run: every owned
+    node's filters, estimates and costs, and every node's external filters,
+    agree (same kernels on the same bins: bit-exact expected, 1e-6 tested)."""
+    import torch
+    from danse_amd.batch import BatchEngine, node_ranges
+    sc = make_case_scene(case)
+    dp, wp = make_case_params(case)
+    dp.simType = 'batch'
+    sc.get_vad_per_frame(dp.DFTsize, dp.Ns, wp.vadMinProportionActive)
+    full = BatchEngine([sc], dp).run().outputs()[0]
+    K = len(case['M'])
+    rngs, c = node_ranges(K, 2)
+    engs = [BatchEngine([sc], dp, nodeRange=r) for r in rngs]
+    bufs = [torch.zeros(c * e.S * e.wext_chunk(), dtype=torch.complex64, device='cuda:0') for e in engs]
+    for it in range(engs[0].iters):
+        for e, b in zip(engs, bufs):
+            e.run_iters(it, it + 1)
+            e.pack_wext(it + 1, b)
+        g = torch.cat(bufs)
+        for e in engs:
+            e.unpack_wext(it + 1, g)
+    torch.cuda.synchronize()
+    exact = True
+    for e, (k0, k1) in zip(engs, rngs):
+        o = e.outputs()[0]
+        for k in range(K):
+            exact &= np.array_equal(o.wTildeExt[k], full.wTildeExt[k])
+            assert np.allclose(o.wTildeExt[k], full.wTildeExt[k], rtol=1e-6, atol=1e-7), (k0, k)
+        for k in range(k0, k1):
+            for a, b in ((o.wTilde[k], full.wTilde[k]), (o.d[:, k], full.d[:, k]), (o.dhat[:, :, k], full.dhat[:, :, k]),
+                         (o.mmseCost[:, k], full.mmseCost[:, k])):
+                exact &= np.array_equal(a, b)
+                assert np.allclose(a, b, rtol=1e-6, atol=1e-7), (k0, k)
+        e.close()
+    print(case['name'], 'bit-exact' if exact else 'within 1e-6')
