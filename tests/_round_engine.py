@@ -4,7 +4,11 @@ node-major [K][S][F] buffer -> update(r) consuming every node's spectrum), so
 that ``danse_amd.dist.ShardedRun`` can be exercised with the gloo backend on
 CPU.  Arithmetic comes from the oracle (oracle/danse_ref_cpu.py): same
 frames, same compression/OLA, same SCM recursion and filter updates; DANSE
-family only, round-synchronous schedule (no SROs)."""
+family only.  With SRO clocks (asynchronous schedule) the spectra buffer
+has the device engine's two round slots ([2][K][S][F], round r -> slot r & 1)
+and node k's update r reads sender q's spectrum of round r - zLag[r, k, q],
+so the sharded exchange of both slots is exercised; no phase compensation
+or full-sample-drift flags (protocol stand-in, not an SRO oracle)."""
 from __future__ import annotations
 
 import numpy as np
@@ -30,18 +34,19 @@ class RoundEngine:
                                    [n.neighborsIdx for n in sc0.wasn])
         self.rt = compile_rounds(ev, fs, p, K)
         self.R = self.rt.nRounds
+        self.zspec_slots = 1 if self.rt.synchronous else 2
         self.torch_device = 'cpu'
         self.zbuf = None
         self.h, self.f = p.winWOLAanalysis, p.winWOLAsynthesis
 
     def zspec_numel(self):
-        return self.K * self.S * self.F * 2
+        return self.zspec_slots * self.K * self.S * self.F * 2
 
     def set_zspec(self, t):
         self.zbuf = t
 
     def _z(self):
-        return self.zbuf.numpy().view(np.complex64).reshape(self.K, self.S, self.F)
+        return self.zbuf.numpy().view(np.complex64).reshape(self.zspec_slots, self.K, self.S, self.F)
 
     def reset(self):
         p, K, F = self.p, self.K, self.F
@@ -66,7 +71,7 @@ class RoundEngine:
             self.st.append(nodes)
 
     def bcast(self, r):
-        zv = self._z()
+        zv = self._z()[r % self.zspec_slots]
         N, Ns = self.N, self.Ns
         for s, sc in enumerate(self.scenes):
             for k in range(self.k0, self.k1):
@@ -88,7 +93,9 @@ class RoundEngine:
                 n = self.st[s][k]
                 fr, b, e = O.local_chunk(sc.wasn[k].data, int(self.rt.upEnd[r, k]), N)
                 yl = (np.fft.fft(fr * self.h[:, None], N, axis=0) / np.sqrt(Ns))[:self.F]
-                y = np.concatenate([yl] + [zv[q, s][:, None].astype(np.complex128) for q in range(K) if q != k], axis=1)
+                lag = [0 if self.rt.synchronous else int(self.rt.zLag[r, k, q]) for q in range(K)]
+                y = np.concatenate([yl] + [zv[(r - lag[q]) % self.zspec_slots, q, s][:, None].astype(np.complex128)
+                                           for q in range(K) if q != k], axis=1)
                 D = y.shape[1]
                 vad = bool(sc.wasn[k].vadPerFrame[r])
                 if vad:

@@ -17,9 +17,12 @@ import torch.multiprocessing as mp
 ROOT = Path(__file__).resolve().parent.parent
 
 
-def _case():
+def _case(sro=False):
     from golden_cases import BATTERY, _d
-    return dict(name='dist', M=[2, 2, 2, 2], dur=1.6, seed=21, danse=_d(BATTERY, nodeUpdating='asy'))
+    c = dict(name='dist', M=[2, 2, 2, 2], dur=1.6, seed=21, danse=_d(BATTERY, nodeUpdating='asy'))
+    if sro:
+        c['sros'] = [0.0, 150.0, 300.0, 450.0]
+    return c
 
 
 def _setup(case, nodes=None):
@@ -28,13 +31,13 @@ def _setup(case, nodes=None):
     dp, wp = make_case_params(case)
     scenes = []
     for sd in (case['seed'], case['seed'] + 1):
-        sc = make_scene(case['M'], sigDur=case['dur'], seed=sd, nodes=nodes)
+        sc = make_scene(case['M'], sigDur=case['dur'], seed=sd, nodes=nodes, SROperNode=case.get('sros'))
         sc.get_vad_per_frame(dp.DFTsize, dp.Ns, wp.vadMinProportionActive)
         scenes.append(sc)
     return dp, scenes
 
 
-def _worker(rank, world, port, outdir):
+def _worker(rank, world, port, outdir, sro=False):
     sys.path.insert(0, str(ROOT))
     sys.path.insert(0, str(ROOT / 'tests'))
     sys.path.insert(0, str(ROOT / 'tests' / 'golden'))
@@ -43,7 +46,7 @@ def _worker(rank, world, port, outdir):
     dist.init_process_group('gloo', rank=rank, world_size=world)
     from danse_amd.dist import ShardedRun, node_range
     from _round_engine import RoundEngine
-    case = _case()
+    case = _case(sro)
     k0, k1 = node_range(len(case['M']), world, rank)
     dp, scenes = _setup(case, nodes=list(range(k0, k1)))
     eng = RoundEngine(scenes, dp, nodeRange=(k0, k1))
@@ -56,9 +59,9 @@ def _worker(rank, world, port, outdir):
     dist.destroy_process_group()
 
 
-def _single():
+def _single(sro=False):
     from _round_engine import RoundEngine
-    dp, scenes = _setup(_case())
+    dp, scenes = _setup(_case(sro))
     eng = RoundEngine(scenes, dp)
     eng.set_zspec(torch.zeros(eng.zspec_numel(), dtype=torch.float32))
     eng.reset()
@@ -68,12 +71,16 @@ def _single():
     return eng, dp, scenes
 
 
-@pytest.mark.parametrize('world', [2, 4])
-def test_node_sharded_equals_single_process(world):
-    ref, _, _ = _single()
+@pytest.mark.parametrize('world,sro', [(2, False), (4, False), (2, True)], ids=['w2', 'w4', 'w2_sro'])
+def test_node_sharded_equals_single_process(world, sro):
+    """sro: SRO clocks (0/150/300/450 ppm), two exchanged round slots and
+    receivers reading the previous round's slot (zLag)."""
+    ref, _, _ = _single(sro)
+    if sro:
+        assert not ref.rt.synchronous and ref.zspec_slots == 2 and int(ref.rt.zLag.max()) == 1
     with tempfile.TemporaryDirectory() as td:
-        port = 29500 + (os.getpid() % 1000) + world
-        mp.spawn(_worker, args=(world, port, td), nprocs=world, join=True)
+        port = 29500 + (os.getpid() % 1000) + world + (7 if sro else 0)
+        mp.spawn(_worker, args=(world, port, td, sro), nprocs=world, join=True)
         for s in range(ref.S):
             for k in range(ref.K):
                 d = np.load(Path(td) / f'd_{s}_{k}.npy')
