@@ -117,6 +117,14 @@ SIGNATURES = {
     'danse_tz_create': (_c_i32, [_c_i32, ctypes.c_void_p, ctypes.c_void_p, _c_i32, _c_i32,
                                  ctypes.POINTER(ctypes.c_void_p)]),
     'danse_tz_destroy': (None, [ctypes.c_void_p]),
+    'danse_metrics_last_error': (ctypes.c_char_p, []),
+    'danse_snr': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, _c_i32,
+                           ctypes.c_void_p, ctypes.c_void_p]),
+    'danse_fwsnrseg_frames': (_c_i32, [ctypes.c_int64, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                       ctypes.POINTER(_c_i32)]),
+    'danse_fwsnrseg': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, _c_i32, ctypes.c_double,
+                                ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_void_p, ctypes.c_void_p,
+                                ctypes.c_void_p]),
     'danse_tz_last_error': (ctypes.c_char_p, [ctypes.c_void_p]),
     'danse_tz_ir': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p, _c_i32, _c_i32, ctypes.c_void_p, ctypes.c_void_p]),
     'danse_tz_compress': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, _c_i32, _c_i32, _c_i32,

@@ -2,7 +2,8 @@
 
 ``hipcc -c -fPIC`` of ``csrc/danse_engine.hip`` (online engine, C-ABI, bcast /
 operator kernels), ``csrc/batch.hip`` (batch-mode engine), ``csrc/dxcp.hip`` (DXCP-PhaT SRO
-estimator), ``csrc/tz.hip`` (T(z) few-samples compression) and of
+estimator), ``csrc/tz.hip`` (T(z) few-samples compression), ``csrc/metrics.hip``
+(SNR / fwSNRseg) and of
 ``csrc/update_class.hip`` once per filter-size class
 (``-DDANSE_DMAX=N``, N = 1..16 and 24..64 in steps of 8, see
 ``csrc/classes.hpp``), in parallel, then one
@@ -31,7 +32,8 @@ FLAGS = ['--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC']
 def _units():
     """(object name, source, extra flags) of every translation unit."""
     u = [('danse_engine.o', CSRC / 'danse_engine.hip', []), ('batch.o', CSRC / 'batch.hip', []),
-         ('dxcp.o', CSRC / 'dxcp.hip', []), ('tz.o', CSRC / 'tz.hip', [])]
+         ('dxcp.o', CSRC / 'dxcp.hip', []), ('tz.o', CSRC / 'tz.hip', []),
+         ('metrics.o', CSRC / 'metrics.hip', [])]
     for n in CLASSES:
         # lane-per-bin classes: no SLP packing of the float32 complex math
         # (the packed pairs need swapped operand copies; with them the eigen

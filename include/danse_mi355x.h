@@ -366,6 +366,24 @@ int danse_tz_ir(danse_tz* eng, const float* wHat, int32_t B, int32_t M, float* w
 int danse_tz_compress(danse_tz* eng, const float* yq, const float* wIR, int32_t B, int32_t M, int32_t L, float* z,
                       void* stream);
 
+/* ---- Enhancement metrics, float64 (csrc/metrics.hip).
+ * danse_snr replaces get_snr(s, n, vad) (danse_toolbox/d_eval.py:573-624):
+ *     s, n: [C][T] double (device; the reference's [T x C] transposed)
+ *     vad:  [C][T] uint8 (device) or NULL (bypassVADuse: whole signal)
+ *     out:  [C] double (device): 10 log10(mean s^2 / mean n^2) over vad.
+ * danse_fwsnrseg replaces get_fwsnrseg(clean, enhanced, fs, frameLen,
+ *   overlap, gamma) (d_eval.py:660-778) for nSig signal pairs at once:
+ *     clean, enhanced: [nSig][T] double (device)
+ *     perFrame: [nSig][nFrames] double (device): the clipped per-frame values
+ *     mean:     [nSig] double (device) or NULL: np.mean over frames (the
+ *               fwSNRseg.before / .after of get_metrics, d_eval.py:236-244).
+ * danse_fwsnrseg_frames gives nFrames = int(T / skip - W / skip).         */
+const char* danse_metrics_last_error(void);
+int danse_snr(const double* s, const double* n, const uint8_t* vad, int64_t T, int32_t C, double* out, void* stream);
+int danse_fwsnrseg_frames(int64_t T, double fs, double frameLen, double overlap, int32_t* nFrames);
+int danse_fwsnrseg(const double* clean, const double* enhanced, int64_t T, int32_t nSig, double fs, double frameLen,
+                   double overlap, double gamma, double* perFrame, double* mean, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

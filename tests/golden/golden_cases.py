@@ -198,6 +198,34 @@ def tz_inputs(case):
 # online cases whose schedule-derived dv fields (SRO estimates / residuals,
 # flag iterations, first-update instant, MSE-cost arrays) and whole-signal
 # STFTs (yinSTFT, bins subsampled) are dumped as fields_<case>.npz
+# enhancement metrics (d_eval.py get_snr / get_fwsnrseg): seeded signals
+METRIC_CASES = [
+    dict(name='metrics_fw_16k', T=16000, fs=16000.0, seed=301, noise=0.3, same=0),
+    dict(name='metrics_fw_ragged', T=24037, fs=16000.0, seed=302, noise=0.05, same=4000),
+    dict(name='metrics_fw_8k_frame20', T=12011, fs=8000.0, seed=303, noise=1.0, same=0, frameLen=0.02,
+         overlap=0.5, gamma=0.3),
+]
+
+
+def metric_inputs(case):
+    """clean: bursts of low-passed noise (speech-like on/off); enhanced: the
+    clean signal scaled, plus noise, identical to it over the first `same`
+    samples (exercises the eps clamp and the 35 dB clip); s / n / vad for
+    get_snr: [T x 3]."""
+    rng = np.random.default_rng(case['seed'])
+    T = case['T']
+    x = rng.standard_normal(T)
+    x = np.convolve(x, np.ones(8) / 8, mode='same')
+    env = (np.sin(2 * np.pi * np.arange(T) / 3000.0) > -0.2).astype(float)
+    clean = x * env
+    enh = 0.8 * clean + case['noise'] * rng.standard_normal(T)
+    enh[:case['same']] = clean[:case['same']]
+    s = rng.standard_normal((T, 3)) * np.array([1.0, 0.5, 2.0])
+    n = rng.standard_normal((T, 3)) * np.array([0.3, 0.7, 1.5])
+    vad = (rng.random((T // 100 + 1, 3)) > 0.4).repeat(100, axis=0)[:T]
+    return clean, enh, s, n, vad
+
+
 FIELD_CASES = ['online_C_sro_comp_asy', 'online_C_sro_noflags_seq', 'online_B_k4m3_seq', 'online_ragged_asy_r2',
                'online_E_fs_L64_asy']
 FIELD_STFT_BIN_STEP = 37

@@ -24,6 +24,7 @@ import _refharness as H  # noqa: E402
 from danse_amd.scene import make_scene, scene_digest  # noqa: E402
 from golden_cases import ONLINE_CASES, BATCH_CASES, SRO_EVENT_CASES, KAT_CASES, kat_inputs  # noqa: E402
 from golden_cases import DXCP_CASES, dxcp_inputs, TZ_CASES, tz_inputs  # noqa: E402
+from golden_cases import METRIC_CASES, metric_inputs  # noqa: E402
 from golden_cases import FIELD_CASES, FIELD_STFT_BIN_STEP  # noqa: E402
 
 
@@ -168,6 +169,16 @@ def _run_tz(ns, case):
     return {'z': z, 'wIR': wIR}
 
 
+def _run_metrics(ns, case):
+    import danse_toolbox.d_eval as ev   # importable once the reference is loaded
+    clean, enh, s, n, vad = metric_inputs(case)
+    kw = {k: case[k] for k in ('frameLen', 'overlap', 'gamma') if k in case}
+    fw = ev.get_fwsnrseg(clean, enh, case['fs'], **kw)
+    return {'fw': np.asarray(fw, dtype=np.float64), 'fwMean': np.mean(fw),
+            'snr': np.asarray(ev.get_snr(s, n, vad)), 'snrAll': np.asarray(ev.get_snr(s, n, vad, bypassVADuse=True)),
+            'snr1': np.asarray(ev.get_snr(s[:, 0], n[:, 0], vad[:, 0]))}
+
+
 def main():
     ns = H.load()
     only = sys.argv[1:]
@@ -177,6 +188,7 @@ def main():
            [('kat', c, _run_kat) for c in KAT_CASES] + \
            [('dxcp', c, _run_dxcp) for c in DXCP_CASES] + \
            [('tz', c, _run_tz) for c in TZ_CASES] + \
+           [('metrics', c, _run_metrics) for c in METRIC_CASES] + \
            [('fields', dict(name=f'fields_{c}', src=c), lambda ns, c: _run_fields(ns, c['src'])) for c in FIELD_CASES]
     for kind, case, fn in jobs:
         name = case['name']

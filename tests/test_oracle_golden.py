@@ -123,3 +123,22 @@ def test_tz_oracle_matches_reference(case, golden_dir):
     assert rel_err(z, g['z']) < TOL
     if case['update']:
         assert rel_err(T.dist_fct_approx_closed(wHat, h, f, case['Ns']), g['wIR']) < TOL
+
+
+@pytest.mark.parametrize('case', __import__('golden_cases').METRIC_CASES, ids=lambda c: c['name'])
+def test_metrics_oracle_vs_reference(case, golden_dir):
+    """oracle/metrics_ref.py (get_snr, get_fwsnrseg) against the reference's
+    own d_eval functions run on the same inputs."""
+    from golden_cases import metric_inputs
+    from oracle import metrics_ref as MR
+    g = np.load(golden_dir / f"{case['name']}.npz")
+    clean, enh, s, n, vad = metric_inputs(case)
+    kw = {k: case[k] for k in ('frameLen', 'overlap', 'gamma') if k in case}
+    fw = MR.get_fwsnrseg(clean, enh, case['fs'], **kw)
+    assert fw.shape == g['fw'].shape
+    assert np.max(np.abs(fw - g['fw'])) <= 1e-9
+    assert np.allclose(MR.get_snr(s, n, vad), g['snr'], rtol=1e-12, atol=1e-12)
+    assert np.allclose(MR.get_snr(s, n, vad, bypassVADuse=True), g['snrAll'], rtol=1e-12, atol=1e-12)
+    assert np.allclose(MR.get_snr(s[:, 0], n[:, 0], vad[:, 0]), g['snr1'], rtol=1e-12, atol=1e-12)
+    if case['same']:
+        assert np.any(g['fw'] == 35.0)   # identical frames clip at 35 dB
