@@ -7,6 +7,8 @@
 * ``get_fwsnrseg(cleanSig, enhancedSig, fs, frameLen=0.03, overlap=0.75,
   gamma=0.2)`` -- ``get_fwsnrseg`` (``d_eval.py:660-778``): the per-frame
   values of one signal pair.
+* ``get_metrics(...)`` -- ``get_metrics`` (``d_eval.py:70-373``) for its
+  'snr' and 'fwSNRseg' entries, with the reference's argument quirks.
 * ``fwsnrseg_batch(clean, enhanced, fs, ...)`` -- device tensors [B][T] in,
   per-frame [B][nFrames] and mean [B] device tensors out (the E battery's
   ΔfwSNRseg per scene without leaving the GPU).
@@ -107,3 +109,71 @@ def get_snr(s, n, vad=None, bypassVADuse=False, device=0):
                          ctypes.c_void_p(out.data_ptr()), _stream(torch, dev)))
     o = out.cpu().numpy()
     return float(o[0]) if C == 1 else o
+
+
+class Metric:
+    """Field names of the reference's ``Metric`` (``d_eval.py:20-33``)."""
+
+    def __init__(self):
+        self.best = None
+        self.before = self.after = self.diff = 0.
+        self.afterLocal = self.diffLocal = self.afterCentr = self.diffCentr = 0.
+        self.afterSSBC = self.diffSSBC = 0.
+        self.dynamicFlag = False
+
+
+def get_metrics(clean, noiseOnly, noisy, filtSpeech, filtNoise, filtSpeech_c=None, filtNoise_c=None,
+                filtSpeech_l=None, filtNoise_l=None, filtSpeech_ssbc=None, filtNoise_ssbc=None, enhan=None,
+                enhan_c=None, enhan_l=None, enhan_ssbc=None, fs=16e3, vad=None, dynamic=None, startIdx=0,
+                endIdx=None, gamma=0.2, fLen=0.03, metricsToPlot=('snr', 'stoi'), bestPerfData=None, k=None,
+                device=0):
+    """``get_metrics`` (``danse_toolbox/d_eval.py:70-373``) for the 'snr' and
+    'fwSNRseg' entries, on the device: every fwSNRseg pair of the call in
+    ONE launch.  Reproduces the reference's argument handling: SNR with
+    ``bypassVADuse = True`` (hard-coded, line 205) and ``get_fwsnrseg(clean,
+    x, fs, fLen, gamma)`` where the positional ``gamma`` lands in the
+    ``overlap`` parameter (lines 236-242: overlap = gamma, gamma = 0.2).
+    'stoi' / 'pesq' / 'sisnr', dynamic metrics and bestPerfData raise."""
+    import torch
+    want = set(metricsToPlot)
+    unsupported = want - {'snr', 'fwSNRseg'}
+    if unsupported:
+        raise NotImplementedError(f'metrics {sorted(unsupported)} are not on the device path (snr, fwSNRseg are)')
+    if dynamic is not None or bestPerfData is not None:
+        raise NotImplementedError('dynamic metrics / bestPerfData are not on the device path')
+    if endIdx is None:
+        endIdx = np.asarray(clean).shape[0]
+    sl = slice(startIdx, endIdx)
+
+    def cut(x):
+        return None if x is None else np.asarray(x, dtype=np.float64)[sl]
+    clean, noiseOnly, noisy = cut(clean), cut(noiseOnly), cut(noisy)
+    fS, fN = cut(filtSpeech), cut(filtNoise)
+    enhan = cut(enhan) if enhan is not None else fS + fN
+    enh = {'': enhan, 'Centr': cut(enhan_c), 'Local': cut(enhan_l), 'SSBC': cut(enhan_ssbc)}
+    filt = {'Centr': (cut(filtSpeech_c), cut(filtNoise_c)), 'Local': (cut(filtSpeech_l), cut(filtNoise_l)),
+            'SSBC': (cut(filtSpeech_ssbc), cut(filtNoise_ssbc))}
+    out = {}
+    if 'snr' in want:
+        snr = Metric()
+        snr.before = get_snr(clean, noiseOnly, vad, True, device)
+        snr.after = get_snr(fS, fN, vad, True, device)
+        snr.diff = snr.after - snr.before
+        for tag in ('Centr', 'Local', 'SSBC'):
+            if enh[tag] is not None:
+                setattr(snr, 'after' + tag, get_snr(filt[tag][0], filt[tag][1], vad, True, device))
+        out['snr'] = snr
+    if 'fwSNRseg' in want:
+        fw = Metric()
+        pairs = [('before', noisy), ('after', enhan)] + \
+                [('after' + t, enh[t]) for t in ('Centr', 'Local', 'SSBC') if enh[t] is not None]
+        # clean_c / clean_l / clean_ssbc are the same slice of clean (d_eval.py:171-174)
+        c = np.stack([clean.ravel()] * len(pairs))
+        e = np.stack([np.asarray(x, dtype=np.float64).ravel() for _, x in pairs])
+        _, mean = fwsnrseg_batch(torch.from_numpy(c), torch.from_numpy(e), fs, fLen, gamma, 0.2, device)
+        mean = mean.cpu().numpy()
+        for (name, _), m in zip(pairs, mean):
+            setattr(fw, name, float(m))
+        fw.diff = fw.after - fw.before
+        out['fwSNRseg'] = fw
+    return out

@@ -226,6 +226,26 @@ def metric_inputs(case):
     return clean, enh, s, n, vad
 
 
+# get_metrics ('snr', 'fwSNRseg' entries) on seeded DANSE-like outputs
+GETMETRICS_CASE = dict(name='metrics_get_metrics', T=32000, fs=16000.0, seed=311, startIdx=2000, endIdx=30500)
+
+
+def get_metrics_inputs(case):
+    rng = np.random.default_rng(case['seed'])
+    T = case['T']
+    x = np.convolve(rng.standard_normal(T), np.ones(6) / 6, mode='same')
+    env = (np.sin(2 * np.pi * np.arange(T) / 4000.0) > -0.3).astype(float)
+    clean = x * env
+    noise = 0.5 * rng.standard_normal(T)
+    kw = dict(clean=clean, noiseOnly=noise, noisy=clean + noise,
+              filtSpeech=0.9 * clean + 0.02 * rng.standard_normal(T), filtNoise=0.1 * noise,
+              filtSpeech_c=0.95 * clean, filtNoise_c=0.05 * noise, filtSpeech_l=0.8 * clean, filtNoise_l=0.3 * noise)
+    kw['enhan_c'] = kw['filtSpeech_c'] + kw['filtNoise_c']
+    kw['enhan_l'] = kw['filtSpeech_l'] + kw['filtNoise_l']
+    kw['vad'] = env.astype(bool)
+    return kw
+
+
 FIELD_CASES = ['online_C_sro_comp_asy', 'online_C_sro_noflags_seq', 'online_B_k4m3_seq', 'online_ragged_asy_r2',
                'online_E_fs_L64_asy']
 FIELD_STFT_BIN_STEP = 37

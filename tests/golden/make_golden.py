@@ -24,7 +24,7 @@ import _refharness as H  # noqa: E402
 from danse_amd.scene import make_scene, scene_digest  # noqa: E402
 from golden_cases import ONLINE_CASES, BATCH_CASES, SRO_EVENT_CASES, KAT_CASES, kat_inputs  # noqa: E402
 from golden_cases import DXCP_CASES, dxcp_inputs, TZ_CASES, tz_inputs  # noqa: E402
-from golden_cases import METRIC_CASES, metric_inputs  # noqa: E402
+from golden_cases import METRIC_CASES, metric_inputs, GETMETRICS_CASE, get_metrics_inputs  # noqa: E402
 from golden_cases import FIELD_CASES, FIELD_STFT_BIN_STEP  # noqa: E402
 
 
@@ -179,6 +179,17 @@ def _run_metrics(ns, case):
             'snr1': np.asarray(ev.get_snr(s[:, 0], n[:, 0], vad[:, 0]))}
 
 
+def _run_get_metrics(ns, case):
+    import danse_toolbox.d_eval as ev
+    m = ev.get_metrics(**get_metrics_inputs(case), fs=case['fs'], startIdx=case['startIdx'], endIdx=case['endIdx'],
+                       metricsToPlot=['snr', 'fwSNRseg'])
+    out = {}
+    for key in ('snr', 'fwSNRseg'):
+        for fld in ('before', 'after', 'diff', 'afterCentr', 'afterLocal'):
+            out[f'{key}_{fld}'] = np.float64(getattr(m[key], fld))
+    return out
+
+
 def main():
     ns = H.load()
     only = sys.argv[1:]
@@ -189,6 +200,7 @@ def main():
            [('dxcp', c, _run_dxcp) for c in DXCP_CASES] + \
            [('tz', c, _run_tz) for c in TZ_CASES] + \
            [('metrics', c, _run_metrics) for c in METRIC_CASES] + \
+           [('metrics', GETMETRICS_CASE, _run_get_metrics)] + \
            [('fields', dict(name=f'fields_{c}', src=c), lambda ns, c: _run_fields(ns, c['src'])) for c in FIELD_CASES]
     for kind, case, fn in jobs:
         name = case['name']

@@ -53,3 +53,19 @@ def test_metrics_errors():
         DM.fwsnrseg_frames(300, 16000.0)          # shorter than one frame
     with pytest.raises(DanseError):
         DM.fwsnrseg_frames(16000, 16000.0, overlap=1.0)
+
+
+def test_get_metrics_vs_reference(golden_dir):
+    """danse_amd.metrics.get_metrics ('snr', 'fwSNRseg'; all fwSNRseg pairs in
+    one launch) against the reference's get_metrics on the same inputs."""
+    from golden_cases import GETMETRICS_CASE as case, get_metrics_inputs
+    from danse_amd import metrics as DM
+    g = np.load(golden_dir / f"{case['name']}.npz")
+    m = DM.get_metrics(**get_metrics_inputs(case), fs=case['fs'], startIdx=case['startIdx'], endIdx=case['endIdx'],
+                       metricsToPlot=['snr', 'fwSNRseg'])
+    for key in ('snr', 'fwSNRseg'):
+        for fld in ('before', 'after', 'diff', 'afterCentr', 'afterLocal'):
+            v, r = getattr(m[key], fld), float(g[f'{key}_{fld}'])
+            assert abs(v - r) <= 1e-9 * max(1.0, abs(r)), (key, fld, v, r)
+    with pytest.raises(NotImplementedError):
+        DM.get_metrics(**get_metrics_inputs(case), fs=case['fs'], metricsToPlot=['stoi'])

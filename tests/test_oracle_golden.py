@@ -142,3 +142,25 @@ def test_metrics_oracle_vs_reference(case, golden_dir):
     assert np.allclose(MR.get_snr(s[:, 0], n[:, 0], vad[:, 0]), g['snr1'], rtol=1e-12, atol=1e-12)
     if case['same']:
         assert np.any(g['fw'] == 35.0)   # identical frames clip at 35 dB
+
+
+def test_get_metrics_quirks_vs_reference(golden_dir):
+    """The reference's get_metrics ('snr', 'fwSNRseg'): SNR over the whole
+    trimmed signal (bypassVADuse hard-coded True) and fwSNRseg with the
+    positional gamma landing in `overlap` (d_eval.py:205,236-242), restated
+    with the oracle functions."""
+    from golden_cases import GETMETRICS_CASE as case, get_metrics_inputs
+    from oracle import metrics_ref as MR
+    g = np.load(golden_dir / f"{case['name']}.npz")
+    kw = get_metrics_inputs(case)
+    sl = slice(case['startIdx'], case['endIdx'])
+    fs = case['fs']
+    c = kw['clean'][sl]
+    assert np.isclose(MR.get_snr(kw['clean'][sl], kw['noiseOnly'][sl]), g['snr_before'], rtol=1e-12)
+    assert np.isclose(MR.get_snr(kw['filtSpeech'][sl], kw['filtNoise'][sl]), g['snr_after'], rtol=1e-12)
+    assert np.isclose(MR.get_snr(kw['filtSpeech_c'][sl], kw['filtNoise_c'][sl]), g['snr_afterCentr'], rtol=1e-12)
+    enh = kw['filtSpeech'][sl] + kw['filtNoise'][sl]
+    for fld, e in (('before', kw['noisy'][sl]), ('after', enh), ('afterCentr', kw['enhan_c'][sl]),
+                   ('afterLocal', kw['enhan_l'][sl])):
+        v = np.mean(MR.get_fwsnrseg(c, e, fs, 0.03, 0.2))   # overlap = gamma = 0.2
+        assert abs(v - g[f'fwSNRseg_{fld}']) <= 1e-9, fld
