@@ -81,6 +81,14 @@ WORKLOADS = {
               desc='D: batch GEVD-DANSE r1, K=32 x 8 mics (D=39), 20 iterations, asy, 10.01 s'),
     'E_L64': dict(M=[2, 3], dur=10.0, nodeUpdating='asy', extra=dict(broadcastType='fewSamples', broadcastLength=64),
                   desc='E: GEVD-DANSE r1, K=2, MK=[2,3], fewSamples L=64 (T(z)), asy, 10 s'),
+    # the battery's SRO setting (config_files/sandbox_config_battery20230919.yaml:24-25): node 2 at
+    # 200 ppm, Oracle estimates, compensation with full-sample-drift flags (no centralised family:
+    # centralised estimates under SRO clocks are not on the device path)
+    'E_L64_sro200': dict(M=[2, 3], dur=10.0, nodeUpdating='asy', sros=[0.0, 200.0],
+                         extra=dict(broadcastType='fewSamples', broadcastLength=64, compensateSROs=True,
+                                    includeFSDflags=True),
+                         desc='E: GEVD-DANSE r1, K=2, MK=[2,3], fewSamples L=64, SROs [0, 200] ppm + compensation, '
+                              'asy, 10 s'),
 }
 
 
