@@ -60,6 +60,7 @@ class DanseBatchCfg(ctypes.Structure):
         ('costTrim', _c_i32),
         ('k0', _c_i32),
         ('k1', _c_i32),
+        ('tgt0', ctypes.c_void_p),
     ]
 
 

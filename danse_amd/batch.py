@@ -83,12 +83,20 @@ class BatchEngine:
             doSolve[:] = 1
         self._doSolve = doSolve
         fi = dict(initType=p.filterInitType, fixedValue=p.filterInitFixedValue)
-        if p.filterInitType == 'random':
-            raise NotImplementedError("filterInitType 'random' in batch mode (the online engine supports it)")
-        self._w0 = _cf32(np.concatenate([init_complex_filter((F, self.D[k]), p.referenceSensor, **fi).ravel()
-                                         for k in range(K)]))
-        self._wExt0 = _cf32(np.concatenate([init_complex_filter((F, self.M[k]), p.referenceSensor, **fi).ravel()
-                                            for k in range(K)]))
+        # 'random' draws over the reference's whole (F, nIter + 1, D) history
+        # (init_from_wasn, d_classes.py:664-700) and batch DANSE starts from its
+        # slot 0; the other init types are the same in every slot
+        Hr = max(self.iters + 1, self.nIter + 1)
+
+        def first(D):
+            if p.filterInitType == 'random':
+                return init_complex_filter((F, Hr, D), p.referenceSensor, **fi)[:, 0, :]
+            return init_complex_filter((F, D), p.referenceSensor, **fi)
+        self._w0 = _cf32(np.concatenate([first(self.D[k]).ravel() for k in range(K)]))
+        self._wExt0 = _cf32(np.concatenate([first(self.M[k]).ravel() for k in range(K)]))
+        # wTildeExtTarget: its own (F, M) draw (d_classes.py:702-708)
+        self._tgt0 = _cf32(np.concatenate([init_complex_filter((F, self.M[k]), p.referenceSensor, **fi).ravel()
+                                           for k in range(K)]))
         extMode = []
         for k in range(K):
             if p.onlyBroadcastRefSensorSigs:
@@ -120,6 +128,7 @@ class BatchEngine:
         c.vad = _ptr(self._vad, ctypes.c_uint8)
         c.doSolve = _ptr(self._doSolve, ctypes.c_uint8)
         c.w0, c.wExt0 = _ptr(self._w0, ctypes.c_float), _ptr(self._wExt0, ctypes.c_float)
+        c.tgt0 = self._tgt0.ctypes.data_as(ctypes.c_void_p)
         c.costTrim = int(costTrim)
         c.k0, c.k1 = self.k0, self.k1
         self._cfg = c

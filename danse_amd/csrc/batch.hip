@@ -414,7 +414,7 @@ struct danse_batch {
   int* dDiag = nullptr;
   const float* y = nullptr;
   const float* clean = nullptr;
-  std::vector<cf> w0, wExt0;   // host initial filters (per node, concatenated)
+  std::vector<cf> w0, wExt0, tgt0;   // host initial filters / external-filter targets (per node, concatenated)
 };
 
 static thread_local std::string g_berr;
@@ -510,6 +510,9 @@ int danse_batch_create(const danse_batch_cfg* c, int device, danse_batch** out) 
       eng->w0[i] = c->w0 ? cf{c->w0[2 * i], c->w0[2 * i + 1]} : cf{0.0f, 0.0f};
     for (long long i = 0; i < b; ++i)
       eng->wExt0[i] = c->wExt0 ? cf{c->wExt0[2 * i], c->wExt0[2 * i + 1]} : cf{0.0f, 0.0f};
+    eng->tgt0 = eng->wExt0;
+    if (c->tgt0)
+      for (long long i = 0; i < b; ++i) eng->tgt0[i] = cf{c->tgt0[2 * i], c->tgt0[2 * i + 1]};
   }
   // device buffers
   BCHK(balloc(&eng->dM, K)); BCHK(balloc(&eng->dBase, K)); BCHK(balloc(&eng->dD, K)); BCHK(balloc(&eng->dExtMode, K));
@@ -628,7 +631,7 @@ int danse_batch_run_iters(danse_batch* eng, int32_t it0, int32_t it1, void* stre
                           (size_t)F * eng->D[k] * sizeof(cf), hipMemcpyHostToDevice, st));
       BCHK(hipMemcpyAsync(eng->wExtHist + (long long)s * eng->wExtStride + eng->wExtOff[k], eng->wExt0.data() + b,
                           (size_t)F * eng->M[k] * sizeof(cf), hipMemcpyHostToDevice, st));
-      BCHK(hipMemcpyAsync(eng->tgt + (long long)s * eng->tgtStride + eng->tgtOff[k], eng->wExt0.data() + b,
+      BCHK(hipMemcpyAsync(eng->tgt + (long long)s * eng->tgtStride + eng->tgtOff[k], eng->tgt0.data() + b,
                           (size_t)F * eng->M[k] * sizeof(cf), hipMemcpyHostToDevice, st));
       a += (long long)F * eng->D[k];
       b += (long long)F * eng->M[k];

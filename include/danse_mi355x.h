@@ -297,6 +297,8 @@ typedef struct danse_batch_cfg {
   int32_t k0, k1;          /* owned nodes [k0, k1) (node-sharded batch DANSE across
                               GPUs: z for every node, SCMs / solves / estimates /
                               cost for the owned ones); k1 <= k0: all nodes     */
+  const float* tgt0;       /* initial external-filter targets (wTildeExtTarget,
+                              d_classes.py:702-708), layout of wExt0; NULL: wExt0 */
 } danse_batch_cfg;
 
 typedef struct danse_batch danse_batch;

@@ -94,6 +94,9 @@ BATCH_CASES = [
          danse=_d(BATTERY, simType='batch', nodeUpdating='asy', maxBatchUpdates=5)),
     dict(name='batch_k3_seq_mwf', M=[1, 2, 3], dur=2.01, seed=7,
          danse=_d(BATTERY, simType='batch', nodeUpdating='seq', maxBatchUpdates=4, performGEVD=False)),
+    # random filter init: slot 0 of the reference's (F, nIter + 1, D) seed-0 draw
+    dict(name='batch_k3_random_init_asy', M=[2, 3, 2], dur=2.01, seed=8,
+         danse=_d(BATTERY, simType='batch', nodeUpdating='asy', maxBatchUpdates=4, filterInitType='random')),
 ]
 
 SRO_EVENT_CASES = [
