@@ -154,3 +154,17 @@ def test_yaml_config_loads():
     assert p.is_fully_connected_wasn()
     assert p.danseParams.Ns == 512 and p.danseParams.performGEVD
     assert list(p.wasnParams.nSensorPerNode) == [1, 1]
+
+
+def test_get_metrics_rejects_metrics_off_the_device_path():
+    """eSTOI / PESQ / SI-SNR, dynamic metrics and bestPerfData raise before
+    any device work (danse_amd/metrics.py get_metrics)."""
+    import numpy as np
+    import pytest
+    from danse_amd import metrics as DM
+    x = np.zeros(4000)
+    for m in (['stoi'], ['pesq'], ['snr', 'sisnr']):
+        with pytest.raises(NotImplementedError):
+            DM.get_metrics(x, x, x, x, x, metricsToPlot=m)
+    with pytest.raises(NotImplementedError):
+        DM.get_metrics(x, x, x, x, x, metricsToPlot=['snr'], dynamic=object())
