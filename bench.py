@@ -40,6 +40,7 @@ sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md, chip-level parameters
 FP32_VALU_PEAK_TFS = 157.3    # ibid., peak FP32 (vector)
+FP32_MFMA_PEAK_TFS = 157.3    # ibid., peak FP32 (matrix, f32-input MFMA: the vector rate on gfx950)
 
 
 def _battery_params(M, nodeUpdating='asy', **extra):
@@ -167,6 +168,12 @@ def main():
     args = ap.parse_args()
     if args.cpu_only:
         wl = WORKLOADS[args.workload]
+        if wl.get('batch'):
+            dp, wp = _battery_params(wl['M'], wl['nodeUpdating'])
+            dp.simType = 'batch'
+            dp.maxBatchUpdates = wl['iters']
+            print(json.dumps(cpu_baseline_batch(wl['M'], wl, dp, wp, args.cpu_seconds)))
+            return
         dp, wp = _wl_params(wl)
         print(json.dumps(cpu_baseline(wl['M'], wl, dp, wp, args.cpu_seconds, args.rounds)))
         return
@@ -248,8 +255,10 @@ def cpu_child(workload, seconds, rounds):
     env = dict(os.environ, HIP_VISIBLE_DEVICES='', CUDA_VISIBLE_DEVICES='', ROCR_VISIBLE_DEVICES='')
     for k in ('RANK', 'WORLD_SIZE', 'LOCAL_RANK'):
         env.pop(k, None)
-    cp = subprocess.run([sys.executable, str(ROOT / 'bench.py'), '--cpu-only', '--workload', workload,
-                         '--cpu-seconds', str(seconds), '--rounds', str(rounds)],
+    cmd = [sys.executable, str(ROOT / 'bench.py'), '--cpu-only', '--workload', workload, '--cpu-seconds', str(seconds)]
+    if rounds is not None:
+        cmd += ['--rounds', str(rounds)]
+    cp = subprocess.run(cmd,
                         env=env, capture_output=True, text=True)
     try:
         return json.loads(cp.stdout.strip().splitlines()[-1])
@@ -445,7 +454,36 @@ def bench_batch(args, wl, S, rank, world, local, dist):
     F = eng.F
     fu_per_step = S * (1 if byNodes else world) * K * eng.nseg * F * eng.iters
     D = M[0] + K - 1
-    herk_flops = S * (eng.k1 - eng.k0) * eng.iters * 4.0 * F * D * (D + 1) * eng.nseg   # SURVEY §8d (Hermitian half)
+    # ---- roofline of the dominant kernels from live HIP events on the run's
+    # stream (danse_batch_set_timing: one event per phase boundary of every
+    # iteration), in a separate pass after the timed steps
+    eng.set_timing(True)
+    step()
+    torch.cuda.synchronize()
+    ph = eng.phase_ms()
+    eng.set_timing(False)
+    nOwn = eng.k1 - eng.k0
+    it = eng.iters
+    # HERK (Hermitian half) 4 F D (D + 1) T flops per node per iteration
+    herk_flops = S * nOwn * 4.0 * F * D * (D + 1) * eng.nseg
+    herk_tfs = herk_flops / (ph['herk'] / it * 1e-3) / 1e12
+    # GEVD solve (rank 1), LAPACK count as in the online roofline: (32/3) D^3 + 12 D^2 per bin
+    solve_flops = S * nOwn * F * (32.0 / 3.0 * D ** 3 + 12.0 * D * D)
+    solve_tfs = solve_flops / (ph['solve'] / it * 1e-3) / 1e12
+    # dhat: read Y (the node's M channels) + Z (K - 1 fused), write dhat: 8 (D + 1) bytes per (node, bin, frame)
+    dhat_bytes = S * nOwn * F * (eng.nseg - 1) * 8.0 * (D + 1)
+    dhat_gbs = dhat_bytes / (ph['dhat'] / it * 1e-3) / 1e9
+    roof = {'bound': 'mfma', 'kernel': 'herk_kernel (Y.Y^H, f32 MFMA 16x16x4)', 'achieved': herk_tfs,
+            'peak': FP32_MFMA_PEAK_TFS, 'unit': 'TFLOP/s', 'frac': herk_tfs / FP32_MFMA_PEAK_TFS, 'traffic': None,
+            'avg_launch_ms': ph['herk'] / it, 'alg_flops_per_launch': herk_flops,
+            'phase_ms_per_iteration': {k: v / it for k, v in ph.items()},
+            'solve': {'kernel': 'filter_update_kernel_2d (GEVD rank 1)', 'bound': 'valu', 'achieved': solve_tfs,
+                      'peak': FP32_VALU_PEAK_TFS, 'unit': 'TFLOP/s', 'frac': solve_tfs / FP32_VALU_PEAK_TFS},
+            'dhat': {'kernel': 'batch_dhat_kernel', 'bound': 'hbm', 'achieved': dhat_gbs, 'peak': HBM_PEAK_GBS,
+                     'unit': 'GB/s', 'frac': dhat_gbs / HBM_PEAK_GBS}}
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        cpu = cpu_child(args.workload, args.cpu_seconds, None)
     if rank == 0:
         line = {
             'metric': 'DANSE frame-updates/sec (nodes x bins)', 'value': fu_per_step * args.steps / el,
@@ -457,15 +495,52 @@ def bench_batch(args, wl, S, rank, world, local, dist):
             'config': {'workload': wl['desc'], 'wasns_per_gpu': S, 'K': K, 'M': M[0], 'D': D, 'bins': F,
                        'frames': eng.nseg, 'iterations': eng.iters,
                        'shard': 'nodes' if byNodes else 'replicas'},
-            'roofline': None,
-            'herk_alg_flops_per_step_per_gpu': herk_flops,
-            'cpu_baseline': None,
+            'roofline': roof,
+            'cpu_baseline': cpu,
             'scene_gen_s': tScene,
         }
         print(json.dumps(line), flush=True)
     eng.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def cpu_baseline_batch(M, wl, dp, wp, seconds):
+    """The float64 CPU oracle of batch DANSE (oracle/danse_ref_cpu.py
+    BatchDANSE: the reference's d_batch / d_core.danse_batch algorithm,
+    per-bin scipy.linalg.eigh), one process, default BLAS threads, timed on
+    this host on a bounded sample: the first iteration's per-node work
+    (y-tilde, both batch SCMs, GEVD solve, external filters, estimate + ISTFT,
+    MMSE cost) for as many nodes as fit the time budget, projected over
+    K nodes x the workload's iterations.  The set-up (STFT of every channel,
+    filter-history allocation) is excluded, as it is on the GPU side."""
+    from danse_amd.scene import make_scene
+    from oracle import danse_ref_cpu as O
+    K = len(M)
+    sc = make_scene(M, sigDur=wl['dur'], seed=2000)
+    sc.get_vad_per_frame(dp.DFTsize, dp.Ns, wp.vadMinProportionActive)
+    b = O.BatchDANSE(sc, dp, vadMinProp=wp.vadMinProportionActive)
+    t = time.perf_counter()
+    n = 0
+    while n < K and (n == 0 or time.perf_counter() - t < seconds):
+        b.batch_update_danse_covmats(n)
+        b.perform_update(n)
+        b.update_external_filters(n)
+        b.batch_estimate(n)
+        b.get_mmse_cost(n)
+        n += 1
+    tn = (time.perf_counter() - t) / n
+    F = dp.DFTsize // 2 + 1
+    nseg = b.yinSTFT[0].shape[1]
+    iters = wl['iters']
+    total = tn * K * iters
+    cores, threads, env = _threads()
+    return {'value': K * nseg * F * iters / total, 'unit': 'frame-updates/s', 'cores': threads, 'kind': 'port',
+            'sample': f'float64 oracle batch DANSE (reference algorithm, per-bin scipy eigh), one process, default '
+                      f'BLAS threads ({env or "no thread env set"}), scene seed 2000, iteration 1 of nodes 0..{n - 1} '
+                      f'({tn:.2f} s per node), projected over {K} nodes x {iters} iterations: {total:.0f} s; host '
+                      f'affinity {cores} cpus',
+            't_node_s': tn, 'nodes_sampled': n, 'projected_run_s': total}
 
 
 def pmc_traffic(wl, S, kernel_substr):

@@ -86,6 +86,7 @@ SIGNATURES = {
     'danse_engine_set_gate': (_c_i32, [ctypes.c_void_p, _c_i32, _p_i32, _p_i32, _p_i32, _p_i32,
                                        ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
     'danse_engine_gate_verdicts': (_c_i32, [ctypes.c_void_p, _p_i32, ctypes.c_void_p]),
+    'danse_engine_gate_launch': (_c_i32, [ctypes.c_void_p, _c_i32, ctypes.c_void_p]),
     'danse_engine_sro_estimates': (_c_i32, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
                                             ctypes.POINTER(ctypes.c_double)]),
     'danse_engine_get': (_c_i32, [ctypes.c_void_p, _c_i32, _c_i32, _c_i32, ctypes.c_void_p, ctypes.c_size_t,
@@ -111,6 +112,8 @@ SIGNATURES = {
     'danse_batch_unpack_wext': (_c_i32, [ctypes.c_void_p, _c_i32, ctypes.c_void_p, ctypes.c_void_p]),
     'danse_batch_output_bytes': (_c_i32, [ctypes.c_void_p, _c_i32, _c_i32, ctypes.POINTER(ctypes.c_size_t)]),
     'danse_batch_get': (_c_i32, [ctypes.c_void_p, _c_i32, _c_i32, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    'danse_batch_set_timing': (_c_i32, [ctypes.c_void_p, _c_i32]),
+    'danse_batch_timing': (_c_i32, [ctypes.c_void_p, _c_i32, _c_i32, ctypes.POINTER(ctypes.c_float)]),
     'danse_dxcp_create': (_c_i32, [_c_i32, _c_i32, ctypes.POINTER(ctypes.c_void_p)]),
     'danse_dxcp_destroy': (None, [ctypes.c_void_p]),
     'danse_dxcp_last_error': (ctypes.c_char_p, [ctypes.c_void_p]),

@@ -161,6 +161,20 @@ class BatchEngine:
         L.check_batch(self.lib.danse_batch_run_iters(self.eng, int(it0), int(it1), self.stream_ptr(stream)), self.eng)
         return self
 
+    PHASES = ('z', 'herk', 'solve', 'ext', 'dhat', 'istft_ola', 'cost')
+
+    def set_timing(self, on=True):
+        """Record HIP events at every phase boundary of every iteration."""
+        L.check_batch(self.lib.danse_batch_set_timing(self.eng, int(bool(on))), self.eng)
+
+    def phase_ms(self, it0=0, it1=None):
+        """Device milliseconds per phase summed over iterations [it0, it1)
+        of the last run (``set_timing`` must be on)."""
+        it1 = self.iters if it1 is None else it1
+        ms = (ctypes.c_float * len(self.PHASES))()
+        L.check_batch(self.lib.danse_batch_timing(self.eng, int(it0), int(it1), ms), self.eng)
+        return dict(zip(self.PHASES, [float(x) for x in ms]))
+
     def wext_chunk(self):
         """Complex64 elements of one (node, scene) chunk of the exchange buffers."""
         return self.F * self.Mmax
@@ -214,6 +228,17 @@ class BatchEngine:
             for s in range(S):
                 res[s].wTilde.append(np.transpose(w[s], (1, 0, 2)).astype(np.complex128))
                 res[s].wTildeExt.append(np.transpose(e[s], (1, 0, 2)).astype(np.complex128))
+        if (self.k0, self.k1) != (0, K):
+            # a node-sharded engine computes the SCMs, filters, estimates and
+            # costs of its own nodes only: the others are not outputs of this
+            # engine (their external filters are, through unpack_wext)
+            for s in range(S):
+                for k in range(K):
+                    if not self.k0 <= k < self.k1:
+                        res[s].d[:, k] = np.nan
+                        res[s].dhat[:, :, k] = np.nan
+                        res[s].mmseCost[:, k] = np.nan
+                        res[s].wTilde[k] = None
         for s in range(S):
             res[s].filters = res[s].wTilde
         return res
@@ -252,11 +277,15 @@ def run_node_sharded(eng, exchange, blockNodes, stream=None, device=None):
     z_q = wExt_q^H y_q of every neighbour q (d_core.py:286-326)."""
     torch = eng.torch
     dev = device if device is not None else f'cuda:{eng.device}'
-    buf = torch.zeros(blockNodes * eng.S * eng.wext_chunk(), dtype=torch.complex64, device=dev)
-    for it in range(eng.iters):
-        eng.run_iters(it, it + 1, stream)
-        eng.pack_wext(it + 1, buf, stream)
-        eng.unpack_wext(it + 1, exchange(buf), stream)
+    st = stream if stream is not None else torch.cuda.current_stream(eng.device)
+    # pack -> collective -> unpack must be ordered on ONE stream: the
+    # collective runs on torch's current stream, so make ``st`` current
+    with torch.cuda.stream(st):
+        buf = torch.zeros(blockNodes * eng.S * eng.wext_chunk(), dtype=torch.complex64, device=dev)
+        for it in range(eng.iters):
+            eng.run_iters(it, it + 1, st)
+            eng.pack_wext(it + 1, buf, st)
+            eng.unpack_wext(it + 1, exchange(buf), st)
     return eng
 
 

@@ -29,7 +29,12 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 template <typename T>
 hipError_t balloc(T** p, size_t n) {
   if (n == 0) n = 1;
-  return hipMalloc((void**)p, n * sizeof(T));
+  hipError_t e = hipMalloc((void**)p, n * sizeof(T));
+  // engine buffers start zeroed: a node-sharded engine never writes the
+  // outputs of nodes it does not own, and those must not read back as
+  // leftover device memory
+  if (e == hipSuccess) e = hipMemset(*p, 0, n * sizeof(T));
+  return e;
 }
 
 // ---------------------------------------------------------------------------
@@ -103,10 +108,13 @@ struct HerkNode {
 // triangle by symmetry.
 DANSE_DEV void store_scm(cf* p, cf v) { *p = v; }
 DANSE_DEV void store_scm(cd* p, cf v) { *p = cdk(v); }
+DANSE_DEV void store_scm64(cf* p, cd v) { *p = cfk(v); }
+DANSE_DEV void store_scm64(cd* p, cd v) { *p = v; }
+typedef double f64x4 __attribute__((ext_vector_type(4)));
 
 // (T: complex float for the stand-alone operator, complex double for the
 // engine, whose solve classes take both SCMs in double)
-template <int NT, typename TN>
+template <int NT, typename TN, int PASSES = 3>
 __global__ void __launch_bounds__(64) herk_kernel(const cf* __restrict__ Y, const cf* __restrict__ Z, int S, int K,
                                                   int MT, int nseg, const int* __restrict__ base,
                                                   const HerkNode* __restrict__ nodes, int nNodes,
@@ -114,6 +122,9 @@ __global__ void __launch_bounds__(64) herk_kernel(const cf* __restrict__ Y, cons
                                                   TN* __restrict__ Ryy, TN* __restrict__ Rnn) {
   constexpr int F = 513;
   constexpr int NP = NT * (NT + 1) / 2;
+  // the engine (TN = complex double) accumulates Rnn in float64; the
+  // stand-alone operator (complex float out) stays float32
+  constexpr bool kRnn64 = sizeof(TN) == 16;
   const int l = threadIdx.x;
   const int f = blockIdx.x % F;
   const int ni = (blockIdx.x / F) % nNodes;
@@ -141,9 +152,73 @@ __global__ void __launch_bounds__(64) herk_kernel(const cf* __restrict__ Y, cons
       stride[I] = K;
     }
   }
+  // PASSES: bit 0 Ryy (VAD frames), bit 1 Rnn (the others); the engine
+  // launches the two passes separately so that the float64 Rnn pass's
+  // accumulators do not set the float32 pass's occupancy
   for (int pass = 0; pass < 2; ++pass) {
+    if (!((PASSES >> pass) & 1)) continue;
     const int t0 = pass ? nv : 0;
     const int cnt = pass ? nseg - nv : nv;
+    const long long o = nd.scmOff + ((long long)s * F + f) * D * D;
+    if (kRnn64 && pass == 1) {
+      // Rnn in float64 (v_mfma_f64_16x16x4_f64: the f32 products are exact
+      // in f64, the sum over the non-VAD frames is not rounded to f32).  The
+      // GEVD filter is conditioned by cond(Rnn) (DESIGN.md "Precision"): an
+      // f32-accumulated Rnn left the D = 39 filters at a per-bin median of
+      // 1.4e-5 against the float64 reference.
+      f64x4 bre[NP], bim[NP];
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+        bre[p] = f64x4(0.0);
+        bim[p] = f64x4(0.0);
+      }
+      for (int b = 0; b < cnt; b += 4) {
+        const int ti = b + tt;
+        const bool ok = ti < cnt;
+        const int t = ok ? fl[t0 + ti] : 0;
+        double vr[NT], vi[NT];
+#pragma unroll
+        for (int I = 0; I < NT; ++I) {
+          const cf x = (ok && act[I]) ? src[I][(long long)t * stride[I]] : cf{0.0f, 0.0f};
+          vr[I] = (double)x.re;
+          vi[I] = (double)x.im;
+        }
+        int p = 0;
+#pragma unroll
+        for (int I = 0; I < NT; ++I) {
+#pragma unroll
+          for (int J = 0; J <= I; ++J) {
+            bre[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(vr[I], vr[J], bre[p], 0, 0, 0);
+            bre[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(vi[I], vi[J], bre[p], 0, 0, 0);
+            bim[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(vi[I], vr[J], bim[p], 0, 0, 0);
+            bim[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(vr[I], -vi[J], bim[p], 0, 0, 0);
+            ++p;
+          }
+        }
+      }
+      const double sc = (cnt > 0) ? 1.0 / (double)cnt : __builtin_nan("");
+      int p = 0;
+#pragma unroll
+      for (int I = 0; I < NT; ++I) {
+#pragma unroll
+        for (int J = 0; J <= I; ++J) {
+#pragma unroll
+          for (int rg = 0; rg < 4; ++rg) {
+            const int row = 16 * I + tt + 4 * rg;   // f64 C/D map: col = lane & 15, row = (lane >> 4) + 4 reg
+            const int col = 16 * J + il;
+            if (row < D && col < D && (I != J || col <= row)) {
+              cd c = cd{sc * bre[p][rg], sc * bim[p][rg]};
+              if (row == col) c.im = 0.0;
+              const long long e0 = o + (long long)row * D + col, e1 = o + (long long)col * D + row;
+              store_scm64(Rnn + e0, c);
+              if (row != col) store_scm64(Rnn + e1, conjg(c));
+            }
+          }
+          ++p;
+        }
+      }
+      continue;
+    }
     f32x4 are[NP], aim[NP];
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
@@ -172,7 +247,6 @@ __global__ void __launch_bounds__(64) herk_kernel(const cf* __restrict__ Y, cons
     }
     // mean over the frames (np.mean of an empty set is NaN, as in the reference)
     const float sc = (cnt > 0) ? 1.0f / (float)cnt : __builtin_nanf("");
-    const long long o = nd.scmOff + ((long long)s * F + f) * D * D;
     int p = 0;
 #pragma unroll
     for (int I = 0; I < NT; ++I) {
@@ -239,52 +313,86 @@ __global__ void batch_ext_kernel(int S, int K, int it, const int* __restrict__ M
   }
 }
 
-// dhat_k[f][t] = sum_i conj(w_k[f][i]) ytilde_k[f][t][i] for t < nseg - 1, and
-// the frame's irfft times the window: one wave per (scene, node, frame).
-__global__ void __launch_bounds__(256) batch_est_kernel(const cf* __restrict__ Y, const cf* __restrict__ Z, int S,
-                                                        int K, int MT, int nseg, const int* __restrict__ M,
-                                                        const int* __restrict__ base, const int* __restrict__ Dk,
-                                                        const cf* __restrict__ wHist, const long long* __restrict__ wOff,
-                                                        long long wStride, int slot, const float* __restrict__ win,
-                                                        const cf* __restrict__ tw, cf* __restrict__ dhat,
-                                                        float* __restrict__ frames, int k0, int nOwn) {
+// dhat_k[f][t] = sum_i conj(w_k[f][i]) ytilde_k[f][t][i] for t < nseg - 1
+// (batch_estimate, d_batch.py): one workgroup per (scene, bin, chunk of
+// kDhTC frames), blockIdx bin-fastest so that the bins of one (node, frame)
+// row of dhat are written by concurrently running workgroups (their 8-byte
+// stores merge in L2).  The observation row Y[s][f][t][0 .. MT) of a frame
+// is 2 KB contiguous and read once (thread (k, t) reads node k's M_k
+// channels of it), the fused row Z[s][f][t][0 .. K) is shared by every
+// node; the filters of the owned nodes at bin f sit in LDS.
+constexpr int kDhThr = 256;
+constexpr int kDhTC = 8;                 // frames per workgroup
+constexpr int kDhLdsCf = 4096;           // LDS filter slots (32 KB)
+__global__ void __launch_bounds__(kDhThr) batch_dhat_kernel(const cf* __restrict__ Y, const cf* __restrict__ Z, int S,
+                                                            int K, int MT, int nseg, const int* __restrict__ M,
+                                                            const int* __restrict__ base, const int* __restrict__ Dk,
+                                                            int Dmax, const cf* __restrict__ wHist,
+                                                            const long long* __restrict__ wOff, long long wStride,
+                                                            int slot, cf* __restrict__ dhat, int k0, int nOwn) {
+  __shared__ cf wl[kDhLdsCf];
+  constexpr int F = 513;
+  const int nfr = nseg - 1;
+  const int nChunk = (nfr + kDhTC - 1) / kDhTC;
+  const int f = blockIdx.x % F;
+  const int chunk = (blockIdx.x / F) % nChunk;
+  const int s = blockIdx.x / (F * nChunk);
+  const int t0 = chunk * kDhTC;
+  const int G = max(1, min(nOwn, kDhLdsCf / Dmax));   // nodes per LDS pass
+  for (int g0 = 0; g0 < nOwn; g0 += G) {
+    const int nG = min(G, nOwn - g0);
+    __syncthreads();
+    for (int e = threadIdx.x; e < nG * Dmax; e += kDhThr) {
+      const int gi = e / Dmax, i = e % Dmax;
+      const int k = k0 + g0 + gi;
+      const int D = Dk[k];
+      wl[e] = i < D ? wHist[(long long)s * wStride + wOff[k] + ((long long)slot * F + f) * D + i] : cf{0.0f, 0.0f};
+    }
+    __syncthreads();
+    for (int o = threadIdx.x; o < nG * kDhTC; o += kDhThr) {
+      const int gi = o % nG, tt = o / nG;
+      const int t = t0 + tt;
+      if (t >= nfr) continue;
+      const int k = k0 + g0 + gi;
+      const int Mk = M[k], D = Dk[k];
+      const cf* wf = wl + gi * Dmax;
+      const long long row = ((long long)s * F + f) * nseg + t;
+      const cf* yl = Y + row * MT + base[k];
+      const cf* zl = Z + row * K;
+      cf acc = cf{0.0f, 0.0f};
+#pragma unroll 4
+      for (int i = 0; i < Mk; ++i) acc = acc + cmul(wf[i], yl[i]);
+#pragma unroll 8
+      for (int j = 0; j < D - Mk; ++j) acc = acc + cmul(wf[Mk + j], zl[(j < k) ? j : j + 1]);
+      dhat[(((long long)s * K + k) * nfr + t) * F + f] = acc;
+    }
+  }
+}
+
+// The windowed inverse real FFT of one dhat frame (scipy istft's irfft):
+// one wave per (scene, owned node, frame), dhat read as one contiguous row.
+__global__ void __launch_bounds__(256) batch_istft_kernel(const cf* __restrict__ dhat, int S, int K, int nseg,
+                                                          const float* __restrict__ win, const cf* __restrict__ tw,
+                                                          float* __restrict__ frames, int k0, int nOwn) {
   __shared__ cf lds[4][wfft::kLdsElems];
   constexpr int F = 513;
   const int nfr = nseg - 1;
   const int wv = threadIdx.x >> 6;
   const long long job = (long long)blockIdx.x * 4 + wv;
-  if (job >= (long long)S * nOwn * nfr) return;
+  if (job >= (long long)S * nOwn * nfr) return;   // whole wave exits together
   const int t = (int)(job % nfr);
   const int k = k0 + (int)((job / nfr) % nOwn);
   const int s = (int)(job / ((long long)nfr * nOwn));
-  const int Mk = M[k], D = Dk[k];
-  const cf* w = wHist + (long long)s * wStride + wOff[k] + (long long)slot * F * D;
   const int l = __lane_id();
-  auto dh = [&](int f) {
-    const cf* yl = Y + (((long long)s * F + f) * nseg + t) * MT + base[k];
-    const cf* zl = Z + (((long long)s * F + f) * nseg + t) * K;
-    const cf* wf = w + (long long)f * D;
-    // unrolled so that several independent gathers are in flight per lane
-    // (the kernel is latency-bound on the strided Y / Z reads)
-    cf acc = cf{0.0f, 0.0f};
-#pragma unroll 4
-    for (int i = 0; i < Mk; ++i) acc = acc + cmul(wf[i], yl[i]);
-#pragma unroll 8
-    for (int j = 0; j < D - Mk; ++j) acc = acc + cmul(wf[Mk + j], zl[(j < k) ? j : j + 1]);
-    return acc;
-  };
-  // each bin once; the Hermitian mirror n >= F reads bin 1024 - n back from LDS
+  const cf* row = dhat + (((long long)s * K + k) * nfr + t) * F;
   cf* dl = lds[wv];
 #pragma unroll
   for (int j = 0; j < 9; ++j) {
     const int n = l + 64 * j;
-    if (n < F) {
-      const cf d = dh(n);
-      dhat[(((long long)s * K + k) * nfr + t) * F + n] = d;
-      dl[n] = d;
-    }
+    if (n < F) dl[n] = row[n];
   }
   wfft::wave_sync();
+  // each bin once; the Hermitian mirror n >= F reads bin 1024 - n
   cf v[16];
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
@@ -352,20 +460,26 @@ __global__ void batch_wstore_kernel(const cf* __restrict__ wTmp, int nRun, int S
 }
 
 // MMSE cost of iteration it: mean over [trim, T - trim) of |clean - d|^2
-// (get_mmse_cost, d_batch.py), fixed-order tree reduction in double.  1024
-// threads with four independent accumulators each: the double add chains,
-// not HBM, bound this kernel (one workgroup per (scene, node)).
-constexpr int kCostThr = 1024;
-__global__ void __launch_bounds__(kCostThr) batch_cost_kernel(const float* __restrict__ clean,
-                                                              const float* __restrict__ d, int T, int trim,
-                                                              double* __restrict__ cost, int K, int k0, int nOwn) {
+// (get_mmse_cost, d_batch.py) in double, in a fixed order: pass 1, one
+// workgroup per (scene, owned node, part) sums every kCostParts-th block of
+// 4 kCostThr samples (tree reduction in LDS); pass 2 adds the kCostParts
+// partial sums of each (scene, node) in order.  (One workgroup per node
+// alone left the chip nearly empty: 32 workgroups at config D.)
+constexpr int kCostThr = 256;
+constexpr int kCostParts = 32;
+__global__ void __launch_bounds__(kCostThr) batch_cost_part_kernel(const float* __restrict__ clean,
+                                                                   const float* __restrict__ d, int T, int trim,
+                                                                   double* __restrict__ part, int K, int k0, int nOwn) {
   __shared__ double red[kCostThr];
-  const long long sk = (long long)(blockIdx.x / nOwn) * K + k0 + blockIdx.x % nOwn;
+  const int p = blockIdx.x % kCostParts;
+  const int so = blockIdx.x / kCostParts;
+  const long long sk = (long long)(so / nOwn) * K + k0 + so % nOwn;
   const float* c = clean + sk * T;
   const float* dd = d + sk * T;
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
   const int hi = T - trim;
-  for (int x0 = trim + threadIdx.x; x0 < hi; x0 += 4 * kCostThr) {
+  constexpr int blk = 4 * kCostThr;
+  for (int x0 = trim + p * blk + threadIdx.x; x0 < hi; x0 += kCostParts * blk) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int x = x0 + u * kCostThr;
@@ -381,7 +495,17 @@ __global__ void __launch_bounds__(kCostThr) batch_cost_kernel(const float* __res
     if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
     __syncthreads();
   }
-  if (threadIdx.x == 0) cost[sk] = red[0] / (double)max(T - 2 * trim, 1);
+  if (threadIdx.x == 0) part[(long long)so * kCostParts + p] = red[0];
+}
+
+__global__ void batch_cost_final_kernel(const double* __restrict__ part, int T, int trim, double* __restrict__ cost,
+                                        int K, int k0, int nOwn, int nSo) {
+  const int so = blockIdx.x * blockDim.x + threadIdx.x;
+  if (so >= nSo) return;
+  const long long sk = (long long)(so / nOwn) * K + k0 + so % nOwn;
+  double acc = 0.0;
+  for (int p = 0; p < kCostParts; ++p) acc += part[(long long)so * kCostParts + p];
+  cost[sk] = acc / (double)max(T - 2 * trim, 1);
 }
 
 }  // namespace
@@ -411,7 +535,14 @@ struct danse_batch {
   cf *dTw = nullptr, *Y = nullptr, *Z = nullptr, *wHist = nullptr, *wExtHist = nullptr,
      *tgt = nullptr, *dhat = nullptr, *wTmp = nullptr;
   double* dCost = nullptr;
+  double* dCostPart = nullptr;   // [S][nOwn][kCostParts]
   int* dDiag = nullptr;
+  int Dmax = 1;
+  // per-phase timing of run_iters (danse_batch_set_timing): events after
+  // every phase of every iteration, [iteration][kBatchPhases + 1]
+  bool timing = false;
+  std::vector<hipEvent_t> ev;
+  int evIters = 0;
   const float* y = nullptr;
   const float* clean = nullptr;
   std::vector<cf> w0, wExt0, tgt0;   // host initial filters / external-filter targets (per node, concatenated)
@@ -558,8 +689,10 @@ int danse_batch_create(const danse_batch_cfg* c, int device, danse_batch** out) 
   BCHK(balloc(&eng->dFramesTD, (size_t)S * K * (nseg - 1) * 1024));
   BCHK(balloc(&eng->dD_, (size_t)S * K * c->T));
   BCHK(balloc(&eng->dCost, (size_t)c->iters * S * K));
+  BCHK(balloc(&eng->dCostPart, (size_t)S * K * kCostParts));
   int Dmax = 0;
   for (int k = 0; k < K; ++k) Dmax = std::max(Dmax, eng->D[k]);
+  eng->Dmax = Dmax;
   BCHK(balloc(&eng->wTmp, (size_t)K * S * F * Dmax));   // one solve launch covers a run of nodes
   BCHK(balloc(&eng->dDiag, (size_t)K * S * F));
   (void)Mmax;
@@ -573,9 +706,10 @@ void danse_batch_destroy(danse_batch* eng) {
   void* ptrs[] = {eng->dM, eng->dBase, eng->dD, eng->dExtMode, eng->dFrames, eng->dNvad, eng->dWOff, eng->dWExtOff,
                   eng->dTgtOff, eng->dNodes, eng->dWin, eng->dBetaExt, eng->dTw, eng->Y, eng->Z, eng->Ryy, eng->Rnn,
                   eng->wHist, eng->wExtHist, eng->tgt, eng->dhat, eng->dFramesTD, eng->dD_, eng->dCost, eng->wTmp,
-                  eng->dDiag};
+                  eng->dDiag, eng->dCostPart};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
+  for (hipEvent_t e : eng->ev) (void)hipEventDestroy(e);
   delete eng;
 }
 
@@ -585,6 +719,8 @@ int danse_batch_set_inputs(danse_batch* eng, const float* y, const float* clean)
   eng->clean = clean;
   return 0;
 }
+
+constexpr int kBatchPhases = 7;
 
 static void launch_herk(danse_batch* e, hipStream_t st) {
   // one launch per tile count (nodes grouped by ceil(D / 16))
@@ -600,8 +736,12 @@ static void launch_herk(danse_batch* e, hipStream_t st) {
       const int nN = all ? e->k1 - e->k0 : 1;
       const unsigned grid = (unsigned)(e->S * nN * e->F);
 #define DANSE_HERK(NTV)                                                                                             \
-  hipLaunchKernelGGL((herk_kernel<NTV, cd>), dim3(grid), dim3(64), 0, st, e->Y, e->Z, e->S, e->K, e->MT, e->nseg, e->dBase, \
-                     dn, nN, e->dFrames, e->dNvad, e->Ryy, e->Rnn)
+  do {                                                                                                              \
+    hipLaunchKernelGGL((herk_kernel<NTV, cd, 1>), dim3(grid), dim3(64), 0, st, e->Y, e->Z, e->S, e->K, e->MT, e->nseg,  \
+                       e->dBase, dn, nN, e->dFrames, e->dNvad, e->Ryy, e->Rnn);                                          \
+    hipLaunchKernelGGL((herk_kernel<NTV, cd, 2>), dim3(grid), dim3(64), 0, st, e->Y, e->Z, e->S, e->K, e->MT, e->nseg,  \
+                       e->dBase, dn, nN, e->dFrames, e->dNvad, e->Ryy, e->Rnn);                                          \
+  } while (0)
       if (nt == 1) DANSE_HERK(1);
       else if (nt == 2) DANSE_HERK(2);
       else if (nt == 3) DANSE_HERK(3);
@@ -645,12 +785,20 @@ int danse_batch_run_iters(danse_batch* eng, int32_t it0, int32_t it1, void* stre
   }
   int Mmax = 0;
   for (int k = 0; k < K; ++k) Mmax = std::max(Mmax, eng->M[k]);
+  // phase boundaries: 0 start, 1 z, 2 HERK, 3 solves, 4 external filters,
+  // 5 dhat, 6 ISTFT + OLA, 7 MMSE cost
+  auto mark = [&](int it, int ph) {
+    if (eng->timing && it < eng->evIters) (void)hipEventRecord(eng->ev[(size_t)it * (kBatchPhases + 1) + ph], st);
+  };
   for (int it = it0; it < it1; ++it) {
+    mark(it, 0);
     hipLaunchKernelGGL(batch_z_kernel, dim3(2048), dim3(256), 0, st, eng->Y, S, K, eng->MT, nseg, eng->dM, eng->dBase,
                        eng->wExtHist, eng->dWExtOff, eng->wExtStride, it, eng->Z);
     BCHK(hipGetLastError());
+    mark(it, 1);
     launch_herk(eng, st);
     BCHK(hipGetLastError());
+    mark(it, 2);
     // Solves (perform_update, d_core.py:298-326): consecutive solving nodes
     // of one filter dimension have adjacent [S][F][D][D] SCM blocks, so one
     // launch covers the whole run (K*S*F bins for equal D: a full chip
@@ -677,23 +825,67 @@ int danse_batch_run_iters(danse_batch* eng, int32_t it0, int32_t it1, void* stre
       BCHK(hipGetLastError());
       k = k1;
     }
+    mark(it, 3);
     hipLaunchKernelGGL(batch_ext_kernel, dim3(512), dim3(256), 0, st, S, K, it, eng->dM, eng->dD, eng->dExtMode,
                        eng->ref, eng->dBetaExt, eng->alphaExt, eng->wHist, eng->dWOff, eng->wStride, H, eng->wExtHist,
                        eng->dWExtOff, eng->wExtStride, eng->tgt, eng->dTgtOff, eng->tgtStride, Mmax, k0,
                        nOwn);
     BCHK(hipGetLastError());
-    const long long jobs = (long long)S * nOwn * (nseg - 1);
-    hipLaunchKernelGGL(batch_est_kernel, dim3((unsigned)((jobs + 3) / 4)), dim3(256), 0, st, eng->Y, eng->Z, S, K,
-                       eng->MT, nseg, eng->dM, eng->dBase, eng->dD, eng->wHist, eng->dWOff, eng->wStride, it + 1,
-                       eng->dWin, eng->dTw, eng->dhat, eng->dFramesTD, k0, nOwn);
-    BCHK(hipGetLastError());
+    mark(it, 4);
+    {
+      const int nfr = nseg - 1;
+      const unsigned g = (unsigned)((long long)S * F * ((nfr + kDhTC - 1) / kDhTC));
+      hipLaunchKernelGGL(batch_dhat_kernel, dim3(g), dim3(kDhThr), 0, st, eng->Y, eng->Z, S, K, eng->MT, nseg, eng->dM,
+                         eng->dBase, eng->dD, eng->Dmax, eng->wHist, eng->dWOff, eng->wStride, it + 1, eng->dhat, k0,
+                         nOwn);
+      BCHK(hipGetLastError());
+      mark(it, 5);
+      const long long jobs = (long long)S * nOwn * nfr;
+      hipLaunchKernelGGL(batch_istft_kernel, dim3((unsigned)((jobs + 3) / 4)), dim3(256), 0, st, eng->dhat, S, K, nseg,
+                         eng->dWin, eng->dTw, eng->dFramesTD, k0, nOwn);
+      BCHK(hipGetLastError());
+    }
     hipLaunchKernelGGL(batch_ola_kernel, dim3(2048), dim3(256), 0, st, eng->dFramesTD, S, K, eng->T, eng->Ns, nseg,
                        eng->dWin, eng->dD_, k0, nOwn);
     BCHK(hipGetLastError());
+    mark(it, 6);
     if (eng->clean) {
-      hipLaunchKernelGGL(batch_cost_kernel, dim3(S * nOwn), dim3(kCostThr), 0, st, eng->clean, eng->dD_, eng->T,
-                         eng->trim, eng->dCost + (size_t)it * S * K, K, k0, nOwn);
+      hipLaunchKernelGGL(batch_cost_part_kernel, dim3(S * nOwn * kCostParts), dim3(kCostThr), 0, st, eng->clean,
+                         eng->dD_, eng->T, eng->trim, eng->dCostPart, K, k0, nOwn);
+      hipLaunchKernelGGL(batch_cost_final_kernel, dim3((S * nOwn + 255) / 256), dim3(256), 0, st, eng->dCostPart, eng->T,
+                         eng->trim, eng->dCost + (size_t)it * S * K, K, k0, nOwn, S * nOwn);
       BCHK(hipGetLastError());
+    }
+    mark(it, 7);
+  }
+  return 0;
+}
+
+int danse_batch_set_timing(danse_batch* eng, int32_t on) {
+  if (!eng) return bfail(eng, "null engine");
+  BCHK(hipSetDevice(eng->dev));
+  eng->timing = on != 0;
+  if (eng->timing && eng->ev.empty()) {
+    eng->evIters = eng->iters;
+    eng->ev.resize((size_t)eng->iters * (kBatchPhases + 1));
+    for (auto& e : eng->ev) BCHK(hipEventCreate(&e));
+  }
+  return 0;
+}
+
+int danse_batch_timing(danse_batch* eng, int32_t it0, int32_t it1, float* ms) {
+  if (!eng || !ms) return bfail(eng, "null argument");
+  if (!eng->timing || eng->ev.empty()) return bfail(eng, "timing not enabled");
+  if (it0 < 0 || it1 > eng->evIters || it0 >= it1) return bfail(eng, "bad iteration range");
+  BCHK(hipSetDevice(eng->dev));
+  for (int p = 0; p < kBatchPhases; ++p) ms[p] = 0.0f;
+  for (int it = it0; it < it1; ++it) {
+    hipEvent_t* e = &eng->ev[(size_t)it * (kBatchPhases + 1)];
+    BCHK(hipEventSynchronize(e[kBatchPhases]));
+    for (int p = 0; p < kBatchPhases; ++p) {
+      float x = 0.0f;
+      BCHK(hipEventElapsedTime(&x, e[p], e[p + 1]));
+      ms[p] += x;
     }
   }
   return 0;

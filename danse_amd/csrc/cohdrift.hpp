@@ -2,7 +2,9 @@
 // (update_sro_estimates + build_phase_shifts_for_srocomp,
 // danse_toolbox/d_classes.py:2364-2621; cohdrift_sro_estimation with
 // method 'ls', danse_toolbox/d_sros.py:19-95), one workgroup per (scene,
-// node k, neighbour q), launched after every round's update:
+// owned node k, neighbour q), launched after every round's update (a
+// receiver needs its own local spectrum and the all-gathered fused spectra
+// only, so a node-sharded engine estimates for its own nodes):
 //   * the coherence of the compensated observation, yyH[0, q] /
 //     sqrt(yyH[0, 0] yyH[q, q]) with yyH = y y^H / D, goes to a ring of
 //     segLength + 1 rounds;
@@ -21,6 +23,7 @@ namespace danse {
 
 struct CohDriftArgs {
   int S, K, MT, F, r, ld, start, every, nIter, compensate;
+  int k0, nOwn;         // receivers k0 .. k0 + nOwn - 1 (a node-sharded engine owns a block)
   double alpha, alphaEps, Ns;
   const int* base;      // [K] first channel of node k
   cd* ring;             // [ld + 1][S][K][K - 1][F]
@@ -38,8 +41,8 @@ __global__ void __launch_bounds__(kCdThreads) cohdrift_kernel(const UpdateArgs a
   __shared__ double red[2][kCdThreads / 64];
   const int K = c.K, F = c.F, r = c.r;
   const int qi = blockIdx.x % (K - 1);
-  const int k = (blockIdx.x / (K - 1)) % K;
-  const int s = blockIdx.x / ((K - 1) * K);
+  const int k = c.k0 + (int)((blockIdx.x / (K - 1)) % c.nOwn);
+  const int s = blockIdx.x / ((K - 1) * c.nOwn);
   const int qg = qi < k ? qi : qi + 1;
   const int t = threadIdx.x;
   const long long ringStride = (long long)c.S * K * (K - 1) * F;

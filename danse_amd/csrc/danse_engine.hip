@@ -645,7 +645,8 @@ static void launch_update(danse_engine* e, int r, hipStream_t st) {
     c.every = e->cdEvery; c.nIter = e->cdNIter; c.compensate = e->cdComp; c.alpha = e->cdAlpha;
     c.alphaEps = e->cdAlphaEps; c.Ns = (double)e->Ns; c.base = e->dBase; c.ring = e->cdRing; c.avgTail = e->cdAvg;
     c.phase = e->cdPhase; c.est = e->cdEst; c.res = e->cdRes; c.R = e->R;
-    hipLaunchKernelGGL(cohdrift_kernel, dim3(e->S * e->K * (e->K - 1)), dim3(kCdThreads), 0, st, make_update(e, r), c);
+    c.k0 = e->k0; c.nOwn = e->k1 - e->k0;
+    hipLaunchKernelGGL(cohdrift_kernel, dim3(e->S * c.nOwn * (e->K - 1)), dim3(kCdThreads), 0, st, make_update(e, r), c);
   }
 }
 
@@ -675,6 +676,28 @@ static void launch_bcast(danse_engine* e, int r, int synth, int bc, hipStream_t 
   BcastArgs a = make_bcast(e, r, synth, bc);
   const unsigned grid = (unsigned)(e->S * (e->k1 - e->k0));
   hipLaunchKernelGGL(bcast_kernel, dim3(grid), dim3(256), 0, st, a);
+}
+
+// the installed speculative gate candidates of round r (danse_engine_set_gate)
+static void launch_gate_round(danse_engine* eng, int r, hipStream_t s) {
+  if (eng->nGate > 0 && eng->gateOff[r + 1] > eng->gateOff[r]) {
+    const int n = eng->gateOff[r + 1] - eng->gateOff[r];
+    const size_t lds = (size_t)eng->gateDmax[r] * (eng->gateDmax[r] + 1) * sizeof(cd);
+    hipLaunchKernelGGL(gate_kernel, dim3(eng->F, n), dim3(64), lds, s, make_update(eng, r), eng->dFnAll,
+                       eng->dGateCand + eng->gateOff[r], eng->dInitScmOff, eng->dScm0, eng->scmPerBin,
+                       eng->dGateVerdict + eng->gateOff[r]);
+  }
+}
+
+int danse_engine_gate_launch(danse_engine* eng, int32_t r, void* stream) {
+  if (!eng || !eng->y) return fail(eng, "inputs not set");
+  if (r < 0 || r >= eng->R) return fail(eng, "round out of range");
+  HIPCHK(hipSetDevice(eng->dev));
+  hipStream_t st = (hipStream_t)stream;
+  if (eng->nGate > 0 && r == 0) HIPCHK(hipMemsetAsync(eng->dGateVerdict, 0xff, eng->nGate * sizeof(int), st));
+  launch_gate_round(eng, r, st);
+  HIPCHK(hipGetLastError());
+  return 0;
 }
 
 int danse_engine_bcast(danse_engine* eng, int32_t r, void* stream) {
@@ -712,13 +735,7 @@ int danse_engine_run(danse_engine* eng, int32_t r0, int32_t r1, void* stream, in
     if (eng->nGate > 0 && r0 == 0) (void)hipMemsetAsync(eng->dGateVerdict, 0xff, eng->nGate * sizeof(int), s);
     for (int r = r0; r < r1; ++r) {
       launch_bcast(eng, r, r > 0, 1, s);
-      if (eng->nGate > 0 && eng->gateOff[r + 1] > eng->gateOff[r]) {
-        const int n = eng->gateOff[r + 1] - eng->gateOff[r];
-        const size_t lds = (size_t)eng->gateDmax[r] * (eng->gateDmax[r] + 1) * sizeof(cd);
-        hipLaunchKernelGGL(gate_kernel, dim3(eng->F, n), dim3(64), lds, s, make_update(eng, r), eng->dFnAll,
-                           eng->dGateCand + eng->gateOff[r], eng->dInitScmOff, eng->dScm0, eng->scmPerBin,
-                           eng->dGateVerdict + eng->gateOff[r]);
-      }
+      launch_gate_round(eng, r, s);
       launch_update(eng, r, s);
     }
     if (r1 == eng->R) launch_bcast(eng, eng->R, 1, 0, s);

@@ -17,6 +17,8 @@
 // eigvalsh >= 0 and the rank test become one float64 Cholesky of the
 // lower-triangle Hermitian matrix with every pivot above D eps trace(X) (the
 // matrix_rank tolerance sigma_max max(M, N) eps with sigma_max <= trace).
+// MWF runs the rank test alone: a signed elimination that accepts negative
+// pivots (an indefinite full-rank SCM passes, as in the reference).
 // One (candidate, bin) per wavefront, the matrix in LDS, lane i owns row i.
 #pragma once
 #include "kernels.hpp"
@@ -94,13 +96,16 @@ __global__ void __launch_bounds__(64) gate_kernel(const UpdateArgs a, const FamN
     for (int o = 32; o >= 1; o >>= 1) tr += __shfl_xor(tr, o);
     const double tol = (double)D * 2.220446049250313e-16 * fabs(tr);
     __syncthreads();
+    // GEVD (eigvalsh >= 0 and full rank): every pivot above tol.  MWF (rank
+    // only, _check_validity_nogevd, d_classes.py:1473-1480): a signed
+    // (LDL^H) elimination -- negative pivots are accepted, |pivot| > tol
     for (int j = 0; j < D; ++j) {
       const double pj = gX[j * P + j].re;
-      if (!(pj > tol)) {
+      if (!(a.gevd ? pj > tol : fabs(pj) > tol)) {
         pass = false;
         break;
       }
-      const double inv = 1.0 / sqrt(pj);
+      const double inv = 1.0 / sqrt(fabs(pj));
       if (li > j && li < D) {
         const cd v = gX[li * P + j];
         gX[li * P + j] = inv * v;
@@ -108,7 +113,11 @@ __global__ void __launch_bounds__(64) gate_kernel(const UpdateArgs a, const FamN
       __syncthreads();
       if (li > j && li < D) {
         const cd lij = gX[li * P + j];
-        for (int k = j + 1; k <= li; ++k) fms_cc(gX[li * P + k], lij, gX[k * P + j]);
+        if (pj > 0.0) {
+          for (int k = j + 1; k <= li; ++k) fms_cc(gX[li * P + k], lij, gX[k * P + j]);
+        } else {
+          for (int k = j + 1; k <= li; ++k) fma_cc(gX[li * P + k], lij, gX[k * P + j]);
+        }
       }
       __syncthreads();
     }

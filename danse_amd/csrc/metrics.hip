@@ -224,6 +224,14 @@ int danse_fwsnrseg(const double* clean, const double* enhanced, int64_t T, int32
   // every frame's last sample is inside the signal: (nf - 1) skip + W <= T
   if ((long long)(p.nf - 1) * p.skip + p.W > T) return fail("fwSNRseg frame table exceeds the signal");
   const size_t lds = (size_t)p.nfft * sizeof(double2) + (size_t)p.nfft * sizeof(double);
+  if (nSig > 65535) return fail("fwSNRseg: more than 65535 signal pairs in one call");
+  {
+    int dev = 0, maxLds = 0;
+    MCHK(hipGetDevice(&dev));
+    MCHK(hipDeviceGetAttribute(&maxLds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev));
+    if (lds > (size_t)maxLds) return fail("fwSNRseg: the FFT workspace exceeds the device's LDS per workgroup");
+    if (lds > 65536) MCHK(hipFuncSetAttribute((const void*)fwsnrseg_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  }
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(fwsnrseg_kernel, dim3(p.nf, nSig), dim3(kThr), lds, st, clean, enhanced, (long long)T, p,
                      perFrame);

@@ -26,7 +26,29 @@ def node_range(K: int, world: int, rank: int):
 
 
 class ShardedRun:
-    def __init__(self, engine, group=None):
+    """Drives a node-sharded engine over ``torch.distributed``.
+
+    Per round r: ``bcast(r)`` for the owned nodes, the in-place all-gather of
+    the fused spectra, the start gate of round r for the owned nodes, then
+    ``update(r)``.
+
+    The reference's start gate (``check_covariance_matrices``,
+    ``d_classes.py:1430-1540``) decides when each node starts updating from
+    its own SCMs only, so each rank checks its own nodes.  A delayed start
+    changes that node's filters and, through z, every other rank's results,
+    so the ranks agree on one outcome: the run goes speculatively first (the
+    flags assume every check passes; the checks run inside the run), the
+    per-rank verdicts are all-reduced (MIN), and if any rank saw a failure
+    every rank repeats the run exactly, deciding each candidate's start
+    synchronously at its round (as ``DanseEngine._run_gated``).
+
+    With RCCL the speculative (or ungated) round sequence -- reset, 310 x
+    (bcast, all-gather, gate, update), finish -- is captured once into a CUDA
+    graph and replayed (``graph=None``: on when the backend is nccl).  With
+    gloo and device tensors the exchange is staged through host memory.
+    """
+
+    def __init__(self, engine, group=None, graph=None):
         import torch
         import torch.distributed as dist
         self.torch = torch
@@ -48,18 +70,83 @@ class ShardedRun:
         chunk = per // self.world
         self.slot = [self.zbuf[i * per:(i + 1) * per] for i in range(self.slots)]
         self.mine = [v[self.rank * chunk:(self.rank + 1) * chunk] for v in self.slot]
+        backend = str(dist.get_backend(group)).lower()
+        # gloo cannot gather device tensors in place: stage through the host
+        self.stage = backend == 'gloo' and self.zbuf.device.type != 'cpu'
+        if self.stage:
+            self.hslot = [torch.zeros(per, dtype=torch.float32) for _ in range(self.slots)]
+        self.graph = (backend == 'nccl') if graph is None else bool(graph)
+        self._graphs = {}
+        self._eager_runs = 0
 
     def exchange(self, r=0):
         i = r % self.slots
-        self.dist.all_gather_into_tensor(self.slot[i], self.mine[i], group=self.group)
+        if self.stage:
+            mine = self.mine[i].cpu()
+            self.dist.all_gather_into_tensor(self.hslot[i], mine, group=self.group)
+            self.slot[i].copy_(self.hslot[i])
+        else:
+            self.dist.all_gather_into_tensor(self.slot[i], self.mine[i], group=self.group)
 
-    def run(self, reset=True):
+    def _rounds(self, reset, gate):
         e = self.eng
         if reset:
             e.reset()
         for r in range(e.R):
             e.bcast(r)
             self.exchange(r)
+            if gate:
+                e.gate_launch(r)
+            e.update(r)
+        e.finish()
+
+    def _sequence(self, reset, gate):
+        """The round sequence, eagerly or as a replayed CUDA graph (captured
+        on the second call, once the communicator and the kernels are warm)."""
+        torch = self.torch
+        key = (bool(reset), bool(gate))
+        if not self.graph or self.stage or self.zbuf.device.type == 'cpu':
+            return self._rounds(reset, gate)
+        g = self._graphs.get(key)
+        if g is None:
+            if self._eager_runs < 1:
+                self._eager_runs += 1
+                return self._rounds(reset, gate)
+            g = torch.cuda.CUDAGraph()
+            side = torch.cuda.Stream(device=self.zbuf.device)
+            side.wait_stream(torch.cuda.current_stream(self.zbuf.device))
+            with torch.cuda.graph(g, stream=side):
+                self._rounds(reset, gate)
+            self._graphs[key] = g
+        g.replay()
+
+    def _all_ok(self, ok):
+        t = self.torch.tensor([1 if ok else 0], dtype=self.torch.int32,
+                              device='cpu' if self.zbuf.device.type == 'cpu' or self.stage else self.zbuf.device)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN, group=self.group)
+        return bool(int(t.item()))
+
+    def run(self, reset=True, gate=True):
+        e = self.eng
+        gating = getattr(e, 'gating', None) is not None and e.gating(gate)
+        if not gating:
+            self._sequence(reset, False)
+            return self
+        if not e.gate_spec_failed:
+            e.begin_run(speculative=True)
+            self._sequence(reset, True)
+            if self._all_ok(e.gate_ok()):
+                return self
+            # some rank's speculative start was wrong: every rank repeats
+            e.mark_gate_failed()
+        e.begin_run(speculative=False)
+        e.reset()
+        pending = e.gate_pending()
+        for r in range(e.R):
+            e.bcast(r)
+            self.exchange(r)
+            if pending and min(pending.values()) == r:
+                e.gate_decide(r, pending)
             e.update(r)
         e.finish()
         return self
@@ -94,3 +181,29 @@ class ShardedEngine:
 
     def finish(self):
         self.e.finish()
+
+    # the start gate (DanseEngine's caller-sequenced gate API)
+    def gating(self, gate=True):
+        return self.e.gating(gate)
+
+    def begin_run(self, speculative):
+        return self.e.begin_run(speculative)
+
+    def gate_launch(self, r):
+        self.e.gate_launch(r)
+
+    def gate_ok(self):
+        return self.e.gate_ok()
+
+    def mark_gate_failed(self):
+        self.e.mark_gate_failed()
+
+    @property
+    def gate_spec_failed(self):
+        return self.e.gate_spec_failed
+
+    def gate_pending(self):
+        return self.e.gate_pending()
+
+    def gate_decide(self, r, pending):
+        self.e.gate_decide(r, pending)

@@ -163,9 +163,6 @@ class DanseEngine:
             # local spectra and the centralised VAD averages every node's VAD;
             # a node-sharded engine only analyses (and only has) its own nodes
             raise NotImplementedError('centralised / single-sensor-broadcast estimates on a node-sharded engine')
-        if (self.k0, self.k1) != (0, K) and p.estimateSROs == 'CohDrift':
-            # the CohDrift kernel runs for every (node, sender) pair of the engine
-            raise NotImplementedError('CohDrift SRO estimation on a node-sharded engine')
         if not self.rt.synchronous and (p.computeCentralised or p.computeSingleSensorBroadcast):
             raise NotImplementedError('centralised / single-sensor-broadcast estimates with asynchronous (SRO) '
                                       'clocks are not on the device path')
@@ -568,8 +565,8 @@ class DanseEngine:
             return 0.0
         return float(self._beta[s, k]) ** int(np.sum(o == L.OP_AVG))
 
-    def _run_gated(self, st):
-        R = self.R
+    def _gate_pending(self):
+        """{(s, f, k): first counter-eligible round} of every owned family-node."""
         pending = {}
         for key, g in self._gateState.items():
             if key[2] < self.k0 or key[2] >= self.k1:
@@ -577,49 +574,110 @@ class DanseEngine:
             e = np.flatnonzero(g['elig'])
             if e.size:
                 pending[key] = int(e[0])
+        return pending
+
+    def _gate_decide(self, rc, pending, st):
+        """The exact gate of round rc (after its broadcast, before its update):
+        check every candidate pending at rc on the device, move the start
+        (and the solve flags) of those that fail to their next eligible
+        round, and upload the flags if they changed."""
+        cands = sorted(key for key, r in pending.items() if r == rc)
+        if not cands:
+            return
+        fam = np.array([c[1] for c in cands], dtype=np.int32)
+        node = np.array([c[2] for c in cands], dtype=np.int32)
+        scn = np.array([c[0] for c in cands], dtype=np.int32)
+        qY = np.array([self._gate_q(c[0], c[2], self._gateState[c]['opY'], rc) for c in cands])
+        qN = np.array([self._gate_q(c[0], c[2], self._gateState[c]['opN'], rc) for c in cands])
+        ver = np.zeros(len(cands), dtype=np.int32)
+        L.check(self.lib.danse_engine_gate(self.eng, rc, len(cands), _ptr(fam, ctypes.c_int32),
+                                           _ptr(node, ctypes.c_int32), _ptr(scn, ctypes.c_int32),
+                                           _ptr(qY, ctypes.c_double), _ptr(qN, ctypes.c_double),
+                                           _ptr(ver, ctypes.c_int32), st), self.eng)
+        changed = False
+        for c, v in zip(cands, ver):
+            s, f, k = c
+            if v:
+                del pending[c]
+                if self.startRound[s, f, k] != rc:
+                    self.flags[:, s, f, k] = self._flags_for(s, f, k, rc)
+                    changed = True
+            else:
+                nxt = np.flatnonzero(self._gateState[c]['elig'][rc + 1:])
+                if nxt.size:
+                    pending[c] = rc + 1 + int(nxt[0])
+                else:
+                    del pending[c]
+                if self.startRound[s, f, k] != -1:
+                    self.flags[:, s, f, k] = self._flags_for(s, f, k, -1)
+                    changed = True
+        if changed:
+            self._gateMoved = True
+            self._flags = np.ascontiguousarray(self.flags)
+            L.check(self.lib.danse_engine_set_flags(self.eng, _ptr(self._flags, ctypes.c_uint8), st), self.eng)
+
+    def _run_gated(self, st):
+        R = self.R
+        pending = self._gate_pending()
         r0 = 0
         while pending:
             rc = min(pending.values())
             if rc > r0:
                 L.check(self.lib.danse_engine_run(self.eng, r0, rc, st, 0), self.eng)
             L.check(self.lib.danse_engine_bcast(self.eng, rc, st), self.eng)
-            cands = sorted(key for key, r in pending.items() if r == rc)
-            fam = np.array([c[1] for c in cands], dtype=np.int32)
-            node = np.array([c[2] for c in cands], dtype=np.int32)
-            scn = np.array([c[0] for c in cands], dtype=np.int32)
-            qY = np.array([self._gate_q(c[0], c[2], self._gateState[c]['opY'], rc) for c in cands])
-            qN = np.array([self._gate_q(c[0], c[2], self._gateState[c]['opN'], rc) for c in cands])
-            ver = np.zeros(len(cands), dtype=np.int32)
-            L.check(self.lib.danse_engine_gate(self.eng, rc, len(cands), _ptr(fam, ctypes.c_int32),
-                                               _ptr(node, ctypes.c_int32), _ptr(scn, ctypes.c_int32),
-                                               _ptr(qY, ctypes.c_double), _ptr(qN, ctypes.c_double),
-                                               _ptr(ver, ctypes.c_int32), st), self.eng)
-            changed = False
-            for c, v in zip(cands, ver):
-                s, f, k = c
-                if v:
-                    del pending[c]
-                    if self.startRound[s, f, k] != rc:
-                        self.flags[:, s, f, k] = self._flags_for(s, f, k, rc)
-                        changed = True
-                else:
-                    nxt = np.flatnonzero(self._gateState[c]['elig'][rc + 1:])
-                    if nxt.size:
-                        pending[c] = rc + 1 + int(nxt[0])
-                    else:
-                        del pending[c]
-                    if self.startRound[s, f, k] != -1:
-                        self.flags[:, s, f, k] = self._flags_for(s, f, k, -1)
-                        changed = True
-            if changed:
-                self._gateMoved = True
-                self._flags = np.ascontiguousarray(self.flags)
-                L.check(self.lib.danse_engine_set_flags(self.eng, _ptr(self._flags, ctypes.c_uint8), st), self.eng)
+            self._gate_decide(rc, pending, st)
             L.check(self.lib.danse_engine_update(self.eng, rc, st), self.eng)
             r0 = rc + 1
             if r0 >= R:
                 break
         return r0
+
+    # ---- the gate for callers that sequence the rounds themselves (the
+    # node-sharded runner, danse_amd.dist.ShardedRun)
+    def gating(self, gate=True):
+        return bool(gate and self.pregiven is None and not self.p.bypassUpdates)
+
+    def begin_run(self, speculative, stream=None):
+        """State bookkeeping before a caller-sequenced run: re-load the init
+        slots a previous run's solves overwrote, restore the counter-compiled
+        flags, and install (speculative) or remove (exact) the in-run gate."""
+        if self._ran:
+            self._load_init_history()
+            self._reset_gate()
+        self._ran = True
+        if speculative:
+            return self._install_gate()
+        self._uninstall_gate()
+        return 0
+
+    def gate_launch(self, r, stream=None):
+        """Speculative gate of round r (between the all-gather and update(r))."""
+        L.check(self.lib.danse_engine_gate_launch(self.eng, int(r), self.stream_ptr(stream)), self.eng)
+
+    def gate_ok(self, stream=None):
+        """True if every speculative gate check of the run passed."""
+        n = self._gateInstalled or 0
+        if n == 0:
+            return True
+        ver = np.zeros(n, dtype=np.int32)
+        L.check(self.lib.danse_engine_gate_verdicts(self.eng, _ptr(ver, ctypes.c_int32), self.stream_ptr(stream)),
+                self.eng)
+        return bool(np.all(ver != 0))
+
+    def mark_gate_failed(self):
+        """A speculative run (on this or another rank) had a failing check:
+        from now on the engine runs the exact host-gated sequence."""
+        self._gateSpecFailed = True
+
+    @property
+    def gate_spec_failed(self):
+        return self._gateSpecFailed
+
+    def gate_pending(self):
+        return self._gate_pending()
+
+    def gate_decide(self, r, pending, stream=None):
+        self._gate_decide(r, pending, self.stream_ptr(stream))
 
     def bcast(self, r, stream=None):
         L.check(self.lib.danse_engine_bcast(self.eng, r, self.stream_ptr(stream)), self.eng)

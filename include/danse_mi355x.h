@@ -224,6 +224,12 @@ int danse_engine_sro_estimates(danse_engine* eng, double* est, double* res);
 int danse_engine_set_gate(danse_engine* eng, int32_t n, const int32_t* round, const int32_t* family,
                           const int32_t* node, const int32_t* scene, const double* qY, const double* qN);
 int danse_engine_gate_verdicts(danse_engine* eng, int32_t* verdict, void* stream);
+/* The speculative gate of round r alone, for callers that sequence the
+ * rounds themselves (the node-sharded runner: bcast(r), all-gather, then
+ * this, then update(r)); r == 0 also re-arms the verdicts.  Asynchronous
+ * and capturable (no host synchronisation).  Same check as inside
+ * danse_engine_run (check_covariance_matrices, d_classes.py:1430-1540).   */
+int danse_engine_gate_launch(danse_engine* eng, int32_t r, void* stream);
 /* Use a caller-owned buffer (same size and layout) for the fused spectra,
  * e.g. a torch tensor that an RCCL all-gather fills in place. */
 int danse_engine_set_zspec(danse_engine* eng, void* ptr);
@@ -334,6 +340,13 @@ int danse_batch_pack_wext(danse_batch* eng, int32_t slot, void* dst, void* strea
 int danse_batch_unpack_wext(danse_batch* eng, int32_t slot, const void* src, void* stream);
 int danse_batch_output_bytes(danse_batch* eng, int32_t which, int32_t node, size_t* bytes);
 int danse_batch_get(danse_batch* eng, int32_t which, int32_t node, void* dst, size_t bytes, void* stream);
+/* Per-phase device timing of danse_batch_run_iters (HIP events recorded on
+ * the run's stream at every phase boundary of every iteration, off by
+ * default).  danse_batch_timing sums iterations [it0, it1) of the last run
+ * into ms[7]: z, Y.Y^H (HERK), solves, external filters, dhat, ISTFT + OLA,
+ * MMSE cost.  Synchronous (waits for iteration it1 - 1).                     */
+int danse_batch_set_timing(danse_batch* eng, int32_t on);
+int danse_batch_timing(danse_batch* eng, int32_t it0, int32_t it1, float* ms);
 
 /* ---- DXCP-PhaT sampling-rate-offset estimator (dxcpphat/sro_estimation.py:
  * 130-345, class DXCPPhaT with its default parameters: fs 16 kHz, 2048-sample

@@ -204,9 +204,13 @@ def update_covmats_batch(yAllFrames, vadAllFrames):
     if len(vadAllFrames) > yAllFrames.shape[1]:
         vadAllFrames = vadAllFrames[:yAllFrames.shape[1]]
     v = vadAllFrames.astype(bool)
-    Ryy = np.mean(np.einsum('ikj,ikl->ikjl', yAllFrames[:, v, :], yAllFrames[:, v, :].conj()), axis=1)
-    Rnn = np.mean(np.einsum('ikj,ikl->ikjl', yAllFrames[:, ~v, :], yAllFrames[:, ~v, :].conj()), axis=1)
-    return Ryy, Rnn
+    # the reference's mean over frames of einsum('ikj,ikl->ikjl') outer
+    # products, as one matmul per bin (the einsum materialises F x T x D x D:
+    # 7.8 GB per node at config D's D = 39)
+
+    def mean_outer(Y):
+        return np.matmul(np.swapaxes(Y, 1, 2), Y.conj()) / Y.shape[1]
+    return mean_outer(yAllFrames[:, v, :]), mean_outer(yAllFrames[:, ~v, :])
 
 
 def cohdrift_sro_estimation_ls(wPos, wPri, avgResProd, Ns, ld, alpha, first, bufferFlagPos, bufferFlagPri):
@@ -944,7 +948,8 @@ class BatchDANSE:
         zB = np.zeros((self.yinSTFT[k].shape[0], self.yinSTFT[k].shape[1], len(self.neighbors[k])), dtype=complex)
         for ii, q in enumerate(self.neighbors[k]):
             ff = self.wTildeExt[q][:, self.i[q], :]
-            zB[:, :, ii] = np.einsum('ij,ikj->ik', ff.conj(), self.yinSTFT[q])
+            # einsum('ij,ikj->ik', conj(ff), Y_q) as a batched matrix-vector product
+            zB[:, :, ii] = np.matmul(self.yinSTFT[q], ff.conj()[:, :, None])[:, :, 0]
         return np.concatenate((self.yinSTFT[k], zB), axis=-1)
 
     def batch_update_danse_covmats(self, k):

@@ -46,6 +46,24 @@ def test_fwsnrseg_batch_mean():
         assert abs(mean[b] - np.mean(ref)) <= 1e-9
 
 
+def test_fwsnrseg_48k_large_lds():
+    """fs = 48 kHz: nfft = 4096, a 96 KiB FFT workspace (above the 64 KiB
+    default dynamic-LDS limit) -- against the oracle per frame."""
+    import torch
+    from danse_amd import metrics as DM
+    from oracle import metrics_ref as MR
+    rng = np.random.default_rng(48)
+    B, T = 2, 48000
+    c = rng.standard_normal((B, T))
+    e = c * 0.8 + 0.3 * rng.standard_normal((B, T))
+    per, _ = DM.fwsnrseg_batch(torch.from_numpy(c).cuda(), torch.from_numpy(e).cuda(), 48000.0)
+    per = per.cpu().numpy()
+    for b in range(B):
+        ref = MR.get_fwsnrseg(c[b], e[b], 48000.0)
+        assert per[b].shape == ref.shape
+        assert np.max(np.abs(per[b] - ref)) <= 1e-8
+
+
 def test_metrics_errors():
     from danse_amd import metrics as DM
     from danse_amd._lib import DanseError

@@ -384,5 +384,40 @@ def test_batch_node_sharded_equals_full(case):
                          (o.mmseCost[:, k], full.mmseCost[:, k])):
                 exact &= np.array_equal(a, b)
                 assert np.allclose(a, b, rtol=1e-6, atol=1e-7), (k0, k)
+        for k in set(range(K)) - set(range(k0, k1)):
+            # not this engine's outputs: marked, never leftover device memory
+            assert o.wTilde[k] is None
+            assert np.isnan(o.d[:, k]).all() and np.isnan(o.mmseCost[:, k]).all()
         e.close()
     print(case['name'], 'bit-exact' if exact else 'within 1e-6')
+
+
+@pytest.mark.timeout(600)
+def test_batch_engine_config_D_shape_vs_oracle():
+    """Config D's shape end to end through BatchEngine: K = 32 nodes x 8 mics
+    (D = 39: the 256-channel STFT, z of 32 senders, the HERK padded 39 -> 48,
+    the 2D solver class, ISTFT and MMSE cost), asy, T = 10.01 s, against the
+    float64 oracle (pinned to the reference's batch fixtures at K = 3) for
+    two batch iterations (the oracle's per-bin eigh costs ~11 s per
+    iteration at D = 39)."""
+    from danse_amd.core import danse_batch
+    from oracle import danse_ref_cpu as O
+    from golden_cases import BATTERY
+    case = dict(name='batch_D_K32x8_asy', M=[8] * 32, dur=10.01, seed=61,
+                danse=dict(BATTERY, nodeUpdating='asy', simType='batch', maxBatchUpdates=2))
+    sc = make_case_scene(case)
+    dp, wp = make_case_params(case)
+    sc.get_vad_per_frame(dp.DFTsize, dp.Ns, wp.vadMinProportionActive)
+    out, _ = danse_batch(sc, dp)
+    ov = O.danse_batch(sc, dp, vadMinProp=wp.vadMinProportionActive)
+    K = 32
+    errs = [_bin_rel(out.wTilde[k][:, 1:3, :], ov.wTilde[k][:, 1:3, :]).ravel() for k in range(K)]
+    st = _stats(np.concatenate(errs))
+    de = rel_err(out.d, ov.d)
+    dhe = rel_err(out.dhat, ov.dhat)
+    cr = np.array(ov.mmseCost, dtype=float)
+    ce = float(np.max(np.abs(out.mmseCost - cr) / np.abs(cr)))
+    print(case['name'], 'w', st, 'd', de, 'dhat', dhe, 'cost', ce)
+    assert out.wTilde[0].shape[-1] == 39
+    assert st['median'] <= 1e-5 and st['p99'] <= 1e-4, st
+    assert de <= 1e-4 and dhe <= 1e-4 and ce <= 1e-4
