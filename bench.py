@@ -325,23 +325,27 @@ def run_online(args, wl, S, rank, world, local, dist, traffic=True, pmc_child=Fa
         torch.cuda.synchronize()
         eng.close()
         return None
+    # with the node-sharded runner the barriers and the max over ranks go
+    # over its gloo control group: an RCCL collective outside the captured
+    # rounds would corrupt the later graph replays (danse_amd/dist.py)
+    ctl = runner.ctl if runner is not None else None
     for _ in range(args.warmup):
         one_pass()
     torch.cuda.synchronize()
     if dist is not None:
-        dist.barrier()
+        dist.barrier(group=ctl)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     for _ in range(args.steps):
         one_pass()
     torch.cuda.synchronize()
     if dist is not None:
-        dist.barrier()
+        dist.barrier(group=ctl)
     torch.cuda.synchronize()
     el = time.perf_counter() - t1
     if dist is not None:
-        tt = torch.tensor([el], dtype=torch.float64, device=f'cuda:{local}')
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        tt = torch.tensor([el], dtype=torch.float64, device='cpu' if ctl is not None else f'cuda:{local}')
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX, group=ctl)
         el = float(tt.item())
     fu_per_step = Stot * K * F * R
     value = fu_per_step * args.steps / el

@@ -44,6 +44,7 @@ class DanseCfg(ctypes.Structure):
         ('fsTab', _p_i32), ('zStreamLen', _c_i32), ('scmInitPerBin', _c_i32),
         ('cohDrift', _c_i32), ('cdSegLength', _c_i32), ('cdStart', _c_i32), ('cdEvery', _c_i32),
         ('cdCompensate', _c_i32), ('cdNIter', _c_i32), ('cdAlpha', ctypes.c_double), ('cdAlphaEps', ctypes.c_double),
+        ('cEnd', _p_i32), ('cPhase', ctypes.POINTER(ctypes.c_double)),
     ]
 
 
@@ -61,6 +62,7 @@ class DanseBatchCfg(ctypes.Structure):
         ('k0', _c_i32),
         ('k1', _c_i32),
         ('tgt0', ctypes.c_void_p),
+        ('obs', _c_i32),
     ]
 
 

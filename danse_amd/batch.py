@@ -4,8 +4,10 @@
 ``BatchDANSEvariables`` (``danse_toolbox/d_batch.py:3-205``): frame VAD,
 padded-STFT frame count, update schedule (seq: node ``i mod K`` at batch
 iteration i, asy / sim: every node), initial filters and external-filter
-modes.  Device path only; fully connected, DANSE estimates only
-(centralised / local batch estimates are not on the device path).
+modes.  Device path only; fully connected.  The centralised and local batch
+estimates (``get_centralized_and_local_estimates``, ``d_batch.py:20-88``) and
+the best-performance reference (``get_best_perf``, ``d_core.py:602-627``) run
+on the same engine with another observation vector (``obs``).
 """
 from __future__ import annotations
 
@@ -23,12 +25,24 @@ from .outputs import stft_frames  # noqa: F401  (re-exported)
 class BatchEngine:
     """S same-shape scenes of one WASN shape, batch DANSE on one device."""
 
-    def __init__(self, scenes, p, device=0, costTrim=1000, nodeRange=None):
+    OBS = {'danse': 0, 'local': 1, 'centr': 2}
+
+    def __init__(self, scenes, p, device=0, costTrim=1000, nodeRange=None, obs='danse', yin='data', wGiven=None):
         """``nodeRange=(k0, k1)``: node-sharded batch DANSE -- this engine
         computes z for every node but SCMs, solves, external filters,
         estimates and costs only for nodes k0..k1-1; the other nodes'
         external filters arrive through :meth:`unpack_wext` (see
-        :func:`run_node_sharded`)."""
+        :func:`run_node_sharded`).
+
+        ``obs='local'`` / ``'centr'``: one batch filter update per node on
+        the node's own sensors / on every sensor of the WASN (centralised
+        VAD, reference index sum(M[:k]) + ref) into history slot 1, with its
+        estimate and untrimmed MMSE cost (pass ``costTrim=0``), as
+        ``get_centralized_and_local_estimates`` (``d_batch.py:20-88``) and
+        ``get_centralized_estimates`` (``d_batch.py:90-125``).  ``yin`` picks
+        the scene signal (``'cleannoise'`` / ``'cleanspeech'``: the
+        best-performance replays), ``wGiven[k]`` (F, >= 2, D) pre-given
+        filters whose slot 1 is used instead of a solve."""
         import torch
         self.torch = torch
         self.lib = L.load_library()
@@ -42,10 +56,11 @@ class BatchEngine:
         self.N, self.Ns = p.DFTsize, p.Ns
         self.F = F = self.N // 2 + 1
         self.T = T = sc0.wasn[0].data.shape[0]
-        if p.simType != 'batch':
+        if obs not in self.OBS:
+            raise ValueError(f'obs must be one of {sorted(self.OBS)}')
+        self.obs = obs
+        if obs == 'danse' and p.simType != 'batch':
             raise ValueError('BatchEngine runs simType batch')
-        if p.computeCentralised or p.computeLocal or p.computeSingleSensorBroadcast:
-            raise NotImplementedError('centralised / local / single-sensor batch estimates are not on the device path')
         for sc in self.scenes:
             if sc.nNodes != K or [n.nSensors for n in sc.wasn] != self.M or sc.wasn[0].data.shape[0] != T:
                 raise ValueError('all scenes of one engine must share the WASN shape')
@@ -59,14 +74,19 @@ class BatchEngine:
         if not 0 <= self.k0 < self.k1 <= K:
             raise ValueError(f'nodeRange {nodeRange} is not a non-empty range of the {K} nodes')
         self.Mmax = max(self.M)
-        self.iters = int(p.maxBatchUpdates)
+        self.iters = int(p.maxBatchUpdates) if obs == 'danse' else 1
         self.nIter = int((T - self.N) / self.Ns) + 1
         self.nseg = nseg = stft_frames(T, self.N, self.Ns)
         if nseg - 1 != self.nIter:
             # the reference's batch_estimate fails with a shape mismatch here (quirk Q9)
             raise ValueError('batch DANSE needs a signal length with (T - N) not a multiple of Ns (quirk Q9)')
-        self.D = [self.M[k] + K - 1 for k in range(K)]
-        # frame VAD, truncated to the STFT frames (update_covmats_batch)
+        base = np.concatenate(([0], np.cumsum(self.M)[:-1])).astype(int)
+        self.D = {'danse': [self.M[k] + K - 1 for k in range(K)], 'local': list(self.M),
+                  'centr': [self.Mtot] * K}[obs]
+        self.ref = [int(base[k] + p.referenceSensor) if obs == 'centr' else int(p.referenceSensor) for k in range(K)]
+        # frame VAD, truncated to the STFT frames (update_covmats_batch); the
+        # centralised vector uses the node average (active if any node is,
+        # init_from_wasn, d_classes.py:905-911)
         vad = np.zeros((S, K, nseg), dtype=np.uint8)
         for s, sc in enumerate(self.scenes):
             for k, nd in enumerate(sc.wasn):
@@ -74,9 +94,16 @@ class BatchEngine:
                 if len(v) < nseg:
                     raise ValueError('vadPerFrame shorter than the STFT frame count')
                 vad[s, k] = v
+            if obs == 'centr':
+                cv = (vad[s].astype(np.float64).sum(axis=0) / K).astype(bool)
+                vad[s] = cv[None, :]
         self._vad = np.ascontiguousarray(vad)
         doSolve = np.zeros((self.iters, K), dtype=np.uint8)
-        if 'seq' in p.nodeUpdating:
+        if wGiven is not None:
+            pass   # pre-given filters: slot 1 = slot 0 = wGiven[k][:, 1]
+        elif obs != 'danse':
+            doSolve[:] = 1
+        elif 'seq' in p.nodeUpdating:
             for it in range(self.iters):
                 doSolve[it, it % K] = 1
         else:
@@ -88,11 +115,19 @@ class BatchEngine:
         # slot 0; the other init types are the same in every slot
         Hr = max(self.iters + 1, self.nIter + 1)
 
-        def first(D):
+        def first(D, ref=p.referenceSensor):
             if p.filterInitType == 'random':
-                return init_complex_filter((F, Hr, D), p.referenceSensor, **fi)[:, 0, :]
-            return init_complex_filter((F, D), p.referenceSensor, **fi)
-        self._w0 = _cf32(np.concatenate([first(self.D[k]).ravel() for k in range(K)]))
+                return init_complex_filter((F, Hr, D), ref, **fi)[:, 0, :]
+            return init_complex_filter((F, D), ref, **fi)
+        self._hInit = [None] * K
+        if obs == 'danse':
+            self._w0 = _cf32(np.concatenate([first(self.D[k]).ravel() for k in range(K)]))
+        else:
+            # the family histories (F, nIter + 1, D) of init_from_wasn /
+            # init_from_wasn_for_best_perf (d_classes.py:378-411)
+            self._hInit = [init_complex_filter((F, self.nIter + 1, self.D[k]), self.ref[k], **fi) for k in range(K)]
+            src = [(wGiven[k][:, 1, :] if wGiven is not None else self._hInit[k][:, 0, :]) for k in range(K)]
+            self._w0 = _cf32(np.concatenate([np.ascontiguousarray(x).ravel() for x in src]))
         self._wExt0 = _cf32(np.concatenate([first(self.M[k]).ravel() for k in range(K)]))
         # wTildeExtTarget: its own (F, M) draw (d_classes.py:702-708)
         self._tgt0 = _cf32(np.concatenate([init_complex_filter((F, self.M[k]), p.referenceSensor, **fi).ravel()
@@ -131,16 +166,16 @@ class BatchEngine:
         c.tgt0 = self._tgt0.ctypes.data_as(ctypes.c_void_p)
         c.costTrim = int(costTrim)
         c.k0, c.k1 = self.k0, self.k1
+        c.obs = self.OBS[obs]
         self._cfg = c
         eng = ctypes.c_void_p()
         L.check_batch(self.lib.danse_batch_create(ctypes.byref(c), int(device), ctypes.byref(eng)))
         self.eng = eng
         y = np.empty((S, self.Mtot, T), dtype=np.float32)
         cl = np.empty((S, K, T), dtype=np.float32)
-        base = np.concatenate(([0], np.cumsum(self.M)[:-1])).astype(int)
         for s, sc in enumerate(self.scenes):
             for k, nd in enumerate(sc.wasn):
-                y[s, base[k]:base[k] + self.M[k], :] = nd.data.T
+                y[s, base[k]:base[k] + self.M[k], :] = getattr(nd, yin).T
                 cl[s, k] = nd.cleanspeech[:, p.referenceSensor]
         self.y = torch.from_numpy(y).to(f'cuda:{device}')
         self.clean = torch.from_numpy(cl).to(f'cuda:{device}')
@@ -243,6 +278,24 @@ class BatchEngine:
             res[s].filters = res[s].wTilde
         return res
 
+    def family_outputs(self):
+        """Outputs of an ``obs='local'`` / ``'centr'`` engine under the
+        reference's names: per scene ``w`` (list of (F, nIter + 1, D): the
+        init history with slot 1 from the solve), ``d`` (T, K), ``dhat``
+        (F, nIter, K), ``mmseCost`` (list of K)."""
+        out = []
+        for r in self.outputs():
+            o = BatchOutputs()
+            o.w = []
+            for k in range(self.K):
+                h = self._hInit[k].copy()
+                h[:, 1, :] = r.wTilde[k][:, 1, :]
+                o.w.append(h)
+            o.d, o.dhat = r.d, r.dhat
+            o.mmseCost = [float(x) for x in r.mmseCost[0]]
+            out.append(o)
+        return out
+
     def close(self):
         if getattr(self, 'eng', None):
             self.lib.danse_batch_destroy(self.eng)
@@ -275,12 +328,14 @@ def run_node_sharded(eng, exchange, blockNodes, stream=None, device=None):
     the other nodes' slots are filled from it before the next iteration's z.
     This is the one data exchange of batch DANSE: node k's estimate needs
     z_q = wExt_q^H y_q of every neighbour q (d_core.py:286-326)."""
+    import contextlib
     torch = eng.torch
     dev = device if device is not None else f'cuda:{eng.device}'
-    st = stream if stream is not None else torch.cuda.current_stream(eng.device)
+    cpu = str(dev) == 'cpu'
+    st = None if cpu else (stream if stream is not None else torch.cuda.current_stream(eng.device))
     # pack -> collective -> unpack must be ordered on ONE stream: the
     # collective runs on torch's current stream, so make ``st`` current
-    with torch.cuda.stream(st):
+    with (contextlib.nullcontext() if cpu else torch.cuda.stream(st)):
         buf = torch.zeros(blockNodes * eng.S * eng.wext_chunk(), dtype=torch.complex64, device=dev)
         for it in range(eng.iters):
             eng.run_iters(it, it + 1, st)

@@ -56,15 +56,48 @@ def danse(wasnObj, p, device=0, graph=True):
     return dv, wasnObj
 
 
-def danse_batch_multi(scenes, p, device=0):
-    """Batch DANSE on S same-shape scenes at once (device batch engine)."""
+def _family_batch(scenes, p, obs, device=0, yin='data', wGiven=None):
+    """One ``obs='local'`` / ``'centr'`` batch engine run (one filter update
+    per node, untrimmed MMSE cost); per-scene ``family_outputs``."""
     from .batch import BatchEngine
+    eng = BatchEngine(scenes, p, device=device, costTrim=0, obs=obs, yin=yin, wGiven=wGiven)
+    try:
+        eng.run()
+        return eng.family_outputs()
+    finally:
+        eng.close()
+
+
+def danse_batch_multi(scenes, p, device=0):
+    """Batch DANSE on S same-shape scenes at once (device batch engine).
+    With ``computeCentralised`` / ``computeLocal`` the centralised and local
+    batch estimates come first, as in ``d_core.danse_batch``
+    (``d_core.py:282-283``, ``get_centralized_and_local_estimates``,
+    ``d_batch.py:20-88``)."""
+    from .batch import BatchEngine
+    fam = {}
+    for name, on in (('Centr', p.computeCentralised), ('Local', p.computeLocal)):
+        if on:
+            fam[name] = _family_batch(scenes, p, 'centr' if name == 'Centr' else 'local', device=device)
     eng = BatchEngine(scenes, p, device=device)
     try:
         eng.run()
-        return eng.outputs()
+        res = eng.outputs()
     finally:
         eng.close()
+    for s, r in enumerate(res):
+        for name, outs in fam.items():
+            o = outs[s]
+            suf = name[0].lower()
+            setattr(r, f'w{name}', o.w)
+            setattr(r, f'd{name}', o.d)
+            setattr(r, f'dHat{name}', o.dhat)
+            setattr(r, f'mmseCost{name}', o.mmseCost)
+            # DANSEoutputs names (d_post.py:41-133)
+            setattr(r, f'filters{name}', o.w)
+            setattr(r, f'TDdesiredSignals_est_{suf}', o.d)
+            setattr(r, f'STFTDdesiredSignals_est_{suf}', o.dhat)
+    return res
 
 
 def danse_batch(wasnObj, p, device=0):
@@ -78,27 +111,61 @@ def danse_batch(wasnObj, p, device=0):
     return out, wasnObj
 
 
+class BestPerf:
+    """``get_best_perf``'s result (a ``BatchDANSEvariables`` in the
+    reference): the fields ``include_best_perf_data`` and the SNR replays
+    read (``d_post.py:152-182``)."""
+    pass
+
+
+def get_best_perf(wasnObj, p, wCentr=None, device=0):
+    """``d_core.get_best_perf`` (``d_core.py:602-627``) for fully connected
+    WASNs: centralised batch estimates without SROs
+    (``init_from_wasn_for_best_perf``, ``d_classes.py:378-470``;
+    ``get_centralized_estimates``, ``d_batch.py:90-125``) on the device batch
+    engine (``obs='centr'``).  The scene generator applies no resampling, so
+    the noSRO signals are the scene signals.  With ``p.preGivenFilters``
+    active the noise-only / speech-only signals are filtered with slot 1 of
+    ``wCentr``."""
+    pg = p.preGivenFilters
+    yin = 'data'
+    if pg.active:
+        yin = 'cleannoise' if pg.purpose == 'noise-only' else 'cleanspeech'
+    o = _family_batch([wasnObj], p, 'centr', device=device, yin=yin, wGiven=wCentr)[0]
+    bp = BestPerf()
+    bp.wCentr, bp.dCentr, bp.dHatCentr, bp.mmseCostCentr = o.w, o.d, o.dhat, o.mmseCost
+    bp.nNodes = wasnObj.nNodes
+    bp.referenceSensor = p.referenceSensor
+    bp.baseFs = wasnObj.wasn[p.referenceSensor].fs if hasattr(wasnObj, 'wasn') else None
+    bp.cleanSpeechSignalsAtNodes = [nd.cleanspeech for nd in wasnObj.wasn]
+    bp.cleanNoiseSignalsAtNodes = [nd.cleannoise for nd in wasnObj.wasn]
+    return bp
+
+
 def generate_signals_for_snr_computation(pD, dv, wasnObj, danse_function=danse, bestPerfRef=False, wCentrBatch=None):
     """``d_core.generate_signals_for_snr_computation`` (``d_core.py:550-599``):
-    noise-only and speech-only replays with the recorded filters.  The
-    best-performance reference (``get_best_perf``: centralised batch estimates
-    without SROs) is not on the device path."""
-    if bestPerfRef:
-        raise NotImplementedError('bestPerfReference (d_core.get_best_perf) is not on the device path')
+    noise-only and speech-only replays with the recorded filters, and with
+    ``bestPerfRef`` the same replays of the best-performance reference
+    (``get_best_perf`` with ``wCentrBatch``)."""
     pU = copy.deepcopy(pD)
     pU.preGivenFilters = PreComputedFilters(
         active=True, internalFilters=dv.wTilde, externalFilters=dv.wTildeExt,
         filtersCentr=getattr(dv, 'wCentr', []), filtersSSBC=getattr(dv, 'wSSBC', []),
         filtersLocal=getattr(dv, 'wLocal', []), purpose='noise-only')
     dv_n, _ = danse_function(wasnObj, pU)
+    bp_n = get_best_perf(wasnObj, pU, wCentr=wCentrBatch) if bestPerfRef else None
     pU.preGivenFilters.purpose = 'speech-only'
     dv_s, _ = danse_function(wasnObj, pU)
+    bp_s = get_best_perf(wasnObj, pU, wCentr=wCentrBatch) if bestPerfRef else None
     out = {}
     for key, src in (('n', dv_n), ('s', dv_s)):
         out[key] = src.d
         out[f'{key}_c'] = getattr(src, 'dCentr', None)
         out[f'{key}_l'] = getattr(src, 'dLocal', None)
         out[f'{key}_ssbc'] = getattr(src, 'dSSBC', None)
+    if bestPerfRef:
+        out['n_bp'] = bp_n.dCentr
+        out['s_bp'] = bp_s.dCentr
     return out
 
 

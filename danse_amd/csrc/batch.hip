@@ -95,8 +95,8 @@ __global__ void batch_z_kernel(const cf* __restrict__ Y, int S, int K, int MT, i
 }
 
 struct HerkNode {
-  int k, D, M;
-  int pad;
+  int k, D, M;        // M: leading channels read straight from the STFT (the rest are z)
+  int ybase;          // STFT channel of the first of them (base[k]; 0 for the centralised vector)
   long long scmOff;   // complex offset of this node's [S][F][D][D] block
 };
 
@@ -143,7 +143,7 @@ __global__ void __launch_bounds__(64) herk_kernel(const cf* __restrict__ Y, cons
     const int i = 16 * I + il;
     act[I] = i < D;
     if (i < Mk) {
-      src[I] = Y + ((long long)s * F + f) * nseg * MT + base[k] + i;
+      src[I] = Y + ((long long)s * F + f) * nseg * MT + nd.ybase + i;
       stride[I] = MT;
     } else {
       const int j = i - Mk;
@@ -519,6 +519,9 @@ struct danse_batch {
   std::string err;
   int S, K, MT, N, Ns, T, F, iters, nseg, gevd, rank, ref, trim;
   int k0 = 0, k1 = 0;   // owned nodes (node-sharded batch DANSE across GPUs)
+  int obs = 0;          // danse_batch_cfg.obs (0 DANSE, 1 local, 2 centralised)
+  std::vector<int> refK, ybase, ycnt;   // per node: reference index, direct STFT channels
+  int *dYBase = nullptr, *dYCnt = nullptr;
   float alphaExt;
   std::vector<int> M, base, D, extMode;
   std::vector<long long> scmOff, wOff, wExtOff, tgtOff;
@@ -580,7 +583,9 @@ int danse_batch_create(const danse_batch_cfg* c, int device, danse_batch** out) 
   if (c->N != 1024) return bfail(nullptr, "only DFTsize 1024 is supported");
   if (c->K < 2 || c->S < 1 || c->iters < 1 || c->nseg < 2) return bfail(nullptr, "bad sizes");
   if (c->rank < 1 || c->rank > kRMax) return bfail(nullptr, "GEVD rank out of range [1, 4]");
+  if (c->obs < 0 || c->obs > 2) return bfail(nullptr, "obs must be 0 (DANSE), 1 (local) or 2 (centralised)");
   eng = new danse_batch();
+  eng->obs = c->obs;
   eng->dev = device;
   BCHK(hipSetDevice(device));
   eng->S = c->S; eng->K = c->K; eng->N = c->N; eng->Ns = c->Ns; eng->T = c->T; eng->F = c->N / 2 + 1;
@@ -595,11 +600,17 @@ int danse_batch_create(const danse_batch_cfg* c, int device, danse_batch** out) 
   eng->base.resize(K);
   eng->D.resize(K);
   int mt = 0, Mmax = 0;
+  eng->refK.resize(K); eng->ybase.resize(K); eng->ycnt.resize(K);
   for (int k = 0; k < K; ++k) {
     eng->base[k] = mt;
     mt += eng->M[k];
     Mmax = std::max(Mmax, eng->M[k]);
-    eng->D[k] = eng->M[k] + K - 1;
+  }
+  for (int k = 0; k < K; ++k) {
+    eng->D[k] = c->obs == 0 ? eng->M[k] + K - 1 : (c->obs == 1 ? eng->M[k] : mt);
+    eng->refK[k] = c->obs == 2 ? eng->base[k] + c->ref : c->ref;
+    eng->ybase[k] = c->obs == 2 ? 0 : eng->base[k];
+    eng->ycnt[k] = c->obs == 2 ? mt : eng->M[k];
     if (eng->D[k] > kMaxDMax) return bfail(eng, "filter dimension > 64 not supported");
     if (c->ref >= eng->M[k]) return bfail(eng, "referenceSensor must be < M_k for every node");
     if (c->gevd && c->rank > eng->D[k]) return bfail(eng, "GEVD rank larger than a filter dimension");
@@ -612,7 +623,7 @@ int danse_batch_create(const danse_batch_cfg* c, int device, danse_batch** out) 
     eng->wOff[k] = wo; wo += (long long)H * F * eng->D[k];
     eng->wExtOff[k] = eo; eo += (long long)H * F * eng->M[k];
     eng->tgtOff[k] = to; to += (long long)F * eng->M[k];
-    eng->nodes.push_back(HerkNode{k, eng->D[k], eng->M[k], 0, eng->scmOff[k]});
+    eng->nodes.push_back(HerkNode{k, eng->D[k], eng->ycnt[k], eng->ybase[k], eng->scmOff[k]});
   }
   eng->scmStride = so;   // Ryy / Rnn are node-major [k][S][F][D][D] (not per scene)
   eng->wStride = wo; eng->wExtStride = eo; eng->tgtStride = to;
@@ -650,6 +661,9 @@ int danse_batch_create(const danse_batch_cfg* c, int device, danse_batch** out) 
   BCHK(balloc(&eng->dFrames, frames.size())); BCHK(balloc(&eng->dNvad, nv.size()));
   BCHK(balloc(&eng->dWOff, K)); BCHK(balloc(&eng->dWExtOff, K)); BCHK(balloc(&eng->dTgtOff, K));
   BCHK(balloc(&eng->dNodes, K));
+  BCHK(balloc(&eng->dYBase, K)); BCHK(balloc(&eng->dYCnt, K));
+  BCHK(hipMemcpy(eng->dYBase, eng->ybase.data(), K * sizeof(int), hipMemcpyHostToDevice));
+  BCHK(hipMemcpy(eng->dYCnt, eng->ycnt.data(), K * sizeof(int), hipMemcpyHostToDevice));
   BCHK(balloc(&eng->dWin, c->N)); BCHK(balloc(&eng->dBetaExt, (size_t)S * K));
   BCHK(balloc(&eng->dTw, wfft::kTwElems));
   BCHK(hipMemcpy(eng->dM, eng->M.data(), K * sizeof(int), hipMemcpyHostToDevice));
@@ -706,7 +720,7 @@ void danse_batch_destroy(danse_batch* eng) {
   void* ptrs[] = {eng->dM, eng->dBase, eng->dD, eng->dExtMode, eng->dFrames, eng->dNvad, eng->dWOff, eng->dWExtOff,
                   eng->dTgtOff, eng->dNodes, eng->dWin, eng->dBetaExt, eng->dTw, eng->Y, eng->Z, eng->Ryy, eng->Rnn,
                   eng->wHist, eng->wExtHist, eng->tgt, eng->dhat, eng->dFramesTD, eng->dD_, eng->dCost, eng->wTmp,
-                  eng->dDiag, eng->dCostPart};
+                  eng->dDiag, eng->dCostPart, eng->dYBase, eng->dYCnt};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (hipEvent_t e : eng->ev) (void)hipEventDestroy(e);
@@ -792,9 +806,11 @@ int danse_batch_run_iters(danse_batch* eng, int32_t it0, int32_t it1, void* stre
   };
   for (int it = it0; it < it1; ++it) {
     mark(it, 0);
-    hipLaunchKernelGGL(batch_z_kernel, dim3(2048), dim3(256), 0, st, eng->Y, S, K, eng->MT, nseg, eng->dM, eng->dBase,
-                       eng->wExtHist, eng->dWExtOff, eng->wExtStride, it, eng->Z);
-    BCHK(hipGetLastError());
+    if (eng->obs == 0) {
+      hipLaunchKernelGGL(batch_z_kernel, dim3(2048), dim3(256), 0, st, eng->Y, S, K, eng->MT, nseg, eng->dM, eng->dBase,
+                         eng->wExtHist, eng->dWExtOff, eng->wExtStride, it, eng->Z);
+      BCHK(hipGetLastError());
+    }
     mark(it, 1);
     launch_herk(eng, st);
     BCHK(hipGetLastError());
@@ -814,10 +830,10 @@ int danse_batch_run_iters(danse_batch* eng, int32_t it0, int32_t it1, void* stre
         continue;
       }
       int k1 = k + 1;
-      while (k1 < eng->k1 && eng->D[k1] == D && eng->doSolve[(size_t)it * K + k1]) ++k1;
+      while (k1 < eng->k1 && eng->D[k1] == D && eng->refK[k1] == eng->refK[k] && eng->doSolve[(size_t)it * K + k1]) ++k1;
       const cd* Ry = eng->Ryy + eng->scmOff[k];
       const cd* Rn = eng->Rnn + eng->scmOff[k];
-      if (!launch_filter_update_class(class_dmax(D), Ry, Rn, (k1 - k) * S * F, D, eng->gevd, eng->rank, eng->ref,
+      if (!launch_filter_update_class(class_dmax(D), Ry, Rn, (k1 - k) * S * F, D, eng->gevd, eng->rank, eng->refK[k],
                                       eng->wTmp, eng->dDiag, st))
         return bfail(eng, "no solver class for this filter dimension");
       hipLaunchKernelGGL(batch_wstore_kernel, dim3(1024), dim3(256), 0, st, eng->wTmp, k1 - k, S, F * D, k,
@@ -826,6 +842,7 @@ int danse_batch_run_iters(danse_batch* eng, int32_t it0, int32_t it1, void* stre
       k = k1;
     }
     mark(it, 3);
+    if (eng->obs == 0)
     hipLaunchKernelGGL(batch_ext_kernel, dim3(512), dim3(256), 0, st, S, K, it, eng->dM, eng->dD, eng->dExtMode,
                        eng->ref, eng->dBetaExt, eng->alphaExt, eng->wHist, eng->dWOff, eng->wStride, H, eng->wExtHist,
                        eng->dWExtOff, eng->wExtStride, eng->tgt, eng->dTgtOff, eng->tgtStride, Mmax, k0,
@@ -835,8 +852,8 @@ int danse_batch_run_iters(danse_batch* eng, int32_t it0, int32_t it1, void* stre
     {
       const int nfr = nseg - 1;
       const unsigned g = (unsigned)((long long)S * F * ((nfr + kDhTC - 1) / kDhTC));
-      hipLaunchKernelGGL(batch_dhat_kernel, dim3(g), dim3(kDhThr), 0, st, eng->Y, eng->Z, S, K, eng->MT, nseg, eng->dM,
-                         eng->dBase, eng->dD, eng->Dmax, eng->wHist, eng->dWOff, eng->wStride, it + 1, eng->dhat, k0,
+      hipLaunchKernelGGL(batch_dhat_kernel, dim3(g), dim3(kDhThr), 0, st, eng->Y, eng->Z, S, K, eng->MT, nseg, eng->dYCnt,
+                         eng->dYBase, eng->dD, eng->Dmax, eng->wHist, eng->dWOff, eng->wStride, it + 1, eng->dhat, k0,
                          nOwn);
       BCHK(hipGetLastError());
       mark(it, 5);

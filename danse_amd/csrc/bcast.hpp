@@ -54,6 +54,8 @@ struct BcastArgs {
   const float* normVal;    // [Ns] OLA normalisation h^2[n] + h^2[n+Ns]
   const cf* tw;            // wave-FFT twiddle table (wfft::kTwElems)
   int dbg;                 // diagnostic ablation mask (DANSE_BCAST_ABLATE; 0 in production)
+  const int* cEnd;         // [R*K] raw stream end of the centralised frame (danse_cfg.cEnd) or null
+  cf* Cspec;               // [2][S][MT][F] (slot r & 1)
 };
 
 // y[(frame end - N) .. frame end) * win, zero before sample 0 -> buf (complex, imag 0)
@@ -114,19 +116,25 @@ __global__ void __launch_bounds__(256) bcast_kernel(const BcastArgs a) {
     cf zp[16];
 #pragma unroll
     for (int c = 0; c < 16; ++c) zp[c] = cf{0.0f, 0.0f};
-    const int nJobs = needUp ? 2 * Mk : Mk;
+    // jobs: [0, Mk) broadcast frames, then the update frames (needUp), then
+    // the raw frames y[cEnd - N, cEnd) of the centralised buffers (cEnd)
+    const int nUp = needUp ? Mk : 0;
+    const int nJobs = Mk + nUp + (a.cEnd ? Mk : 0);
     for (int j = wv; j < nJobs; j += kBcWaves) {
-      const bool up = j >= Mk;
-      const int m = up ? j - Mk : j;
+      const int kind = (j < Mk) ? 0 : (j < Mk + nUp ? 1 : 2);
+      const bool up = kind == 1;
+      const int m = j - (kind == 0 ? 0 : (kind == 1 ? Mk : Mk + nUp));
       const int ch = a.base[k] + m;
+      const int fend = kind == 0 ? bEnd : (kind == 1 ? uEnd : a.cEnd[r * a.K + k]);
       cf v[16];
       if (a.dbg & 8) {
         for (int jj = 0; jj < 16; ++jj) v[jj] = cf{(float)(jj + threadIdx.x), 0.0f};
       } else {
-        load_frame_wave(v, a.y + ((long long)s * a.MT + ch) * a.T, up ? uEnd : bEnd, a.T, a.hA);
+        load_frame_wave(v, a.y + ((long long)s * a.MT + ch) * a.T, fend, a.T, a.hA);
       }
       if (!(a.dbg & 64)) wfft::fft1024(v, L, a.tw);
-      cf* dst = a.Yspec + (((long long)((up ? r + 1 : r) & 1) * a.S + s) * a.MT + ch) * F;
+      cf* dst = (kind == 2) ? a.Cspec + (((long long)(r & 1) * a.S + s) * a.MT + ch) * F
+                            : a.Yspec + (((long long)((up ? r + 1 : r) & 1) * a.S + s) * a.MT + ch) * F;
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
         const int f = wfft::out_index(c);
@@ -134,7 +142,7 @@ __global__ void __launch_bounds__(256) bcast_kernel(const BcastArgs a) {
           const cf Y = invSqNs * v[c];
           if (!(a.dbg & 32)) dst[f] = Y;
           // (fewSamples: z comes from the T(z) chunk, no fused spectrum here)
-          if (!up && !a.fsTab) zp[c] = zp[c] + ((a.dbg & 16) ? Y : cmul(wx[(long long)f * Mk + m], Y));
+          if (kind == 0 && !a.fsTab) zp[c] = zp[c] + ((a.dbg & 16) ? Y : cmul(wx[(long long)f * Mk + m], Y));
         }
       }
     }

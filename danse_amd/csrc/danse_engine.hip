@@ -95,6 +95,11 @@ struct danse_engine {
   std::vector<int> fsTab;          // host copy [R][K][DANSE_FS_FIELDS]
   int* dFsTab = nullptr;
   float *wIR = nullptr, *dSn = nullptr;
+  // centralised / SSBC raw frames under asynchronous clocks (cfg.cEnd)
+  int* dCEnd = nullptr;
+  cf* Cspec = nullptr;
+  int* dChanNode = nullptr;
+  double* dCPhase = nullptr;
 };
 
 static thread_local std::string g_lastErr;
@@ -249,6 +254,7 @@ int danse_engine_reset(danse_engine* eng, void* stream) {
     HIPCHK(hipMemsetAsync(eng->cdRes, 0, (size_t)S * K * (K - 1) * R * sizeof(double), st));
   }
   HIPCHK(hipMemsetAsync(eng->Zspec, 0, (size_t)2 * K * S * F * sizeof(cf), st));
+  if (eng->Cspec) HIPCHK(hipMemsetAsync(eng->Cspec, 0, (size_t)2 * S * eng->MT * F * sizeof(cf), st));
   HIPCHK(hipMemsetAsync(eng->zStream, 0, (size_t)S * K * eng->zLen * sizeof(float), st));
   if (eng->wIR) {
     HIPCHK(hipMemsetAsync(eng->wIR, 0, (size_t)S * K * eng->Mmax * tzc::kA * sizeof(float), st));
@@ -318,8 +324,11 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
   for (int k = 0; k < K; ++k)
     if (c->ref >= eng->M[k]) return fail(eng, "referenceSensor must be < M_k for every node");
 
-  // ---- family-node table (owned nodes), channel lists
+  // ---- family-node table (owned nodes), channel lists; with cEnd the other
+  // nodes' channels of the centralised / SSBC vectors are raw-frame codes
+  // (MT + K + channel, kernels.hpp load_y)
   long long scmOff = 0, wOff = 0, liOff = 0;
+  const int rawBase = mt + K;
   const long long histW = c->keepHistory ? (long long)R + 1 : 2;
   for (int fam = 0; fam < kMaxFam; ++fam) {
     if (!((eng->families >> fam) & 1)) continue;
@@ -330,7 +339,8 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
       if (fam == DANSE_FAM_DANSE || fam == DANSE_FAM_SSBC) {
         for (int m = 0; m < eng->M[k]; ++m) eng->chanList.push_back(eng->base[k] + m);
         for (int q = 0; q < K; ++q)
-          if (q != k) eng->chanList.push_back(fam == DANSE_FAM_DANSE ? mt + q : eng->base[q]);
+          if (q != k)
+            eng->chanList.push_back(fam == DANSE_FAM_DANSE ? mt + q : (c->cEnd ? rawBase : 0) + eng->base[q]);
         fn.D = eng->M[k] + K - 1;
         fn.ref = c->ref;
       } else if (fam == DANSE_FAM_LOCAL) {
@@ -338,7 +348,9 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
         fn.D = eng->M[k];
         fn.ref = c->ref;
       } else {
-        for (int ch = 0; ch < mt; ++ch) eng->chanList.push_back(ch);
+        for (int q = 0; q < K; ++q)
+          for (int m = 0; m < eng->M[q]; ++m)
+            eng->chanList.push_back((q != k && c->cEnd ? rawBase : 0) + eng->base[q] + m);
         fn.D = mt;
         fn.ref = eng->base[k] + c->ref;
       }
@@ -451,6 +463,22 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
   const size_t MT = (size_t)eng->MT;
   HIPCHK(dalloc(&eng->Yspec, 2 * S * MT * F));
   HIPCHK(dalloc(&eng->Zspec, (size_t)2 * K * S * F));
+  if (c->cEnd) {
+    for (int i = 0; i < R * K; ++i)
+      if (c->cEnd[i] < 0 || c->cEnd[i] > c->T + c->N) return fail(eng, "cEnd outside the signal");
+    std::vector<int> chanNode;
+    for (int q = 0; q < K; ++q)
+      for (int m = 0; m < eng->M[q]; ++m) chanNode.push_back(q);
+    HIPCHK(dalloc(&eng->dCEnd, (size_t)R * K));
+    HIPCHK(hipMemcpy(eng->dCEnd, c->cEnd, (size_t)R * K * sizeof(int), hipMemcpyHostToDevice));
+    HIPCHK(dalloc(&eng->dChanNode, MT));
+    HIPCHK(hipMemcpy(eng->dChanNode, chanNode.data(), MT * sizeof(int), hipMemcpyHostToDevice));
+    HIPCHK(dalloc(&eng->Cspec, (size_t)2 * S * MT * F));
+  }
+  if (c->cPhase) {
+    HIPCHK(dalloc(&eng->dCPhase, (size_t)R * K * MT));
+    HIPCHK(hipMemcpy(eng->dCPhase, c->cPhase, (size_t)R * K * MT * sizeof(double), hipMemcpyHostToDevice));
+  }
   HIPCHK(dalloc(&eng->zPrev, (size_t)S * K * c->N));
   HIPCHK(dalloc(&eng->zStream, (size_t)S * K * eng->zLen));
   if (c->fsTab) {
@@ -585,7 +613,7 @@ void danse_engine_destroy(danse_engine* eng) {
                   eng->diag, eng->dW0, eng->dScm0, eng->dExt0, eng->dTgt0, eng->dFnAll, eng->dInitW0Off,
                   eng->dInitScmOff, eng->dExtSrcOff, eng->dTgtOff, eng->dFsTab, eng->wIR, eng->dSn, eng->liCache,
                   eng->dGateCand, eng->dGateVerdict, eng->cdRing, eng->cdAvg, eng->cdPhase, eng->cdEst,
-                  eng->cdRes};
+                  eng->cdRes, eng->dCEnd, eng->Cspec, eng->dChanNode, eng->dCPhase};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (auto& cl : eng->classes) {
@@ -613,6 +641,7 @@ static BcastArgs make_bcast(danse_engine* e, int r, int synth, int bc) {
   a.dbg = e->bcastAblate;
   a.zLen = e->zLen;
   a.fsTab = e->dFsTab;
+  a.cEnd = e->dCEnd; a.Cspec = e->Cspec;
   return a;
 }
 
@@ -628,6 +657,7 @@ static UpdateArgs make_update(danse_engine* e, int r) {
   a.betaExt = e->dBetaExt; a.alphaExt = e->alphaExt; a.gevd = e->gevd; a.rank = e->rank; a.diag = e->diag;
   a.liCache = e->liCache; a.liStride = e->liStride;
   a.cdPhase = e->cdPhase;
+  a.Cspec = e->Cspec; a.chanNode = e->dChanNode; a.cPhase = e->dCPhase;
   return a;
 }
 

@@ -70,7 +70,23 @@ struct UpdateArgs {
   cf* liCache;             // GEVD factor cache per family-node [NT + D][F] (Li = L^-1 packed, g = L^H e_ref)
   const double* cdPhase;   // CohDrift phase accumulator [S][K][K] (adds to zPhase), or null
   long long liStride;      // per scene; null cache = always refactor
+  // centralised / SSBC under asynchronous clocks (danse_cfg.cEnd): channel
+  // codes >= MT + K name raw channel (code - MT - K) of another node, read
+  // from Cspec [2][S][MT][F] (slot r & 1 holds the senders' round-r raw
+  // frames) with that sender's zLag
+  const cf* Cspec;
+  const int* chanNode;     // [MT] node of each channel
+  const double* cPhase;    // [R][K][MT] centralised compensation phase (samples), or null
 };
+
+// yhat *= exp(-j 2 pi f phi / N) (compensate_sros, d_classes.py:1936-2046)
+DANSE_DEV cf sro_rotate(cf v, int f, int F, double ph) {
+  double t = (double)f * ph / (double)(2 * (F - 1));
+  t -= rint(t);
+  float sn, cs;
+  sincospif(-2.0f * (float)t, &sn, &cs);
+  return v * cf{cs, sn};
+}
 
 // The factor of Rnn cached by the last solve of this (scene, family-node) is
 // still the factor of the current Rnn: no Rnn update since that solve (the
@@ -95,9 +111,17 @@ DANSE_DEV bool li_reusable(const UpdateArgs& a, const FamNode& d, int s, int opN
 DANSE_DEV cf load_y(const UpdateArgs& a, const FamNode& d, int s, int f, int li, bool act) {
   const int F = a.F, r = a.r;
   const int c = a.chanList[d.chanOff + (act ? li : 0)];
+  const int rawBase = a.MT + a.K;
   cf v;
   if (c < a.MT) {
     v = a.Yspec[(((long long)((r + 1) & 1) * a.S + s) * a.MT + c) * F + f];
+  } else if (c >= rawBase) {
+    // another node's raw channel in the centralised / SSBC vector
+    // (process_incoming_signals_buffers_centr, d_classes.py:1809-1891)
+    const int ch = c - rawBase;
+    const int q = a.chanNode[ch];
+    const int lag = a.zLag ? a.zLag[((long long)r * a.K + d.k) * a.K + q] : 0;
+    v = a.Cspec[(((long long)((r - lag) & 1) * a.S + s) * a.MT + ch) * F + f];
   } else {
     const int q = c - a.MT;
     const long long lk = ((long long)r * a.K + d.k) * a.K + q;
@@ -106,12 +130,14 @@ DANSE_DEV cf load_y(const UpdateArgs& a, const FamNode& d, int s, int f, int li,
     if (a.zPhase) {
       double ph = a.zPhase[lk];
       if (a.cdPhase) ph += a.cdPhase[((long long)s * a.K + d.k) * a.K + q];
-      double t = (double)f * ph / (double)(2 * (F - 1));
-      t -= rint(t);
-      float sn, cs;
-      sincospif(-2.0f * (float)t, &sn, &cs);
-      v = v * cf{cs, sn};
+      v = sro_rotate(v, f, F, ph);
     }
+  }
+  if (a.cPhase && d.fam == DANSE_FAM_CENTR) {
+    // phaseShiftFactorsCentr of every channel of the centralised vector
+    // (d_classes.py:1996-2038), own channels included
+    const int ch = (c < a.MT) ? c : c - rawBase;
+    v = sro_rotate(v, f, F, a.cPhase[((long long)r * a.K + d.k) * a.MT + ch]);
   }
   return csel(act, v, cf{0.0f, 0.0f});
 }

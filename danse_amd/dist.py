@@ -76,6 +76,12 @@ class ShardedRun:
         if self.stage:
             self.hslot = [torch.zeros(per, dtype=torch.float32) for _ in range(self.slots)]
         self.graph = (backend == 'nccl') if graph is None else bool(graph)
+        # host-side control traffic (gate verdicts, callers' barriers) on a
+        # gloo group: an RCCL collective issued outside the captured graph on
+        # the graph's communicator (or a second one) between two replays makes
+        # the later replays diverge from the eager run
+        # (profiles/round3/rccl_graph_mixing_r3d.log)
+        self.ctl = dist.new_group(backend='gloo') if backend == 'nccl' else group
         self._graphs = {}
         self._eager_runs = 0
 
@@ -121,10 +127,14 @@ class ShardedRun:
         g.replay()
 
     def _all_ok(self, ok):
-        t = self.torch.tensor([1 if ok else 0], dtype=self.torch.int32,
-                              device='cpu' if self.zbuf.device.type == 'cpu' or self.stage else self.zbuf.device)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN, group=self.group)
+        gloo = self.ctl is not self.group or self.zbuf.device.type == 'cpu' or self.stage
+        t = self.torch.tensor([1 if ok else 0], dtype=self.torch.int32, device='cpu' if gloo else self.zbuf.device)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN, group=self.ctl)
         return bool(int(t.item()))
+
+    def barrier(self):
+        """A barrier that leaves the captured RCCL rounds intact (gloo)."""
+        self.dist.barrier(group=self.ctl)
 
     def run(self, reset=True, gate=True):
         e = self.eng

@@ -28,7 +28,7 @@ from dataclasses import dataclass
 import numpy as np
 
 from . import _lib as L
-from .scheduler import initialize_events, compile_rounds, compile_rounds_fs
+from .scheduler import initialize_events, compile_rounds, compile_rounds_fs, FS_BCEND, FS_LEN, FS_POS, FS_ZEND
 from .outputs import host_fields, stft_frames
 
 
@@ -163,10 +163,11 @@ class DanseEngine:
             # local spectra and the centralised VAD averages every node's VAD;
             # a node-sharded engine only analyses (and only has) its own nodes
             raise NotImplementedError('centralised / single-sensor-broadcast estimates on a node-sharded engine')
-        if not self.rt.synchronous and (p.computeCentralised or p.computeSingleSensorBroadcast):
-            raise NotImplementedError('centralised / single-sensor-broadcast estimates with asynchronous (SRO) '
-                                      'clocks are not on the device path')
+        if p.computeSingleSensorBroadcast and p.compensateSROs:
+            # compensate_sros raises here too (d_classes.py:2042-2044)
+            raise NotImplementedError('SRO compensation for single-sensor broadcast not implemented yet.')
         self._build_sro_tables(sc0)
+        self._build_centr_tables(sc0)
         if R < 1:
             raise ValueError('signal too short for one DANSE round')
         if R > self.nIter:
@@ -272,6 +273,79 @@ class DanseEngine:
                 ph[r, k, :] = phi
                 phi[nb] -= est * self.Ns
         self._zPhase = ph
+
+    def _build_centr_tables(self, sc0):
+        """Raw-signal frames of the centralised / SSBC observation vectors
+        under asynchronous clocks (``pre_fill_buffers_centralised`` /
+        ``fill_buffers_centr`` / ``process_incoming_signals_buffers_centr``,
+        ``d_classes.py:1162-1183,1226-1250,1809-1891``).  Every broadcast of
+        sender q appends the same number of raw samples to the centralised
+        buffers as to the z buffers (Ns first samples of the broadcast frame
+        for wholeChunk, the last currL for fewSamples), so the buffer flags are
+        the z flags and receiver k's frame of q is the last N samples of q's
+        raw stream: y_q[E - N, E) with E = ``cEnd[r][q]`` (the stream is
+        contiguous from sample 0, checked here), read with the z lag.  The
+        compensation phase of the centralised vector (``compensate_sros``,
+        ``d_classes.py:1996-2038``) keeps the reference's flag index
+        arithmetic (quirk Q14: the flag of sender q lands on
+        ``[sum(nbM[:q]), sum(nbM[:q + 1]))`` of the neighbour-size list nbM
+        of node k, one channel past its end when empty) and its Oracle
+        estimate index ``[sum(M[:q]), sum(M[:q + 1]))``
+        (``update_sro_estimates``, ``d_classes.py:2364-2621``)."""
+        p, K, R, N, Ns = self.p, self.K, self.R, self.N, self.Ns
+        self._cEnd = None
+        self._cPhase = None
+        if self.rt.synchronous or not (p.computeCentralised or p.computeSingleSensorBroadcast):
+            return
+        if self.fewSamples:
+            tab = self.rt.fsTab
+            cEnd = np.zeros((R, K), dtype=np.int64)
+            for q in range(K):
+                off = None
+                for r in range(R):
+                    ln = int(tab[r, q, FS_LEN])
+                    if ln > 0:
+                        o = int(tab[r, q, FS_BCEND]) - int(tab[r, q, FS_POS]) - ln
+                        if off is None:
+                            off = o
+                        elif o != off:
+                            raise NotImplementedError(f'node {q} raw broadcast stream is not contiguous')
+                if off not in (None, 0):
+                    raise NotImplementedError(f'node {q} raw broadcast stream does not start at sample 0')
+                cEnd[:, q] = tab[:R, q, FS_ZEND]
+        else:
+            bc = self.rt.bcEnd[:R]
+            if R > 1 and not np.all(np.diff(bc, axis=0) == Ns):
+                raise NotImplementedError('consecutive broadcast frames not Ns samples apart (raw stream gap)')
+            cEnd = bc - N + Ns
+        self._cEnd = np.ascontiguousarray(cEnd, dtype=np.int32)
+        if not (p.compensateSROs and p.computeCentralised):
+            return
+        sro = np.array([nd.sro for nd in sc0.wasn], dtype=np.float64)
+        M = self.M
+        MT = self.Mtot
+        ph = np.zeros((R, K, MT), dtype=np.float64)
+        for k in range(K):
+            nbM = [M[q] for q in range(K) if q != k]
+            phi = np.zeros(MT, dtype=np.float64)
+            for r in range(R):
+                if p.includeFSDflags:
+                    extra = np.zeros(MT)
+                    for q in range(K):
+                        if q == k:
+                            continue
+                        b = int(np.sum(nbM[:q]))
+                        e = int(np.sum(nbM[:q + 1]))
+                        if e == b:
+                            e += 1
+                        extra[b:e] = self.rt.flags[r, k, q]
+                    phi += extra
+                ph[r, k, :] = phi
+                for q in range(K):
+                    b = int(np.sum(M[:q]))
+                    e = int(np.sum(M[:q + 1]))
+                    phi[b:e] -= (sro[q] - sro[k]) * 1e-6 * Ns
+        self._cPhase = ph
 
     def _flags_for(self, s, f, k, start):
         """Control bytes of one (scene, family, node) for a start round
@@ -431,6 +505,8 @@ class DanseEngine:
             c.cdCompensate = int(bool(p.compensateSROs))
             c.cdNIter = int(self.nIter)
             c.cdAlpha, c.cdAlphaEps = float(cd.alpha), float(cd.alphaEps)
+        c.cEnd = _ptr(self._cEnd, ctypes.c_int32)
+        c.cPhase = _ptr(self._cPhase, ctypes.c_double)
         c.zStreamLen = int(self.rt.zStreamLen) if self.fewSamples else 0
         self.zLen = c.zStreamLen if self.fewSamples else self.R * self.Ns
         self._cfg = c

@@ -184,3 +184,21 @@ class DANSEoutputs:
         self.TDfiltSpeech_ssbc = snrSigs['s_ssbc']
         self.TDfiltNoise_ssbc = snrSigs['n_ssbc']
         return self
+
+    def include_best_perf_data(self, outBP, sigsSnr: dict):
+        """``DANSEoutputs.include_best_perf_data`` (``d_post.py:152-182``):
+        the best-performance reference (``core.get_best_perf``)."""
+        self.bestPerfData = {
+            'dCentr': outBP.dCentr,
+            'dHatCentr': outBP.dHatCentr,
+            'dCentr_s': sigsSnr['s_bp'],
+            'dCentr_n': sigsSnr['n_bp'],
+            'mseCostCentr': outBP.mmseCostCentr,
+            'wCentr': outBP.wCentr,
+            'fs': outBP.baseFs,
+            'cleanSpeech': np.array([outBP.cleanSpeechSignalsAtNodes[k][:, outBP.referenceSensor]
+                                     for k in range(outBP.nNodes)]).T,
+            'cleanNoise': np.array([outBP.cleanNoiseSignalsAtNodes[k][:, outBP.referenceSensor]
+                                    for k in range(outBP.nNodes)]).T,
+        }
+        return self

@@ -11,9 +11,8 @@ replays, and ``format_output``.  Differences, all loud:
   (``trueRoom``, ``signalType='from_file'``) raise NotImplementedError;
 * ``postprocess`` (metrics, plots, exports; ``sandbox.py:162-``) is out of
   scope: ``main`` returns the formatted ``DANSEoutputs``;
-* ``bestPerfReference`` (``d_core.get_best_perf``) and TI-DANSE (ad-hoc
-  topologies) raise NotImplementedError, as the reference does for batch
-  DANSE in ``danse_it_up``.
+* TI-DANSE (ad-hoc topologies) raises NotImplementedError, as the reference
+  does for batch DANSE in ``danse_it_up``.
 """
 from __future__ import annotations
 
@@ -72,11 +71,14 @@ def danse_it_up(wasnObj, p: TestParameters):
         # the reference raises here too (sandbox.py:116-117); core.danse_batch
         # runs batch mode directly
         raise NotImplementedError('Batch mode not implemented / tested yet.')
-    if p.exportParams.bestPerfReference:
-        raise NotImplementedError('bestPerfReference (d_core.get_best_perf) is not on the device path: set '
-                                  'exportParams.bestPerfReference = False')
     danse_function = core.danse
     dv, wasnObj = danse_function(*args)
-    sigsSnr = core.generate_signals_for_snr_computation(p.danseParams, dv, wasnObj, danse_function, False)
+    bp = p.exportParams.bestPerfReference
+    # best possible performance (centralised, no SROs, batch), sandbox.py:132-155
+    outBP = core.get_best_perf(*args) if bp else None
+    sigsSnr = core.generate_signals_for_snr_computation(p.danseParams, dv, wasnObj, danse_function, bp,
+                                                        wCentrBatch=outBP.wCentr if bp else None)
     out, wasnObj = core.format_output(p.danseParams, dv, wasnObj, sigsSnr=sigsSnr)
+    if bp:
+        out.include_best_perf_data(outBP, sigsSnr)
     return out, wasnObj

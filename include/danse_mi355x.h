@@ -140,6 +140,20 @@ typedef struct danse_cfg {
   int32_t cdNIter;          /* the reference's nIter (estimation stops there)   */
   double cdAlpha;           /* alpha                                            */
   double cdAlphaEps;        /* alphaEps                                         */
+  /* Centralised / single-sensor-broadcast observation vectors under
+   * asynchronous clocks.  The reference sends every node's raw signals
+   * through per-receiver buffers next to z (pre_fill_buffers_centralised /
+   * fill_buffers_centr / process_incoming_signals_buffers_centr,
+   * d_classes.py:1162-1183,1226-1250,1809-1891): receiver k's frame of sender
+   * q is the last N samples of q's raw-signal stream, y_q[E - N, E).  The
+   * device analyses that frame once per (round, sender) and the receivers
+   * read it with the sender's zLag (0 without zLag).  NULL = synchronous: the
+   * receivers use the senders' update-frame spectra.                        */
+  const int32_t* cEnd;      /* [R*K] raw stream end E of sender q's round-r frame */
+  const double* cPhase;     /* [R*K*MT] SRO phase offset (samples) of centralised
+                               channel c at node k's update r (phaseShiftFactors-
+                               Centr, compensate_sros d_classes.py:1996-2038 and
+                               update_sro_estimates 2364-2621); NULL = none     */
 } danse_cfg;
 
 /* Fields of one fsTab entry (round r, node k). */
@@ -305,6 +319,16 @@ typedef struct danse_batch_cfg {
                               cost for the owned ones); k1 <= k0: all nodes     */
   const float* tgt0;       /* initial external-filter targets (wTildeExtTarget,
                               d_classes.py:702-708), layout of wExt0; NULL: wExt0 */
+  int32_t obs;             /* observation vector: 0 DANSE (local mics + the other
+                              nodes' z), 1 local (the node's own mics), 2
+                              centralised (every sensor of the WASN, reference
+                              index sum(M[:k]) + ref): the batch centralised /
+                              local estimates (get_centralized_and_local_estimates,
+                              d_batch.py:20-88) and the best-performance
+                              reference (get_best_perf, d_core.py:602-627;
+                              get_centralized_estimates, d_batch.py:90-125).
+                              With obs != 0 there are no z and no external
+                              filters; doSolve = 0 keeps the pre-given w0.    */
 } danse_batch_cfg;
 
 typedef struct danse_batch danse_batch;

@@ -1025,4 +1025,106 @@ class BatchDANSE:
 
 
 def danse_batch(scene, p, vadMinProp=0.5):
-    return BatchDANSE(scene, p, vadMinProp=vadMinProp).run()
+    b = BatchDANSE(scene, p, vadMinProp=vadMinProp)
+    # d_core.danse_batch computes the centralised / local estimates first
+    # (d_core.py:282-283; no iterations for those)
+    if p.computeCentralised or p.computeLocal:
+        batch_family_estimates(b, centr=p.computeCentralised, local=p.computeLocal)
+    return b.run()
+
+
+def _centr_setup(b):
+    """Centralised frame VAD and STFT (init_from_wasn, d_classes.py:905-964):
+    the per-frame VAD averaged over nodes (active if any node is), the
+    node-stacked STFT yCentrBatch, and the batch SCMs over it."""
+    K = b.K
+    v = np.zeros(len(b.oVAD[0]))
+    for k in range(K):
+        v += b.oVAD[k]
+    v /= K
+    b.centrVAD = v.astype(bool)
+    b.yCentrBatch = np.concatenate(tuple(b.yinSTFT), axis=2)
+    b.Ryycentr, b.Rnncentr = update_covmats_batch(b.yCentrBatch, b.centrVAD)
+
+
+def batch_family_estimates(b, centr=True, local=True):
+    """``get_centralized_and_local_estimates`` (``d_batch.py:20-88``): one
+    filter per node from the batch SCMs of the centralised (all sensors,
+    centralised VAD, reference index sum(M[:k]) + ref) and local observation
+    vectors, stored in history slot i[k] + 1; estimates over all frames but
+    the last, ISTFT / sum(win), and the untrimmed MMSE costs."""
+    p = b.p
+    fn = update_w_gevd if p.performGEVD else update_w
+    rank = p.GEVDrank if p.performGEVD else 1
+    fi = dict(initType=p.filterInitType, fixedValue=p.filterInitFixedValue)
+    K, F, Mt = b.K, b.F, int(sum(b.M))
+    _centr_setup(b)
+    b.wCentr = [init_complex_filter((F, b.nIter + 1, Mt), int(np.sum(b.M[:k]) + p.referenceSensor), **fi)
+                for k in range(K)]
+    b.wLocal = [init_complex_filter((F, b.nIter + 1, b.M[k]), p.referenceSensor, **fi) for k in range(K)]
+    b.dCentr = np.zeros((b.T, K))
+    b.dLocal = np.zeros((b.T, K))
+    b.dHatCentr = np.zeros((F, b.nIter, K), dtype=complex)
+    b.dHatLocal = np.zeros((F, b.nIter, K), dtype=complex)
+
+    def istft(x, k):
+        y = get_istft(x, b.fs[k], b.win, 1 - b.Ns / b.N) / np.sum(b.win)
+        return np.pad(y, (0, b.T - len(y))) if len(y) < b.T else y
+    if centr:
+        for k in range(K):
+            i = b.i[k]
+            b.wCentr[k][:, i + 1, :] = fn(b.Ryycentr, b.Rnncentr,
+                                          refSensorIdx=int(np.sum(b.M[:k]) + p.referenceSensor), rank=rank)
+            b.dHatCentr[:, :, k] = np.einsum('ik,ijk->ij', b.wCentr[k][:, i + 1, :].conj(), b.yCentrBatch[:, :-1, :])
+            b.dCentr[:, k] = istft(b.dHatCentr[:, :, k], k)
+    if local:
+        for k in range(K):
+            i = b.i[k]
+            Ry, Rn = update_covmats_batch(b.yinSTFT[k], b.oVAD[k])
+            b.wLocal[k][:, i + 1, :] = fn(Ry, Rn, refSensorIdx=p.referenceSensor, rank=rank)
+            b.dHatLocal[:, :, k] = np.einsum('ik,ijk->ij', b.wLocal[k][:, i + 1, :].conj(), b.yinSTFT[k][:, :-1, :])
+            b.dLocal[:, k] = istft(b.dHatLocal[:, :, k], k)
+    b.mmseCostLocal = [np.mean(np.abs(b.clean[k][:, p.referenceSensor] - b.dLocal[:, k]) ** 2) for k in range(K)]
+    b.mmseCostCentr = [np.mean(np.abs(b.clean[k][:, p.referenceSensor] - b.dCentr[:, k]) ** 2) for k in range(K)]
+    return b
+
+
+def get_best_perf(scene, p, wCentr=None, vadMinProp=0.5):
+    """``d_core.get_best_perf`` (``d_core.py:602-627``) for fully connected
+    WASNs: batch centralised estimates without SROs
+    (``init_from_wasn_for_best_perf``, ``d_classes.py:378-470``: the noSRO
+    signals -- here the scene signals, which carry no resampling -- or the
+    noise-only / speech-only ones with pre-given filters;
+    ``get_centralized_estimates``, ``d_batch.py:90-125``).  ``wCentr``: the
+    filters of an earlier call (slot 1 is used).  Returns an object with
+    ``wCentr``, ``dCentr``, ``dHatCentr``, ``mmseCostCentr``."""
+    b = BatchDANSE(scene, p, vadMinProp=vadMinProp)
+    pg = p.preGivenFilters
+    if pg.active and pg.purpose == 'noise-only':
+        b.yin = [nd.cleannoise for nd in scene.wasn]
+    elif pg.active and pg.purpose == 'speech-only':
+        b.yin = [nd.cleanspeech for nd in scene.wasn]
+    b.yinSTFT = [get_stft(b.yin[k], b.fs[k], b.win, 1 - b.Ns / b.N) * np.sum(b.win) for k in range(b.K)]
+    fn = update_w_gevd if p.performGEVD else update_w
+    rank = p.GEVDrank if p.performGEVD else 1
+    fi = dict(initType=p.filterInitType, fixedValue=p.filterInitFixedValue)
+    K, F, Mt = b.K, b.F, int(sum(b.M))
+    _centr_setup(b)
+    b.wCentr = [init_complex_filter((F, b.nIter + 1, Mt), int(np.sum(b.M[:k]) + p.referenceSensor), **fi)
+                for k in range(K)]
+    b.dCentr = np.zeros((b.T, K))
+    b.dHatCentr = np.zeros((F, b.nIter, K), dtype=complex)
+    nseg = b.yCentrBatch.shape[1]
+    idx = np.arange(nseg) if nseg == b.nIter else np.arange(nseg - 1)
+    for k in range(K):
+        i = b.i[k]
+        if wCentr is None:
+            b.wCentr[k][:, i + 1, :] = fn(b.Ryycentr, b.Rnncentr,
+                                          refSensorIdx=int(np.sum(b.M[:k]) + p.referenceSensor), rank=rank)
+        else:
+            b.wCentr[k][:, i + 1, :] = wCentr[k][:, i + 1, :]
+        b.dHatCentr[:, :, k] = np.einsum('ik,ijk->ij', b.wCentr[k][:, i + 1, :].conj(), b.yCentrBatch[:, idx, :])
+        y = get_istft(b.dHatCentr[:, :, k], b.fs[k], b.win, 1 - b.Ns / b.N) / np.sum(b.win)
+        b.dCentr[:, k] = np.pad(y, (0, b.T - len(y))) if len(y) < b.T else y
+    b.mmseCostCentr = [np.mean(np.abs(b.clean[k][:, p.referenceSensor] - b.dCentr[:, k]) ** 2) for k in range(K)]
+    return b

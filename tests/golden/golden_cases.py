@@ -84,6 +84,27 @@ ONLINE_CASES = [
     dict(name='online_E_fs_L128_sro_comp', M=[2, 3], dur=2.5, seed=11, sros=[0, 200],
          danse=_d(BATTERY, nodeUpdating='asy', broadcastType='fewSamples', broadcastLength=128,
                   compensateSROs=True, includeFSDflags=True, estimateSROs='Oracle', computeLocal=True)),
+    # the E battery's settings (tests/battery20230919_perf_asfctofL.py:60-104):
+    # local, centralised and single-sensor-broadcast estimates under SRO clocks.
+    # Centralised buffers carry raw signals through the same buffers as z
+    # (fill_buffers_centr / process_incoming_signals_buffers_centr,
+    # d_classes.py:1226-1250,1809-1891); their compensation uses the flag index
+    # arithmetic of compensate_sros (d_classes.py:2000-2038, quirk Q14).  SSBC
+    # with compensation raises in the reference (d_classes.py:2042-2044).
+    dict(name='online_C_sro_centr_asy', M=[2, 3, 2], dur=3.0, seed=16, sros=[0, 100, 200],
+         danse=_d(BATTERY, nodeUpdating='asy', compensateSROs=True, includeFSDflags=True, estimateSROs='Oracle',
+                  computeLocal=True, computeCentralised=True)),
+    dict(name='online_C_sro_ssbc_nocomp_asy', M=[1, 2, 3], dur=3.0, seed=17, sros=[0, 150, 300],
+         danse=_d(BATTERY, nodeUpdating='asy', compensateSROs=False, estimateSROs='Oracle',
+                  computeLocal=True, computeCentralised=True, computeSingleSensorBroadcast=True)),
+    dict(name='online_E_fs_L64_sro_nocomp', M=[2, 3], dur=2.5, seed=18, sros=[0, 200],
+         danse=_d(BATTERY, nodeUpdating='asy', broadcastType='fewSamples', broadcastLength=64,
+                  compensateSROs=False, estimateSROs='Oracle', computeLocal=True, computeCentralised=True,
+                  computeSingleSensorBroadcast=True)),
+    dict(name='online_E_fs_L256_sro_comp_centr', M=[2, 3], dur=2.5, seed=19, sros=[0, 200],
+         danse=_d(BATTERY, nodeUpdating='asy', broadcastType='fewSamples', broadcastLength=256,
+                  compensateSROs=True, includeFSDflags=True, estimateSROs='Oracle', computeLocal=True,
+                  computeCentralised=True)),
     dict(name='online_E_fs_L1_seq', M=[2, 3, 1], dur=2.5, seed=12,
          danse=_d(BATTERY, nodeUpdating='seq', broadcastType='fewSamples', broadcastLength=1)),
 ]
@@ -97,6 +118,21 @@ BATCH_CASES = [
     # random filter init: slot 0 of the reference's (F, nIter + 1, D) seed-0 draw
     dict(name='batch_k3_random_init_asy', M=[2, 3, 2], dur=2.01, seed=8,
          danse=_d(BATTERY, simType='batch', nodeUpdating='asy', maxBatchUpdates=4, filterInitType='random')),
+    # centralised and local batch estimates (get_centralized_and_local_estimates,
+    # d_batch.py:20-88; d_core.py:282-283)
+    dict(name='batch_k3_local_centr_asy', M=[2, 3, 2], dur=2.01, seed=25,
+         danse=_d(BATTERY, simType='batch', nodeUpdating='asy', maxBatchUpdates=3, computeLocal=True,
+                  computeCentralised=True)),
+]
+
+# best-performance reference (d_core.get_best_perf, d_core.py:602-627: batch
+# centralised estimates without SROs), on the online parameters of a case; the
+# noise-only / speech-only replays with the recorded wCentr
+# (generate_signals_for_snr_computation, d_core.py:550-599)
+BESTPERF_CASES = [
+    dict(name='bestperf_k3', M=[2, 3, 2], dur=2.01, seed=26, danse=_d(BATTERY, nodeUpdating='asy')),
+    dict(name='bestperf_k4_mwf', M=[1, 2, 2, 3], dur=2.01, seed=27,
+         danse=_d(SANDBOX, nodeUpdating='seq', performGEVD=False)),
 ]
 
 SRO_EVENT_CASES = [

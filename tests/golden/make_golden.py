@@ -22,7 +22,7 @@ sys.path.insert(0, str(HERE))
 
 import _refharness as H  # noqa: E402
 from danse_amd.scene import make_scene, scene_digest  # noqa: E402
-from golden_cases import ONLINE_CASES, BATCH_CASES, SRO_EVENT_CASES, KAT_CASES, kat_inputs  # noqa: E402
+from golden_cases import ONLINE_CASES, BATCH_CASES, SRO_EVENT_CASES, KAT_CASES, kat_inputs, BESTPERF_CASES  # noqa: E402
 from golden_cases import DXCP_CASES, dxcp_inputs, TZ_CASES, tz_inputs  # noqa: E402
 from golden_cases import METRIC_CASES, metric_inputs, GETMETRICS_CASE, get_metrics_inputs  # noqa: E402
 from golden_cases import FIELD_CASES, FIELD_STFT_BIN_STEP  # noqa: E402
@@ -121,6 +121,34 @@ def _run_batch(ns, case):
            'mmseCost': np.array(out_.mmseCost, dtype=float)}
     for k in range(len(case['M'])):
         out[f'w_{k}'] = out_.filters[k][:, :case['danse']['maxBatchUpdates'] + 1, :]
+    if case['danse'].get('computeCentralised', False):
+        out['dCentr'] = out_.TDdesiredSignals_est_c
+        out['mmseCostCentr'] = np.array(out_.mmseCostCentr, dtype=float)
+        for k in range(len(case['M'])):
+            out[f'wCentr_{k}'] = out_.filtersCentr[k][:, :2, :]
+    if case['danse'].get('computeLocal', False):
+        out['dLocal'] = out_.TDdesiredSignals_est_l
+        out['mmseCostLocal'] = np.array(out_.mmseCostLocal, dtype=float)
+        for k in range(len(case['M'])):
+            out[f'wLocal_{k}'] = out_.filtersLocal[k][:, :2, :]
+    return out
+
+
+def _run_best_perf(ns, case):
+    import copy
+    sc = make_scene(case['M'], sigDur=case['dur'], seed=case['seed'])
+    p = H.make_params(ns, case['M'], **case['danse'])
+    w = H.to_ref_wasn(ns, sc)
+    p, w = H.prep(ns, p, w)
+    bp = ns.core.get_best_perf(w, p.danseParams)
+    out = {'digest': scene_digest(sc), 'dCentr': bp.dCentr, 'mmseCostCentr': np.array(bp.mmseCostCentr, dtype=float)}
+    for k in range(len(case['M'])):
+        out[f'wCentr_{k}'] = bp.wCentr[k][:, :2, :]
+    pU = copy.deepcopy(p.danseParams)
+    for purpose in ('noise-only', 'speech-only'):
+        pU.preGivenFilters = ns.base.PreComputedFilters(active=True, purpose=purpose)
+        o = ns.core.get_best_perf(w, pU, wCentr=bp.wCentr)
+        out[f'dCentr_{purpose[0]}'] = o.dCentr
     return out
 
 
@@ -195,6 +223,7 @@ def main():
     only = sys.argv[1:]
     jobs = [('online', c, _run_online) for c in ONLINE_CASES] + \
            [('batch', c, _run_batch) for c in BATCH_CASES] + \
+           [('bestperf', c, _run_best_perf) for c in BESTPERF_CASES] + \
            [('events', c, _run_sro_events) for c in SRO_EVENT_CASES] + \
            [('kat', c, _run_kat) for c in KAT_CASES] + \
            [('dxcp', c, _run_dxcp) for c in DXCP_CASES] + \

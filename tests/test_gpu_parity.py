@@ -15,7 +15,7 @@ import ctypes
 import numpy as np
 import pytest
 
-from golden_cases import ONLINE_CASES, BATCH_CASES, KAT_CASES, kat_inputs
+from golden_cases import ONLINE_CASES, BATCH_CASES, KAT_CASES, kat_inputs, BESTPERF_CASES
 from _util import make_case_params, make_case_scene, rel_err
 
 pytestmark = pytest.mark.gpu
@@ -146,6 +146,17 @@ def test_online_engine_vs_oracle(case, golden_dir):
             e = rel_err(getattr(dv, nm), getattr(ov, nm))
             print('  ', nm, e)
             assert e <= 1e-4, (nm, e)
+    # the other families' filter histories (local / centralised / SSBC;
+    # under SRO clocks the centralised vector's raw frames and compensation)
+    for wn, fl in (('wLocal', 'computeLocal'), ('wCentr', 'computeCentralised'),
+                   ('wSSBC', 'computeSingleSensorBroadcast')):
+        if case['danse'].get(fl, False):
+            R = dv.nRounds
+            errs = np.concatenate([_bin_rel(getattr(dv, wn)[k][:, 1:R + 1, :], getattr(ov, wn)[k][:, 1:R + 1, :]).ravel()
+                                   for k in range(len(case['M']))])
+            sw = _stats(errs)
+            print('  ', wn, sw)
+            assert sw['p99'] <= 1e-4, (wn, sw)
     # golden (reference itself): same d
     g = np.load(golden_dir / f"{case['name']}.npz")
     dg = rel_err(dv.d, g['d'])
@@ -211,6 +222,51 @@ def test_batch_engine_vs_oracle(case, golden_dir):
     print(case['name'], 'w', st, 'd', de, 'cost', ce, 'd vs golden', dg)
     assert st['median'] <= 1e-5 and st['p99'] <= 1e-4, st
     assert de <= 1e-4 and ce <= 1e-4 and dg <= 1e-4
+    # centralised / local batch estimates (obs = 2 / 1 engines)
+    for fam in ('Centr', 'Local'):
+        if f'd{fam}' not in g:
+            continue
+        sf = _stats(np.concatenate([_bin_rel(getattr(out, f'w{fam}')[k][:, 1, :], getattr(ov, f'w{fam}')[k][:, 1, :]).ravel()
+                                    for k in range(len(case['M']))]))
+        dfe = rel_err(getattr(out, f'd{fam}'), getattr(ov, f'd{fam}'))
+        dfg = rel_err(getattr(out, f'd{fam}'), g[f'd{fam}'])
+        cr = np.array(getattr(ov, f'mmseCost{fam}'))
+        cfe = float(np.max(np.abs(np.array(getattr(out, f'mmseCost{fam}')) - cr) / np.abs(cr)))
+        print('  ', fam, 'w', sf, 'd', dfe, 'd vs golden', dfg, 'cost', cfe)
+        assert sf['median'] <= 1e-5 and sf['p99'] <= 1e-4, sf
+        assert dfe <= 1e-4 and dfg <= 1e-4 and cfe <= 1e-4
+
+
+@pytest.mark.parametrize('case', BESTPERF_CASES, ids=lambda c: c['name'])
+def test_best_perf_vs_oracle(case, golden_dir):
+    """get_best_perf (d_core.py:602-627) on the device batch engine
+    (obs = centralised): filters, estimate and MMSE cost against the float64
+    oracle, and the noise-only / speech-only replays with the recorded
+    filters against the reference's fixture."""
+    import copy
+    from danse_amd import core
+    from danse_amd.params import PreComputedFilters
+    from oracle import danse_ref_cpu as O
+    sc = make_case_scene(case)
+    dp, wp = make_case_params(case)
+    sc.get_vad_per_frame(dp.DFTsize, dp.Ns, wp.vadMinProportionActive)
+    bp = core.get_best_perf(sc, dp)
+    ob = O.get_best_perf(sc, dp, vadMinProp=wp.vadMinProportionActive)
+    g = np.load(golden_dir / f"{case['name']}.npz")
+    st = _stats(np.concatenate([_bin_rel(bp.wCentr[k][:, 1, :], ob.wCentr[k][:, 1, :]).ravel()
+                                for k in range(len(case['M']))]))
+    de, dg = rel_err(bp.dCentr, ob.dCentr), rel_err(bp.dCentr, g['dCentr'])
+    ce = float(np.max(np.abs(np.array(bp.mmseCostCentr) - g['mmseCostCentr']) / g['mmseCostCentr']))
+    print(case['name'], 'w', st, 'd', de, 'd vs golden', dg, 'cost', ce)
+    assert st['median'] <= 1e-5 and st['p99'] <= 1e-4, st
+    assert de <= 1e-4 and dg <= 1e-4 and ce <= 1e-4
+    pU = copy.deepcopy(dp)
+    for purpose in ('noise-only', 'speech-only'):
+        pU.preGivenFilters = PreComputedFilters(active=True, purpose=purpose)
+        o = core.get_best_perf(sc, pU, wCentr=bp.wCentr)
+        e = rel_err(o.dCentr, g[f'dCentr_{purpose[0]}'])
+        print('  ', purpose, e)
+        assert e <= 1e-4, (purpose, e)
 
 
 def test_batch_covmats_op():

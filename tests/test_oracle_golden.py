@@ -4,6 +4,7 @@ import numpy as np
 import pytest
 
 from golden_cases import ONLINE_CASES, BATCH_CASES, SRO_EVENT_CASES, KAT_CASES, DXCP_CASES, TZ_CASES, kat_inputs
+from golden_cases import BESTPERF_CASES
 from danse_amd.scene import scene_digest
 from danse_amd.scheduler import initialize_events
 from oracle import danse_ref_cpu as O
@@ -59,6 +60,34 @@ def test_batch_oracle_matches_reference(case, golden_dir):
     for k in range(len(case['M'])):
         nb = case['danse']['maxBatchUpdates'] + 1
         assert rel_err(bv.wTilde[k][:, :nb, :], g[f'w_{k}']) < TOL
+    for fam in ('Centr', 'Local'):
+        if f'd{fam}' in g:
+            assert rel_err(getattr(bv, f'd{fam}'), g[f'd{fam}']) < TOL
+            assert rel_err(np.array(getattr(bv, f'mmseCost{fam}')), g[f'mmseCost{fam}']) < TOL
+            for k in range(len(case['M'])):
+                assert rel_err(getattr(bv, f'w{fam}')[k][:, :2, :], g[f'w{fam}_{k}']) < TOL
+
+
+@pytest.mark.parametrize('case', BESTPERF_CASES, ids=[c['name'] for c in BESTPERF_CASES])
+def test_best_perf_oracle_matches_reference(case, golden_dir):
+    """get_best_perf (d_core.py:602-627) and its noise-only / speech-only
+    replays with the recorded centralised filters."""
+    import copy
+    from danse_amd.params import PreComputedFilters
+    g = _load(golden_dir, case['name'])
+    sc = make_case_scene(case)
+    assert scene_digest(sc) == str(g['digest'])
+    dp, wp = make_case_params(case)
+    bp = O.get_best_perf(sc, dp, vadMinProp=wp.vadMinProportionActive)
+    assert rel_err(bp.dCentr, g['dCentr']) < TOL
+    assert rel_err(np.array(bp.mmseCostCentr), g['mmseCostCentr']) < TOL
+    for k in range(len(case['M'])):
+        assert rel_err(bp.wCentr[k][:, :2, :], g[f'wCentr_{k}']) < TOL
+    pU = copy.deepcopy(dp)
+    for purpose in ('noise-only', 'speech-only'):
+        pU.preGivenFilters = PreComputedFilters(active=True, purpose=purpose)
+        o = O.get_best_perf(sc, pU, wCentr=bp.wCentr, vadMinProp=wp.vadMinProportionActive)
+        assert rel_err(o.dCentr, g[f'dCentr_{purpose[0]}']) < TOL
 
 
 @pytest.mark.parametrize('case', SRO_EVENT_CASES, ids=[c['name'] for c in SRO_EVENT_CASES])
