@@ -90,11 +90,32 @@ WORKLOADS = {
                                     includeFSDflags=True),
                          desc='E: GEVD-DANSE r1, K=2, MK=[2,3], fewSamples L=64, SROs [0, 200] ppm + compensation, '
                               'asy, 10 s'),
+    # the battery itself (tests/battery20230919_perf_asfctofL.py:60-104): SROs [0, 200] ppm, Oracle
+    # estimates, sandbox_config.yaml families on (local, centralised, SSBC: SSBC with compensation
+    # raises in the reference, d_classes.py:2042-2044, so the comp variants run local + centralised);
+    # --L sets broadcastLength (the device fewSamples schedule covers L = 32..256 under these SROs)
+    'E_noComp': dict(M=[2, 3], dur=10.0, nodeUpdating='asy', sros=[0.0, 200.0],
+                     extra=dict(broadcastType='fewSamples', broadcastLength=64, compensateSROs=False,
+                                computeLocal=True, computeCentralised=True, computeSingleSensorBroadcast=True),
+                     desc='E battery noComp: K=2, MK=[2,3], fewSamples L, SROs [0, 200] ppm, no compensation, '
+                          'DANSE + local + centralised + SSBC, asy, 10 s'),
+    'E_compNoFlags': dict(M=[2, 3], dur=10.0, nodeUpdating='asy', sros=[0.0, 200.0],
+                          extra=dict(broadcastType='fewSamples', broadcastLength=64, compensateSROs=True,
+                                     includeFSDflags=False, computeLocal=True, computeCentralised=True),
+                          desc='E battery compNoFlags: K=2, MK=[2,3], fewSamples L, SROs [0, 200] ppm, Oracle '
+                               'compensation without flags, DANSE + local + centralised, asy, 10 s'),
+    'E_comp': dict(M=[2, 3], dur=10.0, nodeUpdating='asy', sros=[0.0, 200.0],
+                   extra=dict(broadcastType='fewSamples', broadcastLength=64, compensateSROs=True,
+                              includeFSDflags=True, computeLocal=True, computeCentralised=True),
+                   desc='E battery comp: K=2, MK=[2,3], fewSamples L, SROs [0, 200] ppm, Oracle compensation with '
+                        'flags, DANSE + local + centralised, asy, 10 s'),
 }
 
 
 for _n, _w in WORKLOADS.items():
     _w['name'] = _n
+
+_CHILD_ARGS = []   # workload overrides forwarded to the CPU-baseline and PMC child processes
 
 
 def _wl_params(wl):
@@ -156,6 +177,7 @@ def main():
     ap.add_argument('--batch-shard', default='replicas', choices=['replicas', 'nodes'],
                     help='config D on N>1 GPUs: independent WASNs per GPU (weak scaling) or every GPU owning a '
                          'node block of the same WASNs, external filters all-gathered per iteration (strong)')
+    ap.add_argument('--L', type=int, default=None, help='broadcastLength override (fewSamples workloads)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
     ap.add_argument('--no-graph', action='store_true')
@@ -166,6 +188,13 @@ def main():
     ap.add_argument('--rounds', type=int, default=None, help=argparse.SUPPRESS)
     ap.add_argument('--pmc-child', action='store_true', help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.L is not None:
+        w = WORKLOADS[args.workload]
+        if w.get('extra', {}).get('broadcastType') != 'fewSamples':
+            raise SystemExit('--L applies to the fewSamples workloads')
+        w['extra'] = dict(w['extra'], broadcastLength=int(args.L))
+        w['desc'] = w['desc'].replace('fewSamples L=64', f'fewSamples L={args.L}').replace('fewSamples L,', f'fewSamples L={args.L},')
+    _CHILD_ARGS.extend(['--L', str(args.L)] if args.L is not None else [])
     if args.cpu_only:
         wl = WORKLOADS[args.workload]
         if wl.get('batch'):
@@ -255,7 +284,8 @@ def cpu_child(workload, seconds, rounds):
     env = dict(os.environ, HIP_VISIBLE_DEVICES='', CUDA_VISIBLE_DEVICES='', ROCR_VISIBLE_DEVICES='')
     for k in ('RANK', 'WORLD_SIZE', 'LOCAL_RANK'):
         env.pop(k, None)
-    cmd = [sys.executable, str(ROOT / 'bench.py'), '--cpu-only', '--workload', workload, '--cpu-seconds', str(seconds)]
+    cmd = [sys.executable, str(ROOT / 'bench.py'), '--cpu-only', '--workload', workload, '--cpu-seconds', str(seconds),
+           *_CHILD_ARGS]
     if rounds is not None:
         cmd += ['--rounds', str(rounds)]
     cp = subprocess.run(cmd,
@@ -565,7 +595,7 @@ def pmc_traffic(wl, S, kernel_substr):
     for counter in ('FETCH_SIZE', 'WRITE_SIZE'):
         d = os.path.join(tmp, counter)
         cmd = [exe, '--pmc', counter, '--kernel-trace', '-d', d, '-o', 'pmc', '--output-format', 'csv', '--',
-               sys.executable, str(ROOT / 'bench.py'), '--pmc-child', '--workload', wl['name'],
+               sys.executable, str(ROOT / 'bench.py'), '--pmc-child', '--workload', wl['name'], *_CHILD_ARGS,
                '--scenes', str(S)]
         try:
             subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240, check=True)

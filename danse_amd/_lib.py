@@ -120,6 +120,11 @@ SIGNATURES = {
     'danse_dxcp_destroy': (None, [ctypes.c_void_p]),
     'danse_dxcp_last_error': (ctypes.c_char_p, [ctypes.c_void_p]),
     'danse_dxcp_process': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    'danse_dxcp_process_tdoa': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_void_p]),
+    'danse_cl_dxcp_create': (_c_i32, [_c_i32, _c_i32, _c_i32, ctypes.POINTER(ctypes.c_void_p)]),
+    'danse_cl_dxcp_process': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_void_p, ctypes.c_void_p]),
     'danse_tz_create': (_c_i32, [_c_i32, ctypes.c_void_p, ctypes.c_void_p, _c_i32, _c_i32,
                                  ctypes.POINTER(ctypes.c_void_p)]),
     'danse_tz_destroy': (None, [ctypes.c_void_p]),
@@ -131,6 +136,9 @@ SIGNATURES = {
     'danse_fwsnrseg': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, _c_i32, ctypes.c_double,
                                 ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_void_p, ctypes.c_void_p,
                                 ctypes.c_void_p]),
+    'danse_stoi_last_error': (ctypes.c_char_p, []),
+    'danse_stoi': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, _c_i32, ctypes.c_double, _c_i32,
+                            ctypes.c_void_p, ctypes.c_void_p]),
     'danse_tz_last_error': (ctypes.c_char_p, [ctypes.c_void_p]),
     'danse_tz_ir': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p, _c_i32, _c_i32, ctypes.c_void_p, ctypes.c_void_p]),
     'danse_tz_compress': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, _c_i32, _c_i32, _c_i32,

@@ -3,7 +3,7 @@
 ``hipcc -c -fPIC`` of ``csrc/danse_engine.hip`` (online engine, C-ABI, bcast /
 operator kernels), ``csrc/batch.hip`` (batch-mode engine), ``csrc/dxcp.hip`` (DXCP-PhaT SRO
 estimator), ``csrc/tz.hip`` (T(z) few-samples compression), ``csrc/metrics.hip``
-(SNR / fwSNRseg) and of
+(SNR / fwSNRseg), ``csrc/stoi.hip`` ((e)STOI) and of
 ``csrc/update_class.hip`` once per filter-size class
 (``-DDANSE_DMAX=N``, N = 1..16 and 24..64 in steps of 8, see
 ``csrc/classes.hpp``), in parallel, then one
@@ -33,7 +33,7 @@ def _units():
     """(object name, source, extra flags) of every translation unit."""
     u = [('danse_engine.o', CSRC / 'danse_engine.hip', []), ('batch.o', CSRC / 'batch.hip', []),
          ('dxcp.o', CSRC / 'dxcp.hip', []), ('tz.o', CSRC / 'tz.hip', []),
-         ('metrics.o', CSRC / 'metrics.hip', [])]
+         ('metrics.o', CSRC / 'metrics.hip', []), ('stoi.o', CSRC / 'stoi.hip', [])]
     for n in CLASSES:
         # lane-per-bin classes: no SLP packing of the float32 complex math
         # (the packed pairs need swapped operand copies; with them the eigen

@@ -121,7 +121,7 @@ DANSE_DEV int block_argmax(float v, int idx, float* rv, int* ri) {
 }
 
 __global__ void __launch_bounds__(kThreads) dxcp_kernel(const float* __restrict__ x, DxcpState st, DxcpConst c,
-                                                        double* __restrict__ out) {
+                                                        const double* __restrict__ tdoa, double* __restrict__ out) {
   __shared__ cf buf[kN];
   __shared__ cf scratch[8][wfft::kLdsElems];
   __shared__ float up[kNUp];
@@ -270,6 +270,8 @@ __global__ void __launch_bounds__(kThreads) dxcp_kernel(const float* __restrict_
       } else {
         const double s0 = rv[0], s1 = rv[1], s2 = rv[2];
         sto = (double)(im1 - kUps) + (s2 - s0) / 2.0 / (2.0 * s1 - s2 - s0);
+        // TDOA correction, interior maxima only (sro_estimation.py:338-339)
+        if (tdoa) sto += tdoa[p] * 16000.0;
       }
     }
   }
@@ -293,6 +295,140 @@ __global__ void __launch_bounds__(kThreads) dxcp_kernel(const float* __restrict_
   }
 }
 
+// ---- closed loop (CL_DXCPPhaT, sro_estimation.py:12-72) -------------------
+// Per pair: OnlineResampler (online_resampler.py:4-77) of z_i with the
+// controller's current estimate, DelayBuffer (delay_buffer.py:8-26) of z_j,
+// DXCP-PhaT on the synchronised pair, IMC controller (PIT1, Tf = 8).
+struct ClPair {
+  double shift;          // Resampler.shift
+  double dS[3], S[3];    // dSRO_est, SRO_est (newest first)
+  double sroCurr;        // SRO_est_curr
+  int ell;               // CL_DXCPPhaT.ell
+  int zjPtr;             // DelayBuffer.pointer
+};
+
+struct ClState {
+  float* inBuf;          // [P][4 * 2048]  prev - current - next - next2
+  float* outBuf;         // [P][3 * 2048]
+  float* zj;             // [P][3][2048]   delay ring (2 + 1 frames)
+  float* x12;            // [P][2][2048]   the DXCP input of this frame
+  ClPair* cp;            // [P]
+};
+
+constexpr int kB = kFrame;   // blockSize
+
+// hann(4096, sym=False)
+DANSE_DEV float hann4096(int n) { return (float)(0.5 - 0.5 * cos(2.0 * M_PI * (double)n / (double)(2 * kB))); }
+
+__global__ void __launch_bounds__(kThreads) cl_resample_kernel(const float* __restrict__ x, ClState st, DxcpConst c,
+                                                               float* __restrict__ ziOut) {
+  __shared__ cf buf[kN];
+  __shared__ cf scratch[8][wfft::kLdsElems];
+  __shared__ int sel0;
+  __shared__ double rest;
+  const int p = blockIdx.x, tid = threadIdx.x;
+  float* in = st.inBuf + (size_t)p * 4 * kB;
+  float* ob = st.outBuf + (size_t)p * 3 * kB;
+  const float* zi = x + ((size_t)p * 2 + 1) * kB;
+  const float* zjIn = x + ((size_t)p * 2 + 0) * kB;
+  // the input buffer shifted by one block, the new block appended
+  auto nin = [&](int n) { return (n < 3 * kB) ? in[n + kB] : zi[n - 3 * kB]; };
+  if (tid == 0) {
+    ClPair cp = st.cp[p];
+    const double sro = -cp.sroCurr;
+    cp.shift += sro * 1e-6 * kB;
+    const double acc = cp.shift;
+    const double ish = rint(acc);   // np.round: half to even
+    rest = ish - acc;
+    long long s0 = (long long)kB + (long long)ish, s1 = (long long)3 * kB + (long long)ish;
+    if (s0 < 0) {
+      cp.shift -= sro * 1e-6 * kB;
+      s1 -= s0;
+      s0 = 0;
+    } else if (s1 >= 4 * kB) {
+      cp.shift -= sro * 1e-6 * kB;
+      s0 -= s1 - 4 * kB;
+      s1 = 4 * kB;
+    }
+    sel0 = (int)s0;
+    st.cp[p] = cp;
+  }
+  __syncthreads();
+  for (int n = tid; n < kN; n += kThreads) buf[n] = cf{n < 2 * kB ? hann4096(n) * nin(sel0 + n) : 0.0f, 0.0f};
+  {
+    // shift the stored buffer in place: every read before any write
+    float v[4 * kB / kThreads];
+#pragma unroll
+    for (int i = 0; i < 4 * kB / kThreads; ++i) v[i] = nin(tid + i * kThreads);
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4 * kB / kThreads; ++i) in[tid + i * kThreads] = v[i];
+  }
+  __syncthreads();
+  fft8192(buf, scratch, c);
+  // linear phase of the rest shift on the fftshift'ed bin index, then
+  // ifft = conj(fft(conj(.))) / N
+  const double rs = rest;
+  for (int m = tid; m < kN; m += kThreads) {
+    const int k = m < kN / 2 ? m : m - kN;
+    double t = (double)k * rs / (double)kN;
+    t -= rint(t);
+    float sn, cs;
+    sincospif(-2.0f * (float)t, &sn, &cs);
+    buf[m] = conjg(buf[m] * cf{cs, sn});
+  }
+  __syncthreads();
+  fft8192(buf, scratch, c);
+  // overlap-add into blocks 2-3 of the output buffer, shift it by one block
+  float* zo = st.x12 + ((size_t)p * 2 + 1) * kB;
+  for (int n = tid; n < 2 * kB; n += kThreads) {
+    const float y = buf[n].re * (1.0f / kN);   // real(conj(.)) / N
+    const float v = ob[kB + n] + y;
+    if (n < kB) {
+      zo[n] = v;
+      if (ziOut) ziOut[(size_t)p * kB + n] = v;
+    }
+    __syncthreads();   // every read of ob before the shifted writes
+    ob[n] = v;
+  }
+  for (int n = tid; n < kB; n += kThreads) ob[2 * kB + n] = 0.0f;
+  // z_j through the delay ring: write at the pointer, read the oldest
+  const int ptr = st.cp[p].zjPtr;
+  float* ring = st.zj + (size_t)p * 3 * kB;
+  float* zjo = st.x12 + ((size_t)p * 2 + 0) * kB;
+  for (int n = tid; n < kB; n += kThreads) {
+    ring[(size_t)ptr * kB + n] = zjIn[n];
+    zjo[n] = ring[(size_t)((ptr + 1) % 3) * kB + n];
+  }
+  __syncthreads();
+  if (tid == 0) st.cp[p].zjPtr = (ptr + 1) % 3;
+}
+
+// IMC controller update after DXCP-PhaT (sro_estimation.py:56-70)
+__global__ void cl_control_kernel(ClState st, int P, int startDelay, const int* __restrict__ acs,
+                                  const double* __restrict__ dx, double* __restrict__ out) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P) return;
+  const double kNom[3] = {0.0, 0.0251941968627353, -0.0249422548941180};
+  const double kDen[3] = {1.0, -1.96825464010938, 0.968254640109407};
+  ClPair cp = st.cp[p];
+  const double raw = dx[2 * p];
+  double d = (!acs || acs[p] == 1) ? raw : 0.0;
+  if (cp.ell <= startDelay) d = 0.0;
+  cp.dS[2] = cp.dS[1];
+  cp.dS[1] = cp.dS[0];
+  cp.dS[0] = d;
+  cp.S[2] = cp.S[1];
+  cp.S[1] = cp.S[0];
+  cp.S[0] = (kNom[0] * cp.dS[0] + kNom[1] * cp.dS[1] + kNom[2] * cp.dS[2]) - (kDen[1] * cp.S[1] + kDen[2] * cp.S[2]);
+  cp.sroCurr = cp.S[0] + 0.0;   // + SRO_est_op
+  cp.ell += 1;
+  st.cp[p] = cp;
+  out[3 * p] = raw;
+  out[3 * p + 1] = cp.sroCurr;
+  out[3 * p + 2] = cp.shift;
+}
+
 }  // namespace
 
 struct danse_dxcp {
@@ -303,6 +439,10 @@ struct danse_dxcp {
   DxcpConst c{};
   float *dWin = nullptr, *dWres = nullptr;
   cf *dTw = nullptr, *dWtw = nullptr, *dT161 = nullptr, *dT644 = nullptr;
+  // closed loop (danse_cl_dxcp_*): resampler / delay / controller state
+  ClState cl{};
+  int startDelay = 0;
+  double* dxOut = nullptr;   // [P][2] DXCP output of the current frame
 };
 
 static thread_local std::string g_derr;
@@ -411,7 +551,8 @@ void danse_dxcp_destroy(danse_dxcp* eng) {
   if (!eng) return;
   (void)hipSetDevice(eng->dev);
   void* ptrs[] = {eng->dWin, eng->dWres, eng->dTw, eng->dWtw, eng->dT161, eng->dT644, eng->st.ring, eng->st.gavg,
-                  eng->st.cont, eng->st.g2, eng->st.c1, eng->st.ps};
+                  eng->st.cont, eng->st.g2, eng->st.c1, eng->st.ps, eng->cl.inBuf, eng->cl.outBuf, eng->cl.zj,
+                  eng->cl.x12, eng->cl.cp, eng->dxOut};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   delete eng;
@@ -423,7 +564,56 @@ int danse_dxcp_process(danse_dxcp* eng, const float* x, double* out, void* strea
     return -1;
   }
   DCHK(hipSetDevice(eng->dev));
-  hipLaunchKernelGGL(dxcp_kernel, dim3(eng->P), dim3(kThreads), 0, (hipStream_t)stream, x, eng->st, eng->c, out);
+  hipLaunchKernelGGL(dxcp_kernel, dim3(eng->P), dim3(kThreads), 0, (hipStream_t)stream, x, eng->st, eng->c,
+                     (const double*)nullptr, out);
+  DCHK(hipGetLastError());
+  return 0;
+}
+
+int danse_dxcp_process_tdoa(danse_dxcp* eng, const float* x, const double* tdoa, double* out, void* stream) {
+  if (!eng || !x || !out) {
+    g_derr = "null argument";
+    return -1;
+  }
+  DCHK(hipSetDevice(eng->dev));
+  hipLaunchKernelGGL(dxcp_kernel, dim3(eng->P), dim3(kThreads), 0, (hipStream_t)stream, x, eng->st, eng->c, tdoa, out);
+  DCHK(hipGetLastError());
+  return 0;
+}
+
+int danse_cl_dxcp_create(int32_t P, int32_t startDelay, int device, danse_dxcp** out) {
+  danse_dxcp* eng = nullptr;
+  const int rc = danse_dxcp_create(P, device, &eng);
+  if (rc) return rc;
+  eng->startDelay = startDelay;
+  ClState& c = eng->cl;
+  DCHK(hipMalloc((void**)&c.inBuf, (size_t)P * 4 * kB * sizeof(float)));
+  DCHK(hipMalloc((void**)&c.outBuf, (size_t)P * 3 * kB * sizeof(float)));
+  DCHK(hipMalloc((void**)&c.zj, (size_t)P * 3 * kB * sizeof(float)));
+  DCHK(hipMalloc((void**)&c.x12, (size_t)P * 2 * kB * sizeof(float)));
+  DCHK(hipMalloc((void**)&c.cp, (size_t)P * sizeof(ClPair)));
+  DCHK(hipMalloc((void**)&eng->dxOut, (size_t)P * 2 * sizeof(double)));
+  DCHK(hipMemset(c.inBuf, 0, (size_t)P * 4 * kB * sizeof(float)));
+  DCHK(hipMemset(c.outBuf, 0, (size_t)P * 3 * kB * sizeof(float)));
+  DCHK(hipMemset(c.zj, 0, (size_t)P * 3 * kB * sizeof(float)));
+  DCHK(hipMemset(c.x12, 0, (size_t)P * 2 * kB * sizeof(float)));
+  DCHK(hipMemset(c.cp, 0, (size_t)P * sizeof(ClPair)));
+  *out = eng;
+  return 0;
+}
+
+int danse_cl_dxcp_process(danse_dxcp* eng, const float* x, const int32_t* acs, double* out, float* zi, void* stream) {
+  if (!eng || !x || !out || !eng->cl.cp) {
+    g_derr = "null argument or not a closed-loop engine";
+    return -1;
+  }
+  DCHK(hipSetDevice(eng->dev));
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(cl_resample_kernel, dim3(eng->P), dim3(kThreads), 0, st, x, eng->cl, eng->c, zi);
+  hipLaunchKernelGGL(dxcp_kernel, dim3(eng->P), dim3(kThreads), 0, st, (const float*)eng->cl.x12, eng->st, eng->c,
+                     (const double*)nullptr, eng->dxOut);
+  hipLaunchKernelGGL(cl_control_kernel, dim3((eng->P + 63) / 64), dim3(64), 0, st, eng->cl, eng->P, eng->startDelay, acs,
+                     (const double*)eng->dxOut, out);
   DCHK(hipGetLastError());
   return 0;
 }

@@ -310,9 +310,12 @@ class DanseEngine:
                             off = o
                         elif o != off:
                             raise NotImplementedError(f'node {q} raw broadcast stream is not contiguous')
-                if off not in (None, 0):
+                # off < 0: the first chunk starts with the zero padding of a
+                # frame that ends before sample N (raw index < 0 reads zero,
+                # as in the stream); off > 0 would leave unsent samples
+                if off is not None and off > 0:
                     raise NotImplementedError(f'node {q} raw broadcast stream does not start at sample 0')
-                cEnd[:, q] = tab[:R, q, FS_ZEND]
+                cEnd[:, q] = np.maximum(tab[:R, q, FS_ZEND] + (off or 0), 0)
         else:
             bc = self.rt.bcEnd[:R]
             if R > 1 and not np.all(np.diff(bc, axis=0) == Ns):

@@ -12,6 +12,11 @@
 * ``fwsnrseg_batch(clean, enhanced, fs, ...)`` -- device tensors [B][T] in,
   per-frame [B][nFrames] and mean [B] device tensors out (the E battery's
   ΔfwSNRseg per scene without leaving the GPU).
+* ``stoi(x, y, fs_sig, extended=False)`` / ``stoi_batch`` -- ``stoi``
+  (``danse_toolbox/mypystoi/stoi.py:18-119``); at 10 kHz also
+  ``stoi_any_fs`` (``stoi.py:122-239``), which resamples other rates with
+  resampy (absent offline) where this uses the Octave resampler of
+  ``utils.resample_oct``.
 No CPU fallback: the library must be present.
 """
 from __future__ import annotations
@@ -36,6 +41,34 @@ def _dev(x, torch, device):
 
 def _stream(torch, device):
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def stoi_batch(x, y, fs_sig, extended=False, device=0):
+    """(e)STOI of B pairs: x (clean), y (processed) [B][T] device tensors or
+    host arrays; returns a [B] float64 device tensor (csrc/stoi.hip)."""
+    import torch
+    lib = L.load_library()
+    dev = f'cuda:{device}'
+    a = _dev(x, torch, dev)
+    b = _dev(y, torch, dev)
+    if a.ndim == 1:
+        a, b = a[None], b[None]
+    if a.shape != b.shape:
+        raise Exception('x and y should have the same length,' + 'found {} and {}'.format(a.shape, b.shape))
+    B, T = a.shape
+    out = torch.empty((B,), dtype=torch.float64, device=dev)
+    rc = lib.danse_stoi(ctypes.c_void_p(a.data_ptr()), ctypes.c_void_p(b.data_ptr()), int(T), int(B), float(fs_sig),
+                        int(bool(extended)), ctypes.c_void_p(out.data_ptr()), _stream(torch, dev))
+    if rc != 0:
+        raise L.DanseError((lib.danse_stoi_last_error() or b'').decode() or f'error {rc}')
+    return out
+
+
+def stoi(x, y, fs_sig, extended=False, device=0):
+    """``stoi(x, y, fs_sig, extended)`` of one pair (host arrays), a float."""
+    x = np.squeeze(np.asarray(x, dtype=np.float64))
+    y = np.squeeze(np.asarray(y, dtype=np.float64))
+    return float(stoi_batch(x, y, fs_sig, extended, device).cpu().numpy()[0])
 
 
 def fwsnrseg_frames(T, fs, frameLen=0.03, overlap=0.75):
@@ -133,12 +166,16 @@ def get_metrics(clean, noiseOnly, noisy, filtSpeech, filtNoise, filtSpeech_c=Non
     ``bypassVADuse = True`` (hard-coded, line 205) and ``get_fwsnrseg(clean,
     x, fs, fLen, gamma)`` where the positional ``gamma`` lands in the
     ``overlap`` parameter (lines 236-242: overlap = gamma, gamma = 0.2).
-    'stoi' / 'pesq' / 'sisnr', dynamic metrics and bestPerfData raise."""
+    'stoi' / 'estoi' is the extended STOI of every pair of the call in one
+    launch (lines 254-331; the 16 -> 10 kHz resampler is the Octave one,
+    where the reference's stoi_any_fs uses resampy).  'pesq' / 'sisnr',
+    dynamic metrics and bestPerfData raise."""
     import torch
     want = set(metricsToPlot)
-    unsupported = want - {'snr', 'fwSNRseg'}
+    unsupported = want - {'snr', 'fwSNRseg', 'stoi', 'estoi'}
     if unsupported:
-        raise NotImplementedError(f'metrics {sorted(unsupported)} are not on the device path (snr, fwSNRseg are)')
+        raise NotImplementedError(f'metrics {sorted(unsupported)} are not on the device path '
+                                  '(snr, fwSNRseg, stoi are)')
     if dynamic is not None or bestPerfData is not None:
         raise NotImplementedError('dynamic metrics / bestPerfData are not on the device path')
     if endIdx is None:
@@ -176,4 +213,15 @@ def get_metrics(clean, noiseOnly, noisy, filtSpeech, filtNoise, filtSpeech_c=Non
             setattr(fw, name, float(m))
         fw.diff = fw.after - fw.before
         out['fwSNRseg'] = fw
+    if 'stoi' in want or 'estoi' in want:
+        st = Metric()
+        pairs = [('before', noisy), ('after', enhan)] + \
+                [('after' + t, enh[t]) for t in ('Centr', 'Local', 'SSBC') if enh[t] is not None]
+        c = np.stack([clean.ravel()] * len(pairs))
+        e = np.stack([np.asarray(x, dtype=np.float64).ravel() for _, x in pairs])
+        vals = stoi_batch(c, e, fs, extended=True, device=device).cpu().numpy()
+        for (name, _), v in zip(pairs, vals):
+            setattr(st, name, float(v))
+        st.diff = st.after - st.before
+        out['stoi'] = st
     return out

@@ -383,6 +383,24 @@ int danse_dxcp_create(int32_t P, int device, danse_dxcp** out);
 void danse_dxcp_destroy(danse_dxcp* eng);
 const char* danse_dxcp_last_error(const danse_dxcp* eng);
 int danse_dxcp_process(danse_dxcp* eng, const float* x, double* out, void* stream);
+/* process_data(x_12_ell, tdoa): as danse_dxcp_process, with the STO
+ * estimate corrected by tdoa[p] * 16000 samples when its maximum is interior
+ * (sro_estimation.py:338-339).  tdoa: [P] double (device) or NULL.        */
+int danse_dxcp_process_tdoa(danse_dxcp* eng, const float* x, const double* tdoa, double* out, void* stream);
+/* Closed-loop DXCP-PhaT (class CL_DXCPPhaT, sro_estimation.py:12-72) for P
+ * pairs: per frame the OnlineResampler (online_resampler.py:4-77) of z_i by
+ * -SRO_est_curr, the 3-frame DelayBuffer (delay_buffer.py:8-26) of z_j,
+ * DXCP-PhaT on the synchronised pair and the IMC controller (PIT1, Tf = 8;
+ * frozen for ell <= startDelay).  Engines from danse_cl_dxcp_create are
+ * danse_dxcp handles (danse_dxcp_destroy frees them).
+ *   x:   [P][2][2048] float (device): z_j (reference) then z_i
+ *   acs: [P] int32 (device) or NULL (all 1): 0 forces the residual to 0
+ *   out: [P][3] double (device): dSRO_est_curr_raw, SRO_est_curr,
+ *        Resampler.shift after the call (the process() return values)
+ *   zi:  [P][2048] float (device) or NULL: the synchronised z_i block
+ *        (from two calls earlier)                                          */
+int danse_cl_dxcp_create(int32_t P, int32_t startDelay, int device, danse_dxcp** out);
+int danse_cl_dxcp_process(danse_dxcp* eng, const float* x, const int32_t* acs, double* out, float* zi, void* stream);
 
 /* ---- T(z) few-samples compression (broadcastType 'fewSamples').
  * danse_tz_create: analysis window h, synthesis window f (N floats, host), the
@@ -422,6 +440,20 @@ int danse_snr(const double* s, const double* n, const uint8_t* vad, int64_t T, i
 int danse_fwsnrseg_frames(int64_t T, double fs, double frameLen, double overlap, int32_t* nFrames);
 int danse_fwsnrseg(const double* clean, const double* enhanced, int64_t T, int32_t nSig, double fs, double frameLen,
                    double overlap, double gamma, double* perFrame, double* mean, void* stream);
+
+/* (e)STOI, float64 (csrc/stoi.hip) for nSig (clean, processed) pairs,
+ * replacing stoi / stoi_any_fs (danse_toolbox/mypystoi/stoi.py:18-239, the
+ * 'stoi' entry of get_metrics, d_eval.py:254-331, uses extended = True):
+ *     x, y: [nSig][T] double (device), fs: integer sampling rate
+ *     out:  [nSig] double (device)
+ * At fs != 10000 both signals are resampled to 10 kHz with the Octave
+ * resampler of mypystoi utils.resample_oct (utils.py:8-47), as stoi() does;
+ * stoi_any_fs resamples with resampy instead (absent offline: unpinned).
+ * Fewer than 30 STFT frames after silent-frame removal give 1e-5, as the
+ * reference.  Synchronises `stream` (scratch buffers).                 */
+const char* danse_stoi_last_error(void);
+int danse_stoi(const double* x, const double* y, int64_t T, int32_t nSig, double fs, int32_t extended, double* out,
+               void* stream);
 
 #ifdef __cplusplus
 }

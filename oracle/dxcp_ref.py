@@ -161,3 +161,119 @@ def run(x1, x2):
         sro[i] = out['SROppm_est_out']
         sto[i] = out['STOsmp_est_out']
     return sro, sto
+
+
+# --------------------------------------------------------------------------- #
+# Closed loop: CL_DXCPPhaT (sro_estimation.py:12-72) with its
+# OnlineResampler (online_resampler.py:4-77) and DelayBuffer
+# (delay_buffer.py:8-26); the same NumPy calls in the same order.
+# --------------------------------------------------------------------------- #
+class DelayBuffer:
+    def __init__(self, shape):
+        self.data = np.zeros(shape)
+        self.length = shape[-1]
+        self.pointer = 0
+
+    def write(self, frame):
+        self.data[..., self.pointer] = frame
+        self.pointer = (self.pointer + 1) % self.length
+
+    def read(self):
+        return self.data[..., self.pointer]
+
+
+class OnlineResampler:
+    """Integer shift by buffer selection, fractional rest by a linear phase
+    on the 2x-interpolated FFT of the Hann-windowed two-block selection,
+    overlap-added: returns the block from two calls earlier."""
+
+    def __init__(self, blockSize=FRAME):
+        self.blockSize = blockSize
+        self.fftSize = blockSize * 4
+        self.shift = 0
+        self.k = np.fft.fftshift(np.arange(-self.fftSize / 2, self.fftSize / 2))
+        self.win = signal.windows.hann(blockSize * 2, sym=False)
+        self.inputBuffer = np.zeros((blockSize * 4,))
+        self.outputBuffer = np.zeros((blockSize * 3,))
+
+    def process(self, signalBlock, sro, sto=0):
+        B = self.blockSize
+        self.inputBuffer[:(3 * B)] = self.inputBuffer[B:]
+        self.inputBuffer[3 * B:] = signalBlock
+        self.shift += sro * 1e-6 * B
+        accShift = self.shift + sto
+        integer_shift = np.round(accShift)
+        rest_shift = integer_shift - accShift
+        selectStart = int(B + integer_shift)
+        selectEnd = int((B + 2 * B) + integer_shift)
+        if selectStart < 0:
+            self.shift -= sro * 1e-6 * B
+            selectEnd = selectEnd - selectStart
+            selectStart = 0
+        elif selectEnd >= np.size(self.inputBuffer):
+            self.shift -= sro * 1e-6 * B
+            selectStart = selectStart - (selectEnd - np.size(self.inputBuffer))
+            selectEnd = np.size(self.inputBuffer)
+        sel = self.inputBuffer[selectStart:selectEnd]
+        X = np.fft.fft(self.win * sel, self.fftSize)
+        X *= np.exp(-1j * 2 * np.pi * self.k / self.fftSize * rest_shift)
+        self.outputBuffer[B:] = self.outputBuffer[B:] + np.real(np.fft.ifft(X))[:int(B * 2)]
+        self.outputBuffer[:2 * B] = self.outputBuffer[B:]
+        self.outputBuffer[2 * B:] = np.zeros((B,))
+        return self.outputBuffer[:B]
+
+
+class CL_DXCPPhaT:
+    """Resample z_i with the current estimate, delay z_j by the resampler's
+    two blocks (+1), DXCP-PhaT on the synchronised pair, IMC controller
+    (PIT1, Tf = 8) on the residual."""
+
+    def __init__(self, start_delay=0):
+        self.DXCPPhaT = DXCPPhaT()
+        self.Resampler = OnlineResampler()
+        self.zjBuffer = DelayBuffer((FRAME, 2 + 1))
+        self.dSRO_est = np.zeros(3)
+        self.SRO_est = np.zeros(3)
+        self.dSRO_est_curr = 0
+        self.dSRO_est_curr_raw = 0
+        self.SRO_est_curr = 0
+        self.SRO_est_op = 0
+        self.K_Nom = [0, 0.0251941968627353, -0.0249422548941180]
+        self.K_Denom = [1, -1.96825464010938, 0.968254640109407]
+        self.start_delay = start_delay
+        self.ell = 0
+
+    def process(self, x_12_ell, acs=1):
+        x_12_ell = np.array(x_12_ell, dtype=np.float64)
+        z_i = self.Resampler.process(x_12_ell[:, 1].flatten(), -self.SRO_est_curr)
+        x_12_ell[:, 1] = z_i
+        self.zjBuffer.write(x_12_ell[:, 0].flatten())
+        x_12_ell[:, 0] = self.zjBuffer.read()
+        res = self.DXCPPhaT.process_data(x_12_ell)
+        self.dSRO_est_curr_raw = res['SROppm_est_out']
+        self.dSRO_est_curr = res['SROppm_est_out'] if acs == 1 else 0
+        if self.ell <= self.start_delay:
+            self.dSRO_est_curr = 0
+        self.dSRO_est[1:] = self.dSRO_est[:-1]
+        self.dSRO_est[0] = self.dSRO_est_curr
+        self.SRO_est[1:] = self.SRO_est[:-1]
+        self.SRO_est[0] = np.dot(self.K_Nom, self.dSRO_est) - np.dot(self.K_Denom[1:], self.SRO_est[1:])
+        self.SRO_est_curr = self.SRO_est[0] + self.SRO_est_op
+        self.ell += 1
+        return self.dSRO_est_curr_raw, self.SRO_est_curr, self.Resampler.shift, z_i
+
+
+def run_closed_loop(x1, x2, start_delay=0, acs=None):
+    """Feed (z_j = x1, z_i = x2) frame by frame; per frame (raw residual ppm,
+    controlled SRO estimate ppm, resampler shift, synchronised z_i block)."""
+    cl = CL_DXCPPhaT(start_delay)
+    n = len(x1) // FRAME
+    out = np.zeros((n, 3))
+    zi = np.zeros((n, FRAME))
+    for i in range(n):
+        fr = np.stack((x1[i * FRAME:(i + 1) * FRAME], x2[i * FRAME:(i + 1) * FRAME]), axis=1)
+        a = 1 if acs is None else int(acs[i])
+        d, s, sh, z = cl.process(fr, a)
+        out[i] = (d, s, sh)
+        zi[i] = z
+    return out, zi

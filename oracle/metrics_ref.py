@@ -93,3 +93,125 @@ def get_fwsnrseg(cleanSig, enhancedSig, fs, frameLen=0.03, overlap=0.75, gamma=0
     snrlog = 10 * np.log10((ce ** 2) / err)
     fw = np.sum(wf * snrlog, 0) / np.sum(wf, 0)
     return np.clip(fw, 0, 35)
+
+
+# --------------------------------------------------------------------------- #
+# (e)STOI -- danse_toolbox/mypystoi/stoi.py:18-239, utils.py (pystoi).
+# Restated without the EPS-level random perturbation of row_col_normalize
+# (utils.py:134-149: EPS * np.random.standard_normal, ~1e-16 relative).
+# --------------------------------------------------------------------------- #
+STOI_FS = 10000
+STOI_NFRAME = 256
+STOI_NFFT = 512
+STOI_NUMBAND = 15
+STOI_MINFREQ = 150
+STOI_N = 30
+STOI_BETA = -15.0
+STOI_DYN = 40
+EPS = np.finfo('float').eps
+
+
+def thirdoct(fs=STOI_FS, nfft=STOI_NFFT, num_bands=STOI_NUMBAND, min_freq=STOI_MINFREQ):
+    """utils.py:57-84: the bin range [lo, hi) of every 1/3-octave band."""
+    f = np.linspace(0, fs, nfft + 1)[:nfft // 2 + 1]
+    k = np.arange(num_bands).astype(float)
+    lo = min_freq * np.power(2., (2 * k - 1) / 6)
+    hi = min_freq * np.power(2., (2 * k + 1) / 6)
+    out = np.zeros((num_bands, 2), dtype=np.int64)
+    for i in range(num_bands):
+        out[i, 0] = np.argmin(np.square(f - lo[i]))
+        out[i, 1] = np.argmin(np.square(f - hi[i]))
+    return out
+
+
+def resample_window_oct(p, q):
+    """utils.py:8-40 (Kaiser-windowed sinc of the Octave resampler)."""
+    g = np.gcd(p, q)
+    p, q = p // g, q // g
+    log10_rejection = -3.0
+    stop = 1. / (2 * max(p, q))
+    roll = stop / 10
+    rej = -20 * log10_rejection
+    L = np.ceil((rej - 8) / (28.714 * roll))
+    t = np.arange(-L, L + 1)
+    ideal = 2 * p * stop * np.sinc(2 * stop * t)
+    if 21 <= rej <= 50:
+        beta = 0.5842 * (rej - 21) ** 0.4 + 0.07886 * (rej - 21)
+    elif rej > 50:
+        beta = 0.1102 * (rej - 8.7)
+    else:
+        beta = 0.0
+    return np.kaiser(2 * L + 1, beta) * ideal
+
+
+def resample_oct(x, p, q):
+    """utils.py:43-47: resample_poly(x, p, q) with that window (sum-normalised)."""
+    from scipy.signal import resample_poly
+    h = resample_window_oct(p, q)
+    return resample_poly(x, p, q, window=h / np.sum(h))
+
+
+def _hann(n):
+    return np.hanning(n + 2)[1:-1]
+
+
+def remove_silent_frames(x, y, dyn_range=STOI_DYN, framelen=STOI_NFRAME, hop=STOI_NFRAME // 2):
+    """utils.py:102-126."""
+    w = _hann(framelen)
+    xf = np.array([w * x[i:i + framelen] for i in range(0, len(x) - framelen, hop)])
+    yf = np.array([w * y[i:i + framelen] for i in range(0, len(x) - framelen, hop)])
+    e = 20 * np.log10(np.linalg.norm(xf, axis=1) + EPS)
+    mask = (np.max(e) - dyn_range - e) < 0
+    xf, yf = xf[mask], yf[mask]
+    n = (len(xf) - 1) * hop + framelen
+    xs, ys = np.zeros(n), np.zeros(n)
+    for i in range(xf.shape[0]):
+        xs[i * hop:i * hop + framelen] += xf[i]
+        ys[i * hop:i * hop + framelen] += yf[i]
+    return xs, ys
+
+
+def stoi_stft(x, win=STOI_NFRAME, nfft=STOI_NFFT, overlap=2):
+    """utils.py:87-99."""
+    hop = int(win / overlap)
+    w = _hann(win)
+    return np.array([np.fft.rfft(w * x[i:i + win], n=nfft) for i in range(0, len(x) - win, hop)])
+
+
+def stoi(x, y, fs_sig, extended=False):
+    """stoi.py:18-119 (``stoi``; resample_oct to 10 kHz) -- and, at
+    fs_sig == 10000, ``stoi_any_fs`` (stoi.py:122-239), whose only
+    difference is resampy for fs_sig != 10000."""
+    x = np.squeeze(np.asarray(x, dtype=np.float64))
+    y = np.squeeze(np.asarray(y, dtype=np.float64))
+    if fs_sig != STOI_FS:
+        x = resample_oct(x, STOI_FS, int(fs_sig))
+        y = resample_oct(y, STOI_FS, int(fs_sig))
+    x, y = remove_silent_frames(x, y)
+    xs = stoi_stft(x).T
+    ys = stoi_stft(y).T
+    if xs.shape[-1] < STOI_N:
+        return 1e-5
+    bands = thirdoct()
+    obm = np.zeros((STOI_NUMBAND, STOI_NFFT // 2 + 1))
+    for i, (lo, hi) in enumerate(bands):
+        obm[i, lo:hi] = 1
+    xt = np.sqrt(obm @ np.square(np.abs(xs)))
+    yt = np.sqrt(obm @ np.square(np.abs(ys)))
+    xseg = np.array([xt[:, m - STOI_N:m] for m in range(STOI_N, xt.shape[1] + 1)])
+    yseg = np.array([yt[:, m - STOI_N:m] for m in range(STOI_N, xt.shape[1] + 1)])
+    if extended:
+        def rcn(a):
+            a = a - np.mean(a, axis=-1, keepdims=True)
+            a = a / np.sqrt(np.sum(np.square(a), axis=-1, keepdims=True))
+            a = a - np.mean(a, axis=1, keepdims=True)
+            return a / np.sqrt(np.sum(np.square(a), axis=1, keepdims=True))
+        xn, yn = rcn(xseg), rcn(yseg)
+        return np.sum(xn * yn / STOI_N) / xn.shape[0]
+    nc = np.linalg.norm(xseg, axis=2, keepdims=True) / (np.linalg.norm(yseg, axis=2, keepdims=True) + EPS)
+    yp = np.minimum(yseg * nc, xseg * (1 + 10 ** (-STOI_BETA / 20)))
+    yp = yp - np.mean(yp, axis=2, keepdims=True)
+    xs_ = xseg - np.mean(xseg, axis=2, keepdims=True)
+    yp /= (np.linalg.norm(yp, axis=2, keepdims=True) + EPS)
+    xs_ /= (np.linalg.norm(xs_, axis=2, keepdims=True) + EPS)
+    return np.sum(yp * xs_) / (xs_.shape[0] * xs_.shape[1])

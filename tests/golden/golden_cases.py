@@ -182,6 +182,22 @@ DXCP_CASES = [
 ]
 
 
+# closed-loop DXCP-PhaT (CL_DXCPPhaT, sro_estimation.py:12-72): online
+# resampler + delay buffer + DXCP-PhaT + IMC controller; acsEvery > 0 sets
+# acs = 0 on every acsEvery-th frame
+CLDXCP_CASES = [
+    dict(name='cldxcp_sro100', dur=40.0, sro=100.0, delay=3.5, seed=34, startDelay=0, acsEvery=0),
+    dict(name='cldxcp_sro_m60', dur=30.0, sro=-60.0, delay=-2.0, seed=35, startDelay=12, acsEvery=7),
+]
+
+
+def cldxcp_acs(case, n):
+    a = np.ones(n, dtype=np.int64)
+    if case['acsEvery'] > 0:
+        a[::case['acsEvery']] = 0
+    return a
+
+
 def dxcp_inputs(case, fs=16000.0):
     """Exact evaluation of a random multi-sine at each channel's sample
     instants (no resampler needed), plus independent sensor noise."""
@@ -288,3 +304,36 @@ def get_metrics_inputs(case):
 FIELD_CASES = ['online_C_sro_comp_asy', 'online_C_sro_noflags_seq', 'online_B_k4m3_seq', 'online_ragged_asy_r2',
                'online_E_fs_L64_asy']
 FIELD_STFT_BIN_STEP = 37
+
+
+# (e)STOI (danse_toolbox/mypystoi/stoi.py): at 10 kHz stoi_any_fs (no
+# resampling; resampy is absent offline), at 16 kHz stoi() (the Octave
+# resampler utils.resample_oct, scipy); extended (eSTOI, what get_metrics
+# uses, d_eval.py:254-331) and classic
+STOI_CASES = [
+    dict(name='stoi_10k', T=60000, fs=10000, seed=401, noise=0.4, fn='stoi_any_fs'),
+    dict(name='stoi_16k_oct', T=96000, fs=16000, seed=402, noise=0.25, fn='stoi'),
+    dict(name='stoi_16k_oct_ragged', T=80123, fs=16000, seed=403, noise=1.0, fn='stoi'),
+]
+
+
+def stoi_inputs(case):
+    """clean: on/off bursts of coloured noise with silent stretches (the
+    silent-frame removal drops them); enhanced: scaled clean plus noise."""
+    rng = np.random.default_rng(case['seed'])
+    T = case['T']
+    x = rng.standard_normal(T)
+    x = np.convolve(x, np.ones(6) / 6, mode='same')
+    env = (np.sin(2 * np.pi * np.arange(T) / (0.7 * case['fs'])) > 0.1).astype(float)
+    env *= 0.5 + 0.5 * np.abs(np.sin(2 * np.pi * np.arange(T) / (0.13 * case['fs'])))
+    clean = x * env
+    enh = 0.7 * clean + case['noise'] * np.convolve(rng.standard_normal(T), np.ones(3) / 3, mode='same')
+    return clean, enh
+
+
+# end to end: the reference's online DANSE, its noise-only / speech-only
+# replays (generate_signals_for_snr_computation, d_core.py:550-599) and
+# get_metrics (d_eval.py:70-373; snr and fwSNRseg -- its stoi needs resampy)
+# per node, from sample startIdx to the end
+E2E_METRICS_CASE = dict(name='metrics_e2e_k3', M=[2, 2, 2], dur=4.0, seed=31, startIdx=16000,
+                        danse=_d(BATTERY, nodeUpdating='asy', computeLocal=True, computeCentralised=True))

@@ -23,9 +23,9 @@ sys.path.insert(0, str(HERE))
 import _refharness as H  # noqa: E402
 from danse_amd.scene import make_scene, scene_digest  # noqa: E402
 from golden_cases import ONLINE_CASES, BATCH_CASES, SRO_EVENT_CASES, KAT_CASES, kat_inputs, BESTPERF_CASES  # noqa: E402
-from golden_cases import DXCP_CASES, dxcp_inputs, TZ_CASES, tz_inputs  # noqa: E402
+from golden_cases import DXCP_CASES, dxcp_inputs, TZ_CASES, tz_inputs, CLDXCP_CASES, cldxcp_acs  # noqa: E402
 from golden_cases import METRIC_CASES, metric_inputs, GETMETRICS_CASE, get_metrics_inputs  # noqa: E402
-from golden_cases import FIELD_CASES, FIELD_STFT_BIN_STEP  # noqa: E402
+from golden_cases import FIELD_CASES, FIELD_STFT_BIN_STEP, STOI_CASES, stoi_inputs, E2E_METRICS_CASE  # noqa: E402
 
 
 def _run_online(ns, case):
@@ -190,6 +190,22 @@ def _run_dxcp(ns, case):
     return {'sro': sro, 'sto': sto}
 
 
+def _run_cldxcp(ns, case):
+    import sro_estimation   # dxcpphat/ (on sys.path once the reference is loaded)
+    x1, x2 = dxcp_inputs(case)
+    cl = sro_estimation.CL_DXCPPhaT(start_delay=case['startDelay'])
+    n = len(x1) // 2048
+    acs = cldxcp_acs(case, n)
+    out = np.zeros((n, 3))
+    zi = np.zeros((n, 2048))
+    for i in range(n):
+        fr = np.stack((x1[i * 2048:(i + 1) * 2048], x2[i * 2048:(i + 1) * 2048]), axis=1)
+        d, s_, sh, z = cl.process(fr, int(acs[i]))
+        out[i] = (d, s_, sh)
+        zi[i] = z
+    return {'out': out, 'zi': zi[::5]}
+
+
 def _run_tz(ns, case):
     wHat, yq, h, f, wPrev = tz_inputs(case)
     z, wIR = ns.base.danse_compression_few_samples(yq, wHat, case['L'], wPrev, h, f, case['Ns'],
@@ -218,6 +234,41 @@ def _run_get_metrics(ns, case):
     return out
 
 
+def _run_stoi(ns, case):
+    import importlib
+    st = importlib.import_module('danse_toolbox.mypystoi.stoi')   # the module (the package re-exports a function of that name)
+    x, y = stoi_inputs(case)
+    fn = getattr(st, case['fn'])
+    np.random.seed(0)   # row_col_normalize adds EPS-scaled noise from the global generator
+    return {'estoi': np.float64(fn(x, y, case['fs'], extended=True)),
+            'stoi': np.float64(fn(x, y, case['fs'], extended=False))}
+
+
+def _run_e2e_metrics(ns, case):
+    import danse_toolbox.d_eval as ev
+    sc = make_scene(case['M'], sigDur=case['dur'], seed=case['seed'])
+    p = H.make_params(ns, case['M'], **case['danse'])
+    w = H.to_ref_wasn(ns, sc)
+    p, w = H.prep(ns, p, w)
+    dv, w = ns.core.danse(w, p.danseParams)
+    sigs = ns.core.generate_signals_for_snr_computation(p.danseParams, dv, w, ns.core.danse)
+    ref = p.danseParams.referenceSensor
+    out = {'digest': scene_digest(sc)}
+    for k in range(len(case['M'])):
+        nd = sc.wasn[k]
+        m = ev.get_metrics(clean=nd.cleanspeech[:, ref], noiseOnly=nd.cleannoise[:, ref], noisy=nd.data[:, ref],
+                           filtSpeech=sigs['s'][:, k], filtNoise=sigs['n'][:, k],
+                           filtSpeech_c=sigs['s_c'][:, k], filtNoise_c=sigs['n_c'][:, k],
+                           filtSpeech_l=sigs['s_l'][:, k], filtNoise_l=sigs['n_l'][:, k],
+                           enhan=dv.d[:, k], enhan_c=dv.dCentr[:, k], enhan_l=dv.dLocal[:, k],
+                           startIdx=case['startIdx'], endIdx=nd.data.shape[0], fs=nd.fs, vad=nd.vad,
+                           metricsToPlot=['snr', 'fwSNRseg'])
+        for key in ('snr', 'fwSNRseg'):
+            for fld in ('before', 'after', 'diff', 'afterCentr', 'afterLocal'):
+                out[f'{key}_{fld}_{k}'] = np.float64(getattr(m[key], fld))
+    return out
+
+
 def main():
     ns = H.load()
     only = sys.argv[1:]
@@ -227,9 +278,12 @@ def main():
            [('events', c, _run_sro_events) for c in SRO_EVENT_CASES] + \
            [('kat', c, _run_kat) for c in KAT_CASES] + \
            [('dxcp', c, _run_dxcp) for c in DXCP_CASES] + \
+           [('cldxcp', c, _run_cldxcp) for c in CLDXCP_CASES] + \
            [('tz', c, _run_tz) for c in TZ_CASES] + \
            [('metrics', c, _run_metrics) for c in METRIC_CASES] + \
            [('metrics', GETMETRICS_CASE, _run_get_metrics)] + \
+           [('stoi', c, _run_stoi) for c in STOI_CASES] + \
+           [('metrics', E2E_METRICS_CASE, _run_e2e_metrics)] + \
            [('fields', dict(name=f'fields_{c}', src=c), lambda ns, c: _run_fields(ns, c['src'])) for c in FIELD_CASES]
     for kind, case, fn in jobs:
         name = case['name']

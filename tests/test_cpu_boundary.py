@@ -157,13 +157,14 @@ def test_yaml_config_loads():
 
 
 def test_get_metrics_rejects_metrics_off_the_device_path():
-    """eSTOI / PESQ / SI-SNR, dynamic metrics and bestPerfData raise before
-    any device work (danse_amd/metrics.py get_metrics)."""
+    """PESQ / SI-SNR, dynamic metrics and bestPerfData raise before any
+    device work (danse_amd/metrics.py get_metrics; snr, fwSNRseg and
+    (e)STOI are on the device)."""
     import numpy as np
     import pytest
     from danse_amd import metrics as DM
     x = np.zeros(4000)
-    for m in (['stoi'], ['pesq'], ['snr', 'sisnr']):
+    for m in (['pesq'], ['snr', 'sisnr'], ['stoi', 'pesq']):
         with pytest.raises(NotImplementedError):
             DM.get_metrics(x, x, x, x, x, metricsToPlot=m)
     with pytest.raises(NotImplementedError):

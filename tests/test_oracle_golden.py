@@ -193,3 +193,37 @@ def test_get_metrics_quirks_vs_reference(golden_dir):
                    ('afterLocal', kw['enhan_l'][sl])):
         v = np.mean(MR.get_fwsnrseg(c, e, fs, 0.03, 0.2))   # overlap = gamma = 0.2
         assert abs(v - g[f'fwSNRseg_{fld}']) <= 1e-9, fld
+
+
+from golden_cases import STOI_CASES, stoi_inputs  # noqa: E402
+
+
+@pytest.mark.parametrize('case', STOI_CASES, ids=[c['name'] for c in STOI_CASES])
+def test_stoi_oracle_vs_reference(case, golden_dir):
+    """oracle/metrics_ref.stoi against mypystoi (stoi_any_fs at 10 kHz, stoi
+    at 16 kHz), both float64 (the reference adds EPS-scale noise in eSTOI)."""
+    from oracle import metrics_ref as MR
+    g = _load(golden_dir, case['name'])
+    x, y = stoi_inputs(case)
+    assert abs(MR.stoi(x, y, case['fs'], extended=True) - float(g['estoi'])) <= 1e-12
+    assert abs(MR.stoi(x, y, case['fs'], extended=False) - float(g['stoi'])) <= 1e-12
+
+
+from golden_cases import CLDXCP_CASES, cldxcp_acs  # noqa: E402
+
+
+@pytest.mark.parametrize('case', CLDXCP_CASES, ids=[c['name'] for c in CLDXCP_CASES])
+def test_cl_dxcp_oracle_matches_reference(case, golden_dir):
+    """oracle/dxcp_ref.run_closed_loop against the reference's CL_DXCPPhaT
+    (sro_estimation.py:12-72): bit for bit."""
+    import warnings
+    from golden_cases import dxcp_inputs
+    from oracle import dxcp_ref as D
+    g = _load(golden_dir, case['name'])
+    x1, x2 = dxcp_inputs(case)
+    n = len(x1) // 2048
+    with warnings.catch_warnings():
+        warnings.simplefilter('ignore', DeprecationWarning)
+        out, zi = D.run_closed_loop(x1, x2, case['startDelay'], cldxcp_acs(case, n))
+    assert np.array_equal(out, g['out'])
+    assert np.array_equal(zi[::5], g['zi'])
