@@ -178,6 +178,9 @@ def main():
                     help='config D on N>1 GPUs: independent WASNs per GPU (weak scaling) or every GPU owning a '
                          'node block of the same WASNs, external filters all-gathered per iteration (strong)')
     ap.add_argument('--L', type=int, default=None, help='broadcastLength override (fewSamples workloads)')
+    ap.add_argument('--scene-gen', default='auto', choices=['auto', 'host', 'device'],
+                    help='synthetic scenes from the host generator (danse_amd.scene.make_scene) or the device one '
+                         '(csrc/scene.hip, with SRO resampling); auto: device from 64 scenes per GPU on')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
     ap.add_argument('--no-graph', action='store_true')
@@ -324,15 +327,26 @@ def run_online(args, wl, S, rank, world, local, dist, traffic=True, pmc_child=Fa
         nodes = None
     t0 = time.time()
     scenes = []
-    for i, sd in enumerate(seeds):
-        sc = make_scene(M, sigDur=wl['dur'], seed=1000 + sd, nodes=nodes, SROperNode=wl.get('sros'))
-        sc.get_vad_per_frame(dp.DFTsize, dp.Ns, wp.vadMinProportionActive)
-        scenes.append(sc)
-        if (i + 1) % 64 == 0:
-            print(f'# {i + 1}/{len(seeds)} scenes generated', file=sys.stderr, flush=True)
+    gen = args.scene_gen if args.scene_gen != 'auto' else ('device' if len(seeds) >= 64 else 'host')
+    yDev = None
+    if gen == 'device':
+        from danse_amd.scene import make_scenes_device
+        scenes, dev = make_scenes_device(M, len(seeds), sigDur=wl['dur'], seed=1000 + seeds[0],
+                                         SROperNode=wl.get('sros'), device=local)
+        yDev = dev['data']
+        for sc in scenes:
+            sc.get_vad_per_frame(dp.DFTsize, dp.Ns, wp.vadMinProportionActive)
+        torch.cuda.synchronize()
+    else:
+        for i, sd in enumerate(seeds):
+            sc = make_scene(M, sigDur=wl['dur'], seed=1000 + sd, nodes=nodes, SROperNode=wl.get('sros'))
+            sc.get_vad_per_frame(dp.DFTsize, dp.Ns, wp.vadMinProportionActive)
+            scenes.append(sc)
+            if (i + 1) % 64 == 0:
+                print(f'# {i + 1}/{len(seeds)} scenes generated', file=sys.stderr, flush=True)
     tScene = time.time() - t0
     eng = DanseEngine(scenes, dp, vadMinProp=wp.vadMinProportionActive, device=local, keepHistory=True,
-                      nodeRange=(k0, k1))
+                      nodeRange=(k0, k1), yDevice=yDev)
     R, F = eng.R, eng.F
     stream = torch.cuda.current_stream()
 
@@ -426,7 +440,8 @@ def run_online(args, wl, S, rank, world, local, dist, traffic=True, pmc_child=Fa
             'hbm_GBs': gbs, 'hbm_frac': gbs / HBM_PEAK_GBS, 'valu_TFs': tfs, 'valu_frac': tfs / FP32_VALU_PEAK_TFS}
     return {
         'value': value, 'ms_per_step': el / args.steps * 1e3, 'rounds': R,
-        'data': f'synthetic random-IR scenes (seeded), {Stot} scenes x {K} nodes x {F} bins x {R} rounds per step',
+        'data': f'synthetic random-IR scenes (seeded, {gen} generator{", SRO-resampled" if gen == "device" and wl.get("sros") else ""}), '
+                f'{Stot} scenes x {K} nodes x {F} bins x {R} rounds per step',
         'config': {'workload': wl['desc'], 'scenes_per_gpu': S, 'K': K, 'M': M if len(set(M)) > 1 else M[0],
                    'D': Dk if len(set(Dk)) > 1 else Dk[0], 'bins': F, 'rounds': R, 'shard': shard,
                    'gevd_rank': 1, 'graph': not args.no_graph},

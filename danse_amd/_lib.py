@@ -28,6 +28,16 @@ EXT_COPY, EXT_RELAX, EXT_KEEP, EXT_REFONLY = 0, 1, 2, 3
 OUT_W, OUT_WEXT, OUT_D, OUT_DHAT, OUT_Z, OUT_DIAG = 0, 1, 2, 3, 4, 5
 
 
+class SceneCfg(ctypes.Structure):
+    _fields_ = [
+        ('S', _c_i32), ('K', _c_i32), ('M', _p_i32), ('T', _c_i32), ('nIR', _c_i32), ('seed', ctypes.c_int64),
+        ('fs', ctypes.c_double), ('snr', ctypes.c_double), ('selfnoiseSNR', ctypes.c_double),
+        ('pauseDuration', ctypes.c_double), ('pauseSpacing', ctypes.c_double),
+        ('vadEnergyDecrease_dB', ctypes.c_double), ('vadWinLength', ctypes.c_double),
+        ('sroPpm', ctypes.POINTER(ctypes.c_double)),
+    ]
+
+
 class DanseCfg(ctypes.Structure):
     _fields_ = [
         ('S', _c_i32), ('K', _c_i32), ('M', _p_i32),
@@ -44,7 +54,7 @@ class DanseCfg(ctypes.Structure):
         ('fsTab', _p_i32), ('zStreamLen', _c_i32), ('scmInitPerBin', _c_i32),
         ('cohDrift', _c_i32), ('cdSegLength', _c_i32), ('cdStart', _c_i32), ('cdEvery', _c_i32),
         ('cdCompensate', _c_i32), ('cdNIter', _c_i32), ('cdAlpha', ctypes.c_double), ('cdAlphaEps', ctypes.c_double),
-        ('cEnd', _p_i32), ('cPhase', ctypes.POINTER(ctypes.c_double)),
+        ('cEnd', _p_i32), ('cPhase', ctypes.POINTER(ctypes.c_double)), ('dxcp', _c_i32),
     ]
 
 
@@ -120,6 +130,7 @@ SIGNATURES = {
     'danse_dxcp_destroy': (None, [ctypes.c_void_p]),
     'danse_dxcp_last_error': (ctypes.c_char_p, [ctypes.c_void_p]),
     'danse_dxcp_process': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    'danse_dxcp_reset': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p]),
     'danse_dxcp_process_tdoa': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.c_void_p]),
     'danse_cl_dxcp_create': (_c_i32, [_c_i32, _c_i32, _c_i32, ctypes.POINTER(ctypes.c_void_p)]),
@@ -136,6 +147,9 @@ SIGNATURES = {
     'danse_fwsnrseg': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, _c_i32, ctypes.c_double,
                                 ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_void_p, ctypes.c_void_p,
                                 ctypes.c_void_p]),
+    'danse_scene_last_error': (ctypes.c_char_p, []),
+    'danse_scene_generate': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.c_void_p]),
     'danse_stoi_last_error': (ctypes.c_char_p, []),
     'danse_stoi': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, _c_i32, ctypes.c_double, _c_i32,
                             ctypes.c_void_p, ctypes.c_void_p]),

@@ -17,6 +17,7 @@
 #include <string>
 #include <vector>
 
+#include "../../include/danse_mi355x.h"
 #include "classes.hpp"
 #include "wfft.hpp"
 

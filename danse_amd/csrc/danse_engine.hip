@@ -9,6 +9,7 @@
 #include <string>
 #include <vector>
 
+#include "../../include/danse_mi355x.h"
 #include "bcast.hpp"
 #include "classes.hpp"
 #include "gate.hpp"
@@ -95,6 +96,13 @@ struct danse_engine {
   std::vector<int> fsTab;          // host copy [R][K][DANSE_FS_FIELDS]
   int* dFsTab = nullptr;
   float *wIR = nullptr, *dSn = nullptr;
+  // DXCP-PhaT SRO estimation in the loop (cfg.dxcp, an extension: the
+  // reference's integration raises, quirk Q12): one estimator per (scene,
+  // receiver, sender), fed every kDxEvery rounds
+  int dxcpOn = 0;
+  danse_dxcp* dx = nullptr;
+  float* dxFrames = nullptr;     // [P][2][2048]
+  double *dxOut = nullptr, *dxEst = nullptr;   // [P][2], [S][K][K] current estimate (relative SRO)
   // centralised / SSBC raw frames under asynchronous clocks (cfg.cEnd)
   int* dCEnd = nullptr;
   cf* Cspec = nullptr;
@@ -242,13 +250,70 @@ __global__ void fs_ir_init_kernel(float* wIR, int K, int Mmax, int ref, int N) {
   if (threadIdx.x == 0) wIR[((long long)sk * Mmax + ref) * tzc::kA + N] = 1.0f;
 }
 
+// ---- DXCP-PhaT in the loop (extension; SURVEY §8e "DXCP per node pair after
+// the z all-gather").  Every kDxEvery = 2048 / Ns rounds each receiver k
+// feeds its estimator of sender q with the 2048 newest samples of its
+// local reference sensor (ending at the update frame end upEnd[r][k]) and of
+// q's fused-signal stream as k has received it ((r + 1 - zLag) Ns samples):
+// consecutive, non-overlapping DXCP-PhaT frames (sro_estimation.py:208-227).
+// The estimate of q's sampling rate relative to k's, eps_kq = -SRO ppm 1e-6
+// (DXCP-PhaT reports the second channel's sampling-period excess), replaces
+// the Oracle value of update_sro_estimates (d_classes.py:2364-2621): the
+// sender's phase accumulator loses eps Ns after every round's update.
+constexpr int kDxFrame = 2048;
+__global__ void __launch_bounds__(256) dxcp_gather_kernel(const UpdateArgs a, const int* upEnd, const float* y,
+                                                          const float* zStream, int zLen, int T, int Ns,
+                                                          const int* base, int ref, int k0, int nOwn,
+                                                          float* frames) {
+  const int K = a.K, r = a.r;
+  const int qi = blockIdx.x % (K - 1);
+  const int k = k0 + (int)((blockIdx.x / (K - 1)) % nOwn);
+  const int s = blockIdx.x / ((K - 1) * nOwn);
+  const int q = qi < k ? qi : qi + 1;
+  const int e0 = upEnd[r * K + k];
+  const int lag = a.zLag ? a.zLag[((long long)r * K + k) * K + q] : 0;
+  const long long zEnd = (long long)(r + 1 - lag) * Ns;
+  const float* yl = y + ((long long)s * a.MT + base[k] + ref) * T;
+  const float* zs = zStream + ((long long)s * K + q) * zLen;
+  float* f = frames + (long long)blockIdx.x * 2 * kDxFrame;
+  for (int n = threadIdx.x; n < kDxFrame; n += blockDim.x) {
+    const long long iy = (long long)e0 - kDxFrame + n, iz = zEnd - kDxFrame + n;
+    f[n] = (iy >= 0 && iy < T) ? yl[iy] : 0.0f;
+    f[kDxFrame + n] = (iz >= 0 && iz < zLen) ? zs[iz] : 0.0f;
+  }
+}
+
+// after round r's update: new DXCP estimates on feeding rounds, then the
+// phase accumulation and the SROsEstimates / SROsResiduals rows of round r
+__global__ void dxcp_round_kernel(int S, int K, int k0, int nOwn, int r, int R, int fed, int compensate, double Ns,
+                                  const double* dxOut, double* est, double* phase, double* estHist,
+                                  double* resHist) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= S * nOwn * (K - 1)) return;
+  const int qi = p % (K - 1);
+  const int k = k0 + (p / (K - 1)) % nOwn;
+  const int s = p / ((K - 1) * nOwn);
+  const int q = qi < k ? qi : qi + 1;
+  double* e = est + ((long long)s * K + k) * K + q;
+  if (fed) *e = -dxOut[2 * p] * 1e-6;
+  const double v = *e;
+  const long long o = (((long long)s * K + k) * R + r) * (K - 1) + qi;
+  resHist[o] = v;
+  estHist[o] = compensate ? v : 0.0;
+  if (compensate) phase[((long long)s * K + k) * K + q] -= v * Ns;
+}
+
 int danse_engine_reset(danse_engine* eng, void* stream) {
   if (!eng) return fail(eng, "null engine");
   HIPCHK(hipSetDevice(eng->dev));
   hipStream_t st = (hipStream_t)stream;
   const int S = eng->S, K = eng->K, F = eng->F, R = eng->R;
   HIPCHK(hipMemsetAsync(eng->zPrev, 0, (size_t)S * K * eng->N * sizeof(float), st));
-  if (eng->cohDrift) {
+  if (eng->dxcpOn) {
+    HIPCHK(hipMemsetAsync(eng->dxEst, 0, (size_t)S * K * K * sizeof(double), st));
+    if (danse_dxcp_reset(eng->dx, st) != 0) return fail(eng, std::string("DXCP estimator: ") + danse_dxcp_last_error(eng->dx));
+  }
+  if (eng->cohDrift || eng->dxcpOn) {
     HIPCHK(hipMemsetAsync(eng->cdPhase, 0, (size_t)S * K * K * sizeof(double), st));
     HIPCHK(hipMemsetAsync(eng->cdEst, 0, (size_t)S * K * (K - 1) * R * sizeof(double), st));
     HIPCHK(hipMemsetAsync(eng->cdRes, 0, (size_t)S * K * (K - 1) * R * sizeof(double), st));
@@ -506,6 +571,25 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
   HIPCHK(dalloc(&eng->d, (size_t)kMaxFam * S * K * c->T));
   HIPCHK(dalloc(&eng->diag, (size_t)S * K * kMaxFam));
   if (eng->liStride > 0) HIPCHK(dalloc(&eng->liCache, (size_t)S * eng->liStride));
+  if (c->dxcp) {
+    if (c->cohDrift) return fail(eng, "DXCP-PhaT and CohDrift estimation are exclusive");
+    if (c->fsTab) return fail(eng, "DXCP-PhaT estimation runs on wholeChunk broadcasts");
+    if (kDxFrame % c->Ns) return fail(eng, "DXCP-PhaT frames need Ns dividing 2048");
+    eng->dxcpOn = 1;
+    eng->cdComp = c->cdCompensate;
+    const size_t P = (size_t)S * (c->k1 - c->k0) * (K - 1);
+    const size_t nq = (size_t)S * K * (K - 1);
+    HIPCHK(dalloc(&eng->dxFrames, P * 2 * kDxFrame));
+    HIPCHK(dalloc(&eng->dxOut, P * 2));
+    HIPCHK(dalloc(&eng->dxEst, (size_t)S * K * K));
+    HIPCHK(dalloc(&eng->cdPhase, (size_t)S * K * K));
+    HIPCHK(dalloc(&eng->cdEst, nq * R));
+    HIPCHK(dalloc(&eng->cdRes, nq * R));
+    HIPCHK(hipMemset(eng->cdEst, 0, nq * R * sizeof(double)));
+    HIPCHK(hipMemset(eng->cdRes, 0, nq * R * sizeof(double)));
+    if (danse_dxcp_create((int)P, device, &eng->dx) != 0)
+      return fail(eng, std::string("DXCP estimator: ") + danse_dxcp_last_error(nullptr));
+  }
   if (c->cohDrift) {
     if (c->cdSegLength < 1 || c->cdEvery < 1 || c->cdStart < c->cdSegLength) return fail(eng, "bad CohDrift parameters");
     eng->cohDrift = 1;
@@ -613,9 +697,11 @@ void danse_engine_destroy(danse_engine* eng) {
                   eng->diag, eng->dW0, eng->dScm0, eng->dExt0, eng->dTgt0, eng->dFnAll, eng->dInitW0Off,
                   eng->dInitScmOff, eng->dExtSrcOff, eng->dTgtOff, eng->dFsTab, eng->wIR, eng->dSn, eng->liCache,
                   eng->dGateCand, eng->dGateVerdict, eng->cdRing, eng->cdAvg, eng->cdPhase, eng->cdEst,
-                  eng->cdRes, eng->dCEnd, eng->Cspec, eng->dChanNode, eng->dCPhase};
+                  eng->cdRes, eng->dCEnd, eng->Cspec, eng->dChanNode, eng->dCPhase, eng->dxFrames, eng->dxOut,
+                  eng->dxEst};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
+  if (eng->dx) danse_dxcp_destroy(eng->dx);
   for (auto& cl : eng->classes) {
     if (cl.dev) (void)hipFree(cl.dev);
     if (cl.devIds) (void)hipFree(cl.devIds);
@@ -677,6 +763,19 @@ static void launch_update(danse_engine* e, int r, hipStream_t st) {
     c.phase = e->cdPhase; c.est = e->cdEst; c.res = e->cdRes; c.R = e->R;
     c.k0 = e->k0; c.nOwn = e->k1 - e->k0;
     hipLaunchKernelGGL(cohdrift_kernel, dim3(e->S * c.nOwn * (e->K - 1)), dim3(kCdThreads), 0, st, make_update(e, r), c);
+  }
+  if (e->dxcpOn) {
+    const int nOwn = e->k1 - e->k0;
+    const int P = e->S * nOwn * (e->K - 1);
+    const int every = kDxFrame / e->Ns;
+    const int fed = ((r + 1) % every) == 0;
+    if (fed) {
+      hipLaunchKernelGGL(dxcp_gather_kernel, dim3(P), dim3(256), 0, st, make_update(e, r), e->dUpEnd, e->y, e->zStream,
+                         e->zLen, e->T, e->Ns, e->dBase, e->ref, e->k0, nOwn, e->dxFrames);
+      (void)danse_dxcp_process(e->dx, e->dxFrames, e->dxOut, st);
+    }
+    hipLaunchKernelGGL(dxcp_round_kernel, dim3((P + 63) / 64), dim3(64), 0, st, e->S, e->K, e->k0, nOwn, r, e->R, fed,
+                       e->cdComp, (double)e->Ns, e->dxOut, e->dxEst, e->cdPhase, e->cdEst, e->cdRes);
   }
 }
 
@@ -903,7 +1002,7 @@ int danse_engine_gate_verdicts(danse_engine* eng, int32_t* verdict, void* stream
 int danse_engine_sro_estimates(danse_engine* eng, double* est, double* res) {
   if (!eng || !est || !res) return fail(eng, "null argument");
   const size_t n = (size_t)eng->S * eng->K * eng->R * (eng->K - 1);
-  if (!eng->cohDrift) {
+  if (!eng->cohDrift && !eng->dxcpOn) {
     std::fill(est, est + n, 0.0);
     std::fill(res, res + n, 0.0);
     return 0;

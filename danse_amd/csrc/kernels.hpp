@@ -20,7 +20,7 @@
 #pragma once
 #include "common.hpp"
 #include "solver.hpp"
-#include "../../include/danse_mi355x.h"
+#include "../../include/danse_mi355x_defs.h"
 
 namespace danse {
 

@@ -1,0 +1,417 @@
+// Synthetic acoustic scenes on the device (the input
+// producer of the E battery's 4096 scenes), the random-IR / random-signal
+// path of siggen (trueRoom false, signalType random; siggen/utils.py
+// build_wasn 1155-1411, resample_for_sro 1579-1622, apply_self_noise
+// 1414-1431; siggen/classes.py random signals 32-64):
+//   sources: a uniform [-1, 1] desired signal with on/off pauses and one
+//            uniform noise source per scene;
+//   per sensor: random IRs uniform [-0.5, 0.5] (0.2 s), causal convolution
+//            of both sources (register-tiled direct convolution, LDS);
+//   SNR set at mic 0 of node 0 (one noise gain per scene);
+//   SRO: node k's signals resampled to fs (1 + SRO_k 1e-6) by a Kaiser-
+//            windowed sinc (the reference uses resampy, absent offline: this
+//            resampler is our own, parity unpinned), truncated / zero-padded
+//            to T as resample_for_sro;
+//   white self-noise per sensor at selfnoiseSNR against the sensor's clean
+//            (asynchronous) power; cleannoise carries the reference sensor's
+//            self-noise on every channel;
+//   energy VAD on the node's mic-0 wet speech (centred window, threshold
+//            max(x^2) / 10^(dB/10)).
+// Random numbers come from a counter-based hash (splitmix64) keyed by
+// (seed, stream, index): any scene or node can be regenerated on its own.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <string>
+#include <vector>
+
+#include "../../include/danse_mi355x.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(const std::string& m) {
+  g_err = m;
+  return 1;
+}
+
+#define GCHK(x)                                                                         \
+  do {                                                                                  \
+    hipError_t e_ = (x);                                                                \
+    if (e_ != hipSuccess) return fail(std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+constexpr int kThr = 256;
+
+__host__ __device__ inline unsigned long long mix64(unsigned long long z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+// uniform in [-1, 1) from (key, index)
+__host__ __device__ inline double urand(unsigned long long key, unsigned long long i) {
+  const unsigned long long r = mix64(key ^ mix64(i + 0x632BE59BD9B4E019ull));
+  return (double)(r >> 11) * (2.0 / 9007199254740992.0) - 1.0;
+}
+__host__ __device__ inline unsigned long long stream_key(unsigned long long seed, unsigned long long a,
+                                                         unsigned long long b, unsigned long long c) {
+  return mix64(mix64(mix64(seed) ^ (a * 0x9E3779B1ull)) ^ (b * 0x85EBCA77ull + c * 0xC2B2AE3Dull + 1));
+}
+// streams
+enum { kStDesired = 1, kStNoise = 2, kStIrS = 3, kStIrN = 4, kStSelf = 5 };
+
+struct SceneArgs {
+  int S, K, MT, T, nIR;
+  unsigned long long seed;
+  double fs, pauseDur, pauseSpacing;
+  const int* chanNode;    // [MT]
+  const int* chanMic;     // [MT]
+};
+
+// sources: d (pauses: zero where t mod (pause + spacing) >= spacing) and n
+__global__ void src_kernel(SceneArgs a, float* __restrict__ d, float* __restrict__ nz) {
+  const long long n = (long long)a.S * a.T;
+  const double period = a.pauseDur + a.pauseSpacing;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+    const int s = (int)(e / a.T);
+    const long long t = e % a.T;
+    const double tt = (double)t / a.fs;
+    const double dv = urand(stream_key(a.seed + s, kStDesired, 0, 0), t);
+    d[e] = (fmod(tt, period) >= a.pauseSpacing) ? 0.0f : (float)dv;
+    nz[e] = (float)urand(stream_key(a.seed + s, kStNoise, 0, 0), t);
+  }
+}
+
+// IRs [S][MT][2][nIR], uniform [-0.5, 0.5]
+__global__ void ir_kernel(SceneArgs a, float* __restrict__ ir) {
+  const long long n = (long long)a.S * a.MT * 2 * a.nIR;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+    const int j = (int)(e % a.nIR);
+    const int w = (int)((e / a.nIR) % 2);
+    const int c = (int)((e / (2LL * a.nIR)) % a.MT);
+    const int s = (int)(e / (2LL * a.nIR * a.MT));
+    ir[e] = (float)(0.5 * urand(stream_key(a.seed + s, w ? kStIrN : kStIrS, a.chanNode[c], a.chanMic[c]), j));
+  }
+}
+
+// Causal convolution out[t] = sum_j h[j] x[t - j] (t < T) for every (scene,
+// channel, source): one workgroup per 2048 outputs of one row; the input
+// segment and the IR in LDS (chunks of kConvTap taps); each thread keeps 8
+// consecutive outputs and slides the input window through registers
+// (8 FMA per LDS read of the input, the IR read is a broadcast).
+constexpr int kConvOut = 2048, kConvPer = 8, kConvTap = 1024;
+__global__ void __launch_bounds__(kThr) conv_kernel(SceneArgs a, const float* __restrict__ d,
+                                                    const float* __restrict__ nz, const float* __restrict__ ir,
+                                                    float* __restrict__ wS, float* __restrict__ wN) {
+  __shared__ float xs[kConvOut + kConvTap];
+  __shared__ float hs[kConvTap];
+  const int nBlk = (a.T + kConvOut - 1) / kConvOut;
+  const int blk = blockIdx.x % nBlk;
+  const long long row = blockIdx.x / nBlk;     // (s, c, w)
+  const int w = (int)(row % 2);
+  const int c = (int)((row / 2) % a.MT);
+  const int s = (int)(row / (2LL * a.MT));
+  const float* x = (w ? nz : d) + (long long)s * a.T;
+  const float* h = ir + (((long long)s * a.MT + c) * 2 + w) * a.nIR;
+  const int t0 = blk * kConvOut;
+  const int tb = t0 + threadIdx.x * kConvPer;   // this thread's first output
+  float acc[kConvPer];
+#pragma unroll
+  for (int i = 0; i < kConvPer; ++i) acc[i] = 0.0f;
+  for (int j0 = 0; j0 < a.nIR; j0 += kConvTap) {
+    const int nj = min(kConvTap, a.nIR - j0);
+    __syncthreads();
+    // inputs x[t0 - j0 - nj + 1 .. t0 - j0 + kConvOut) -> xs[0 .. kConvOut + nj - 1)
+    const int base = t0 - j0 - nj + 1;
+    for (int i = threadIdx.x; i < kConvOut + nj - 1; i += kThr) {
+      const int idx = base + i;
+      xs[i] = (idx >= 0 && idx < a.T) ? x[idx] : 0.0f;
+    }
+    for (int i = threadIdx.x; i < nj; i += kThr) hs[i] = h[j0 + i];
+    __syncthreads();
+    // out[tb + i] += sum_jj hs[jj] x[tb + i - j0 - jj], x[q] = xs[q - base]
+    const int o = tb - j0 - base;   // xs index of x[tb - j0]
+    float win[kConvPer];
+#pragma unroll
+    for (int i = 0; i < kConvPer; ++i) win[i] = xs[o + i];
+#pragma unroll 8
+    for (int jj = 0; jj < nj; ++jj) {
+      const float hv = hs[jj];
+#pragma unroll
+      for (int i = 0; i < kConvPer; ++i) acc[i] = fmaf(hv, win[i], acc[i]);
+      // slide: next tap reads x one sample earlier
+#pragma unroll
+      for (int i = kConvPer - 1; i > 0; --i) win[i] = win[i - 1];
+      win[0] = (jj + 1 < nj) ? xs[o - jj - 1] : 0.0f;
+    }
+  }
+  float* out = (w ? wN : wS) + ((long long)s * a.MT + c) * a.T;
+#pragma unroll
+  for (int i = 0; i < kConvPer; ++i)
+    if (tb + i < a.T) out[tb + i] = acc[i];
+}
+
+// Kaiser-windowed sinc resampling of one row to the node's rate fs (1 + eps):
+// y[n] = x(n / (1 + eps)), half-width kHalf input samples, cutoff
+// min(1, 1 + eps) * kRoll; zero past ceil(T (1 + eps)) (resample_for_sro pads)
+constexpr int kHalf = 32;
+constexpr double kRoll = 0.95, kBeta = 8.0;
+__device__ double bessel_i0(double x) {
+  double s = 1.0, t = 1.0;
+  for (int k = 1; k < 40; ++k) {
+    t *= (x / (2.0 * k)) * (x / (2.0 * k));
+    s += t;
+  }
+  return s;
+}
+__global__ void resample_kernel(const float* __restrict__ x, int rows, int T, const double* __restrict__ epsRow,
+                                float* __restrict__ y) {
+  const long long n = (long long)rows * T;
+  const double i0b = bessel_i0(kBeta);
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+    const int r = (int)(e / T);
+    const long long t = e % T;
+    const double eps = epsRow[r];
+    const float* xr = x + (long long)r * T;
+    if (eps == 0.0) {
+      y[e] = xr[t];
+      continue;
+    }
+    const long long outLen = (long long)ceil((double)T * (1.0 + eps));
+    if (t >= outLen) {
+      y[e] = 0.0f;
+      continue;
+    }
+    const double p = (double)t / (1.0 + eps);
+    const double fc = fmin(1.0, 1.0 + eps) * kRoll;
+    const long long i0 = (long long)floor(p);
+    double acc = 0.0;
+    for (long long i = i0 - kHalf + 1; i <= i0 + kHalf; ++i) {
+      if (i < 0 || i >= T) continue;
+      const double u = p - (double)i;
+      const double r2 = u / (double)kHalf;
+      if (fabs(r2) >= 1.0) continue;
+      const double a = M_PI * fc * u;
+      const double sinc = (u == 0.0) ? 1.0 : sin(a) / a;
+      acc += (double)xr[i] * fc * sinc * bessel_i0(kBeta * sqrt(1.0 - r2 * r2)) / i0b;
+    }
+    y[e] = (float)acc;
+  }
+}
+
+// mean of x^2 over each row, in double (fixed order: per-thread partials, tree)
+__global__ void __launch_bounds__(kThr) power_kernel(const float* __restrict__ x, int T, double* __restrict__ out) {
+  __shared__ double red[kThr];
+  const float* r = x + (long long)blockIdx.x * T;
+  double a = 0.0;
+  for (int t = threadIdx.x; t < T; t += kThr) a += (double)r[t] * (double)r[t];
+  red[threadIdx.x] = a;
+  __syncthreads();
+  for (int w = kThr / 2; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[blockIdx.x] = red[0] / (double)T;
+}
+
+// max of x^2 over node k's mic-0 row (row s * MT + base[k]); grid S * K
+__global__ void __launch_bounds__(kThr) max_sq_kernel(const float* __restrict__ x, int T, int K, int MT,
+                                                      const int* __restrict__ base, double* __restrict__ out) {
+  __shared__ double red[kThr];
+  const int s = blockIdx.x / K, k = blockIdx.x % K;
+  const float* r = x + ((long long)s * MT + base[k]) * T;
+  double a = 0.0;
+  for (int t = threadIdx.x; t < T; t += kThr) a = fmax(a, (double)r[t] * (double)r[t]);
+  red[threadIdx.x] = a;
+  __syncthreads();
+  for (int w = kThr / 2; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + w]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[blockIdx.x] = red[0];
+}
+
+// clean = wS + gN wN (asynchronous); self-noise scaled against the clean
+// power; data = clean + sn; cleanspeech = wS; cleannoise = gN wN + sn of the
+// node's reference (mic 0) sensor.  gains: [S][MT] self-noise gain, gN [S].
+__global__ void mix_kernel(SceneArgs a, const float* __restrict__ wS, const float* __restrict__ wN,
+                           const double* __restrict__ gN, const double* __restrict__ gSelf,
+                           const int* __restrict__ base, float* __restrict__ data, float* __restrict__ cs,
+                           float* __restrict__ cn) {
+  const long long n = (long long)a.S * a.MT * a.T;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+    const long long t = e % a.T;
+    const int c = (int)((e / a.T) % a.MT);
+    const int s = (int)(e / ((long long)a.T * a.MT));
+    const int k = a.chanNode[c];
+    const int c0 = base[k];
+    const double g = gN[s];
+    const double clean = (double)wS[e] + g * (double)wN[e];
+    const double sn = gSelf[(long long)s * a.MT + c] * urand(stream_key(a.seed + s, kStSelf, k, a.chanMic[c]), t);
+    const double sn0 = gSelf[(long long)s * a.MT + c0] * urand(stream_key(a.seed + s, kStSelf, k, 0), t);
+    data[e] = (float)(clean + sn);
+    cs[e] = wS[e];
+    cn[e] = (float)(g * (double)wN[e] + sn0);
+  }
+}
+
+// energy VAD of node k's mic-0 wet speech: window of nw samples centred on
+// each sample, [i - nw/2, i + nw/2) clipped, energy > max(x^2) / 10^(dB/10)
+__global__ void vad_kernel(const float* __restrict__ wS, int S, int K, int MT, int T, const int* __restrict__ base,
+                           int nw, double dB, const double* __restrict__ maxSq, uint8_t* __restrict__ vad) {
+  const long long n = (long long)S * K * T;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+    const long long i = e % T;
+    const int k = (int)((e / T) % K);
+    const int s = (int)(e / ((long long)T * K));
+    const float* x = wS + ((long long)s * MT + base[k]) * T;
+    const long long b = max(i - nw / 2, 0LL), en = min(i + nw / 2, (long long)T);
+    double acc = 0.0;
+    for (long long j = b; j < en; ++j) acc += (double)x[j] * (double)x[j];
+    vad[e] = acc > maxSq[(long long)s * K + k] / pow(10.0, dB / 10.0) ? 1 : 0;
+  }
+}
+
+__global__ void gain_kernel(const double* __restrict__ Ps, const double* __restrict__ Pn, int S, int MT, double snr,
+                            double* __restrict__ gN) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= S) return;
+  // SNR at mic 0 of node 0 (single noise source), unresampled signals
+  const double ps = Ps[(long long)s * MT], pn = Pn[(long long)s * MT];
+  gN[s] = pow(10.0, -(snr - 10.0 * log10(ps / pn)) / 20.0);
+}
+
+// self-noise gain 10^(-(snr - 10 log10(Pc / Psn)) / 20) with Psn the mean of
+// the uniform draws squared (computed exactly on the host side: 1/3 in
+// expectation; here the empirical mean of this row's draws)
+__global__ void __launch_bounds__(kThr) self_gain_kernel(SceneArgs a, const float* __restrict__ wS,
+                                                         const float* __restrict__ wN, const double* __restrict__ gN,
+                                                         double selfSnr, double* __restrict__ gSelf) {
+  __shared__ double rc[kThr], rn[kThr];
+  const long long row = blockIdx.x;   // (s, c)
+  const int c = (int)(row % a.MT);
+  const int s = (int)(row / a.MT);
+  const int k = a.chanNode[c];
+  const double g = gN[s];
+  const unsigned long long key = stream_key(a.seed + s, kStSelf, k, a.chanMic[c]);
+  double pc = 0.0, pn = 0.0;
+  for (int t = threadIdx.x; t < a.T; t += kThr) {
+    const double cl = (double)wS[row * a.T + t] + g * (double)wN[row * a.T + t];
+    const double u = urand(key, t);
+    pc += cl * cl;
+    pn += u * u;
+  }
+  rc[threadIdx.x] = pc;
+  rn[threadIdx.x] = pn;
+  __syncthreads();
+  for (int w = kThr / 2; w > 0; w >>= 1) {
+    if (threadIdx.x < w) {
+      rc[threadIdx.x] += rc[threadIdx.x + w];
+      rn[threadIdx.x] += rn[threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) gSelf[row] = pow(10.0, -(selfSnr - 10.0 * log10(rc[0] / rn[0])) / 20.0);
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* danse_scene_last_error(void) { return g_err.c_str(); }
+
+int danse_scene_generate(const danse_scene_cfg* c, float* data, float* cleanspeech, float* cleannoise, uint8_t* vad,
+                         void* stream) {
+  if (!c || !data || !cleanspeech || !cleannoise || !vad) return fail("null argument");
+  if (c->S < 1 || c->K < 1 || c->T < 1 || c->nIR < 1 || !c->M) return fail("bad sizes");
+  hipStream_t st = (hipStream_t)stream;
+  const int S = c->S, K = c->K, T = c->T;
+  std::vector<int> chanNode, chanMic, base(K);
+  for (int k = 0; k < K; ++k) {
+    base[k] = (int)chanNode.size();
+    for (int m = 0; m < c->M[k]; ++m) {
+      chanNode.push_back(k);
+      chanMic.push_back(m);
+    }
+  }
+  const int MT = (int)chanNode.size();
+  std::vector<double> epsRow((size_t)S * MT * 2);
+  for (int s = 0; s < S; ++s)
+    for (int ch = 0; ch < MT; ++ch)
+      for (int w = 0; w < 2; ++w) epsRow[((size_t)s * MT + ch) * 2 + w] = c->sroPpm ? c->sroPpm[chanNode[ch]] * 1e-6 : 0.0;
+  std::vector<void*> owned;
+  auto cleanup = [&]() {
+    for (void* p : owned) (void)hipFree(p);
+  };
+  auto alloc = [&](void** p, size_t bytes) -> bool {
+    if (hipMalloc(p, bytes < 8 ? 8 : bytes) != hipSuccess) return false;
+    owned.push_back(*p);
+    return true;
+  };
+  int *dNode = nullptr, *dMic = nullptr, *dBase = nullptr;
+  float *d = nullptr, *nz = nullptr, *ir = nullptr, *wsw = nullptr, *wsr = nullptr;
+  double *dEps = nullptr, *Ps = nullptr, *gN = nullptr, *gSelf = nullptr, *mx = nullptr;
+  const size_t rowT = (size_t)T * sizeof(float);
+  if (!alloc((void**)&dNode, MT * sizeof(int)) || !alloc((void**)&dMic, MT * sizeof(int)) ||
+      !alloc((void**)&dBase, K * sizeof(int)) || !alloc((void**)&d, (size_t)S * rowT) ||
+      !alloc((void**)&nz, (size_t)S * rowT) || !alloc((void**)&ir, (size_t)S * MT * 2 * c->nIR * sizeof(float)) ||
+      !alloc((void**)&wsw, (size_t)S * MT * 2 * rowT) || !alloc((void**)&wsr, (size_t)S * MT * 2 * rowT) ||
+      !alloc((void**)&dEps, epsRow.size() * sizeof(double)) || !alloc((void**)&Ps, (size_t)S * MT * 2 * sizeof(double)) ||
+      !alloc((void**)&gN, (size_t)S * sizeof(double)) || !alloc((void**)&gSelf, (size_t)S * MT * sizeof(double)) ||
+      !alloc((void**)&mx, (size_t)S * K * sizeof(double))) {
+    cleanup();
+    return fail("scene: device allocation failed");
+  }
+  if (hipMemcpyAsync(dNode, chanNode.data(), MT * sizeof(int), hipMemcpyHostToDevice, st) != hipSuccess ||
+      hipMemcpyAsync(dMic, chanMic.data(), MT * sizeof(int), hipMemcpyHostToDevice, st) != hipSuccess ||
+      hipMemcpyAsync(dBase, base.data(), K * sizeof(int), hipMemcpyHostToDevice, st) != hipSuccess ||
+      hipMemcpyAsync(dEps, epsRow.data(), epsRow.size() * sizeof(double), hipMemcpyHostToDevice, st) != hipSuccess) {
+    cleanup();
+    return fail("scene: upload failed");
+  }
+  SceneArgs a{};
+  a.S = S; a.K = K; a.MT = MT; a.T = T; a.nIR = c->nIR; a.seed = (unsigned long long)c->seed;
+  a.fs = c->fs; a.pauseDur = c->pauseDuration; a.pauseSpacing = c->pauseSpacing;
+  a.chanNode = dNode; a.chanMic = dMic;
+  auto grid = [](long long n) { return dim3((unsigned)std::min<long long>((n + kThr - 1) / kThr, 1 << 20)); };
+  hipLaunchKernelGGL(src_kernel, grid((long long)S * T), dim3(kThr), 0, st, a, d, nz);
+  hipLaunchKernelGGL(ir_kernel, grid((long long)S * MT * 2 * c->nIR), dim3(kThr), 0, st, a, ir);
+  // wet signals: rows (s, c, w) of wsw = [S][MT][2][T] interleaved as (wS, wN) per channel
+  float* wS = wsw;                                   // [S][MT][T]
+  float* wN = wsw + (size_t)S * MT * T;              // [S][MT][T]
+  {
+    const int nBlk = (T + kConvOut - 1) / kConvOut;
+    hipLaunchKernelGGL(conv_kernel, dim3((unsigned)((long long)S * MT * 2 * nBlk)), dim3(kThr), 0, st, a, d, nz, ir, wS,
+                       wN);
+  }
+  // noise gain from the synchronous mic-0 powers of node 0
+  hipLaunchKernelGGL(power_kernel, dim3(S * MT), dim3(kThr), 0, st, wS, T, Ps);
+  hipLaunchKernelGGL(power_kernel, dim3(S * MT), dim3(kThr), 0, st, wN, T, Ps + (size_t)S * MT);
+  hipLaunchKernelGGL(gain_kernel, dim3((S + 63) / 64), dim3(64), 0, st, Ps, Ps + (size_t)S * MT, S, MT, c->snr, gN);
+  // VAD from the synchronous wet speech at each node's mic 0
+  hipLaunchKernelGGL(max_sq_kernel, dim3(S * K), dim3(kThr), 0, st, wS, T, K, MT, dBase, mx);
+  {
+    const int nw = std::max((int)(c->vadWinLength * c->fs), 1);
+    hipLaunchKernelGGL(vad_kernel, grid((long long)S * K * T), dim3(kThr), 0, st, wS, S, K, MT, T, dBase, nw,
+                       c->vadEnergyDecrease_dB, mx, vad);
+  }
+  // SRO resampling of wS and wN per node (rows of both halves)
+  float* rS = wsr;
+  float* rN = wsr + (size_t)S * MT * T;
+  hipLaunchKernelGGL(resample_kernel, grid((long long)S * MT * T), dim3(kThr), 0, st, wS, S * MT, T, dEps, rS);
+  hipLaunchKernelGGL(resample_kernel, grid((long long)S * MT * T), dim3(kThr), 0, st, wN, S * MT, T, dEps, rN);
+  hipLaunchKernelGGL(self_gain_kernel, dim3(S * MT), dim3(kThr), 0, st, a, rS, rN, gN, c->selfnoiseSNR, gSelf);
+  hipLaunchKernelGGL(mix_kernel, grid((long long)S * MT * T), dim3(kThr), 0, st, a, rS, rN, gN, gSelf, dBase, data,
+                     cleanspeech, cleannoise);
+  const hipError_t le = hipGetLastError();
+  const hipError_t se = hipStreamSynchronize(st);
+  cleanup();
+  if (le != hipSuccess) return fail(std::string("scene launch: ") + hipGetErrorString(le));
+  if (se != hipSuccess) return fail(std::string("scene: ") + hipGetErrorString(se));
+  return 0;
+}
+
+}  // extern "C"

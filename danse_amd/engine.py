@@ -119,7 +119,7 @@ class DanseEngine:
     """
 
     def __init__(self, scenes, p, vadMinProp=0.5, device=0, keepHistory=True, nodeRange=None,
-                 pregiven=None, yin='data'):
+                 pregiven=None, yin='data', yDevice=None):
         import torch
         self.torch = torch
         self.lib = L.load_library()
@@ -132,9 +132,11 @@ class DanseEngine:
         self.Mtot = int(sum(self.M))
         self.N, self.Ns = p.DFTsize, p.Ns
         self.F = self.N // 2 + 1
-        self.T = sc0.wasn[0].data.shape[0]
+        # the scene signals may live on the device only (yDevice, e.g.
+        # scene.make_scenes_device): the length comes from the time stamps
+        self.T = len(sc0.wasn[0].timeStamps)
         for sc in self.scenes:
-            if sc.nNodes != K or [n.nSensors for n in sc.wasn] != self.M or sc.wasn[0].data.shape[0] != self.T:
+            if sc.nNodes != K or [n.nSensors for n in sc.wasn] != self.M or len(sc.wasn[0].timeStamps) != self.T:
                 raise ValueError('all scenes of one engine must share the WASN shape')
             if any(not np.array_equal(n.timeStamps, m.timeStamps) for n, m in zip(sc.wasn, sc0.wasn)):
                 raise ValueError('all scenes of one engine must share the node clocks')
@@ -207,12 +209,17 @@ class DanseEngine:
         self._build_flags()
         self._build_cfg()
         # inputs [S][Mtot][T] float32 on the device
-        y = np.empty((S, self.Mtot, self.T), dtype=np.float32)
-        for s, sc in enumerate(self.scenes):
-            for k, nd in enumerate(sc.wasn):
-                arr = getattr(nd, yin)
-                y[s, base[k]:base[k] + self.M[k], :] = arr.T
-        self.y = torch.from_numpy(y).to(f'cuda:{device}')
+        if yDevice is not None:
+            if tuple(yDevice.shape) != (S, self.Mtot, self.T) or yDevice.dtype != torch.float32 or not yDevice.is_cuda:
+                raise ValueError('yDevice must be a float32 device tensor [S][sum M][T]')
+            self.y = yDevice.contiguous()
+        else:
+            y = np.empty((S, self.Mtot, self.T), dtype=np.float32)
+            for s, sc in enumerate(self.scenes):
+                for k, nd in enumerate(sc.wasn):
+                    arr = getattr(nd, yin)
+                    y[s, base[k]:base[k] + self.M[k], :] = arr.T
+            self.y = torch.from_numpy(y).to(f'cuda:{device}')
         L.check(self.lib.danse_engine_set_inputs(self.eng, ctypes.c_void_p(self.y.data_ptr())), self.eng)
         if pregiven is not None:
             self._load_pregiven(pregiven)
@@ -246,14 +253,29 @@ class DanseEngine:
                       else np.ascontiguousarray(self.rt.zLag[:R], dtype=np.uint8))
         self._zPhase = None
         self.cohDrift = p.estimateSROs == 'CohDrift'
-        if self.cohDrift:
+        self.dxcp = p.estimateSROs == 'DXCPPhaT'
+        if self.dxcp:
+            # the build's extension (the reference raises here, d_classes.py:
+            # 2469-2481, quirk Q12): device DXCP-PhaT estimators per (receiver,
+            # sender) feed the phase compensation (danse_cfg.dxcp)
+            if self.fewSamples:
+                raise NotImplementedError('DXCP-PhaT SRO estimation runs on wholeChunk broadcasts')
+            if any(n.fs and abs(n.fs / (1 + n.sro * 1e-6) - 16000.0) > 1e-6 for n in sc0.wasn) or self.N != 1024 \
+                    or 2048 % self.Ns:
+                raise NotImplementedError('DXCP-PhaT (default parameters) needs 16 kHz, N = 1024 and Ns dividing 2048')
+            if (self.k0, self.k1) != (0, K):
+                raise NotImplementedError('DXCP-PhaT estimation on a node-sharded engine (the z streams are not '
+                                          'exchanged)')
+            if p.computeCentralised and p.compensateSROs:
+                raise NotImplementedError('centralised estimates with DXCP-PhaT SRO estimation')
+        elif self.cohDrift:
             cd = p.cohDrift
             if cd.loop != 'closed' or cd.estimationMethod != 'ls':
                 raise NotImplementedError("CohDrift on the device path: closed loop, estimationMethod 'ls'")
             if 'asy' not in p.nodeUpdating or self.fewSamples or p.computeCentralised:
                 raise NotImplementedError('CohDrift on the device path: asy node updating, wholeChunk, no centralised')
         elif p.estimateSROs != 'Oracle':
-            raise NotImplementedError(f'estimateSROs={p.estimateSROs!r} (the reference raises for DXCP-PhaT in DANSE)')
+            raise ValueError(f'estimateSROs={p.estimateSROs!r}')
         if not p.compensateSROs:
             return
         sro = np.array([nd.sro for nd in sc0.wasn], dtype=np.float64)
@@ -266,7 +288,7 @@ class DanseEngine:
             nb = [q for q in range(K) if q != k]
             # CohDrift: the estimates accumulate on the device (cohdrift.hpp);
             # the table keeps the full-sample-drift flags only
-            est = np.zeros(len(nb)) if self.cohDrift else (sro[nb] - sro[k]) * 1e-6
+            est = np.zeros(len(nb)) if (self.cohDrift or self.dxcp) else (sro[nb] - sro[k]) * 1e-6
             for r in range(R):
                 if p.includeFSDflags:
                     phi[nb] += self.rt.flags[r, k, nb]
@@ -508,6 +530,9 @@ class DanseEngine:
             c.cdCompensate = int(bool(p.compensateSROs))
             c.cdNIter = int(self.nIter)
             c.cdAlpha, c.cdAlphaEps = float(cd.alpha), float(cd.alphaEps)
+        if self.dxcp:
+            c.dxcp = 1
+            c.cdCompensate = int(bool(p.compensateSROs))
         c.cEnd = _ptr(self._cEnd, ctypes.c_int32)
         c.cPhase = _ptr(self._cPhase, ctypes.c_double)
         c.zStreamLen = int(self.rt.zStreamLen) if self.fewSamples else 0
@@ -845,7 +870,7 @@ class DanseEngine:
         Yh = Yh[..., 0].astype(np.float64) + 1j * Yh[..., 1].astype(np.float64)
         solveFlags = (self.flags[:, :, L.FAM_DANSE, :] & L.FLAG_SOLVE) != 0     # [R][S][K]
         neighbors0 = [list(n.neighborsIdx) for n in self.scenes[0].wasn]
-        if self.cohDrift:
+        if self.cohDrift or self.dxcp:
             cdE = np.zeros((S, K, self.R, K - 1))
             cdR = np.zeros((S, K, self.R, K - 1))
             L.check(self.lib.danse_engine_sro_estimates(self.eng, _ptr(cdE, ctypes.c_double),
@@ -859,7 +884,7 @@ class DanseEngine:
             for nm, v in host_fields(p, [n.sro for n in self.scenes[s].wasn], neighbors0, self.rt, nI, nseg,
                                      fsr).items():
                 setattr(r, nm, v)
-            if self.cohDrift:
+            if self.cohDrift or self.dxcp:
                 r.SROsEstimates = [np.zeros((nI, K - 1)) for _ in range(K)]
                 r.SROsResiduals = [np.zeros((nI, K - 1)) for _ in range(K)]
                 for k in range(K):

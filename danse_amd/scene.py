@@ -197,3 +197,60 @@ def scene_digest(scene: Scene) -> str:
         h.update(node.data.astype(np.float32).tobytes())
         h.update(node.vad.astype(np.uint8).tobytes())
     return h.hexdigest()
+
+
+def make_scenes_device(nSensorPerNode, S, sigDur=10.0, fs=16000.0, seed=0, snr=5.0, selfnoiseSNR=15.0,
+                       irDuration=0.2, pauseDuration=0.5, pauseSpacing=0.5, vadEnergyDecrease_dB=40.0,
+                       vadWinLength=0.04, SROperNode=None, device=0, host_signals=False):
+    """S random-IR scenes generated on the device (``danse_scene_generate``,
+    csrc/scene.hip): the same scene model as :func:`make_scene`, with its own
+    counter-based random numbers (scene s from ``seed + s``) and the SRO
+    resampling that :func:`make_scene` omits (node k's signals at
+    fs (1 + SRO_k 1e-6); our Kaiser-windowed sinc, the reference uses
+    resampy).  Returns ``(scenes, dev)``: Scene objects whose nodes carry the
+    time stamps, VAD and -- with ``host_signals`` -- the signals as float32
+    host arrays, and ``dev`` = dict of device tensors ``data``,
+    ``cleanspeech``, ``cleannoise`` [S][sum M][T] float32 and ``vad``
+    [S][K][T] uint8 (``DanseEngine(..., yDevice=dev['data'])`` takes the
+    inputs without a host round trip)."""
+    import ctypes
+    import torch
+    from . import _lib as L
+    lib = L.load_library()
+    M = [int(m) for m in nSensorPerNode]
+    K, MT, T = len(M), int(sum(M)), int(sigDur * fs)
+    dev = f'cuda:{device}'
+    out = {key: torch.empty((S, MT, T), dtype=torch.float32, device=dev) for key in ('data', 'cleanspeech', 'cleannoise')}
+    out['vad'] = torch.empty((S, K, T), dtype=torch.uint8, device=dev)
+    sros = np.zeros(K) if SROperNode is None else np.asarray(SROperNode, dtype=np.float64)
+    Marr = np.asarray(M, dtype=np.int32)
+    sroArr = np.ascontiguousarray(sros, dtype=np.float64)
+    c = L.SceneCfg()
+    c.S, c.K, c.M, c.T, c.nIR, c.seed = S, K, Marr.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), T, \
+        int(irDuration * fs), int(seed)
+    c.fs, c.snr, c.selfnoiseSNR = float(fs), float(snr), float(selfnoiseSNR)
+    c.pauseDuration, c.pauseSpacing = float(pauseDuration), float(pauseSpacing)
+    c.vadEnergyDecrease_dB, c.vadWinLength = float(vadEnergyDecrease_dB), float(vadWinLength)
+    c.sroPpm = sroArr.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+    st = ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+    rc = lib.danse_scene_generate(ctypes.byref(c), ctypes.c_void_p(out['data'].data_ptr()),
+                                  ctypes.c_void_p(out['cleanspeech'].data_ptr()),
+                                  ctypes.c_void_p(out['cleannoise'].data_ptr()), ctypes.c_void_p(out['vad'].data_ptr()),
+                                  st)
+    if rc != 0:
+        raise L.DanseError((lib.danse_scene_last_error() or b'').decode() or f'error {rc}')
+    vad = out['vad'].cpu().numpy()
+    host = {key: out[key].cpu().numpy() for key in ('data', 'cleanspeech', 'cleannoise')} if host_signals else None
+    base = np.concatenate(([0], np.cumsum(M)[:-1])).astype(int)
+    scenes = []
+    for s in range(S):
+        wasn = []
+        for k in range(K):
+            fsSRO = fs * (1 + sros[k] / 1e6)
+            sl = slice(base[k], base[k] + M[k])
+            sig = {key: (host[key][s, sl].T if host is not None else None) for key in ('data', 'cleanspeech', 'cleannoise')}
+            wasn.append(SceneNode(index=k, nSensors=M[k], fs=fsSRO, timeStamps=np.arange(T) / fsSRO,
+                                  neighborsIdx=[q for q in range(K) if q != k], sro=float(sros[k]),
+                                  vad=vad[s, k][:, None], **sig))
+        scenes.append(Scene(wasn=wasn, fs=fs, seed=seed + s))
+    return scenes, out

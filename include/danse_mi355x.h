@@ -31,44 +31,7 @@
 extern "C" {
 #endif
 
-#define DANSE_MAX_FAMILIES 4   /* DANSE, local, centralised, single-sensor broadcast */
-
-enum danse_family {
-  DANSE_FAM_DANSE = 0,   /* wTilde / d / dhat                 d_classes.py:2290-2320 */
-  DANSE_FAM_LOCAL = 1,   /* wLocal / dLocal                   d_classes.py:2339-2350 */
-  DANSE_FAM_CENTR = 2,   /* wCentr / dCentr                   d_classes.py:2321-2338 */
-  DANSE_FAM_SSBC = 3     /* wSSBC / dSSBC                     d_classes.py:2351-2362 */
-};
-
-/* Per-round, per-(scene, family, node) control byte (host-computed schedule).
- * bits 0-1: Ryy op   bits 2-3: Rnn op   (0 keep, 1 set to yy^H, 2 exp. average)
- *           (spatial_covariance_matrix_update + conditional_scm_updating,
- *            d_classes.py:2048-2267)
- * bit 4   : solve (filter update: not bypassed and gate passed,
- *           d_classes.py:1298-1313 / 2290-2362); else w[i+1] = w[i]
- * bit 5   : refresh the asy external-filter target (timeBtwExternalFiltUpdates,
- *           d_classes.py:1680-1694)                                         */
-#define DANSE_OP_KEEP 0
-#define DANSE_OP_SET 1
-#define DANSE_OP_AVG 2
-#define DANSE_FLAG_SOLVE 0x10
-#define DANSE_FLAG_EXT_TARGET 0x20
-#define DANSE_FLAG_PREGIVEN 0x40   /* w[i+1], wExt[i+1] pre-loaded (danse_engine_put):
-                                      update_using_pregiven_filters, d_classes.py:1338-1352 */
-#define DANSE_FLAG_INITSLOT 0x80   /* the family-node has not started updating: its filter
-                                      for this round is the (pre-loaded) init slot w[i+1]
-                                      (perform_update leaves wTilde[:, i+1] untouched,
-                                      d_classes.py:2290-2362; differs from w[i] only for
-                                      filterInitType 'random') */
-
-/* External-filter update mode per node (update_external_filters,
- * d_classes.py:1627-1694). */
-enum danse_ext_mode {
-  DANSE_EXT_COPY = 0,    /* seq or noExternalFilterRelaxation: wExt[i+1] = w[i+1][:M]     */
-  DANSE_EXT_RELAX = 1,   /* asy/sim: wExt[i+1] = b wExt[i] + (1-b) target; target update */
-  DANSE_EXT_KEEP = 2,    /* noFusionAtSingleSensorNodes and M_k == 1                      */
-  DANSE_EXT_REFONLY = 3  /* onlyBroadcastRefSensorSigs                                    */
-};
+#include "danse_mi355x_defs.h"
 
 typedef struct danse_cfg {
   /* sizes */
@@ -154,19 +117,17 @@ typedef struct danse_cfg {
                                channel c at node k's update r (phaseShiftFactors-
                                Centr, compensate_sros d_classes.py:1996-2038 and
                                update_sro_estimates 2364-2621); NULL = none     */
+  /* DXCP-PhaT SRO estimation in the loop (estimateSROs 'DXCPPhaT'; the
+   * reference's own integration raises, d_classes.py:2469-2481, quirk Q12:
+   * this is an extension).  One DXCP-PhaT estimator (sro_estimation.py:
+   * 130-345, default parameters) per (scene, receiver k, sender q), fed every
+   * 2048 / Ns rounds with the 2048 newest samples of k's reference sensor
+   * (ending at upEnd[r][k]) and of q's fused-signal stream as k received it;
+   * eps_kq = -(SRO ppm) 1e-6 replaces the Oracle estimate: with
+   * cdCompensate the sender's phase loses eps Ns after every update.
+   * wholeChunk broadcasts; exclusive with cohDrift.  0 = off.             */
+  int32_t dxcp;
 } danse_cfg;
-
-/* Fields of one fsTab entry (round r, node k). */
-enum danse_fs_field {
-  DANSE_FS_BCEND = 0,   /* broadcast frame end floor(t fs) of node k's broadcast in round r */
-  DANSE_FS_LEN = 1,     /* currL: samples appended to node k's stream (0: none)             */
-  DANSE_FS_POS = 2,     /* stream position of that chunk                                    */
-  DANSE_FS_IRSRC = 3,   /* >= 0: refresh the T(z) IR from wExt iteration IRSRC first
-                           (upTDfilterEvery timer); -1: keep the current IR                 */
-  DANSE_FS_ZEND = 4,    /* node k's stream length the receivers' round-r z frame ends at
-                           (their frame = stream[ZEND - N, ZEND), zero before 0)            */
-  DANSE_FS_FIELDS = 5
-};
 
 typedef struct danse_engine danse_engine;
 
@@ -383,6 +344,8 @@ int danse_dxcp_create(int32_t P, int device, danse_dxcp** out);
 void danse_dxcp_destroy(danse_dxcp* eng);
 const char* danse_dxcp_last_error(const danse_dxcp* eng);
 int danse_dxcp_process(danse_dxcp* eng, const float* x, double* out, void* stream);
+/* Every pair back to its initial state (asynchronous on `stream`).         */
+int danse_dxcp_reset(danse_dxcp* eng, void* stream);
 /* process_data(x_12_ell, tdoa): as danse_dxcp_process, with the STO
  * estimate corrected by tdoa[p] * 16000 samples when its maximum is interior
  * (sro_estimation.py:338-339).  tdoa: [P] double (device) or NULL.        */
@@ -401,6 +364,32 @@ int danse_dxcp_process_tdoa(danse_dxcp* eng, const float* x, const double* tdoa,
  *        (from two calls earlier)                                          */
 int danse_cl_dxcp_create(int32_t P, int32_t startDelay, int device, danse_dxcp** out);
 int danse_cl_dxcp_process(danse_dxcp* eng, const float* x, const int32_t* acs, double* out, float* zi, void* stream);
+
+/* ---- Synthetic scenes on the device (csrc/scene.hip):
+ * the random-IR / random-signal path of siggen (build_wasn, siggen/utils.py:
+ * 1155-1411, trueRoom false, signalType random) for S scenes at once --
+ * paused uniform desired source and uniform noise source per scene, uniform
+ * random IRs per sensor (causal convolution), noise gain for `snr` at mic 0
+ * of node 0, per-node SRO resampling to fs (1 + sroPpm 1e-6) by a Kaiser-
+ * windowed sinc (resample_for_sro, utils.py:1579-1622, uses resampy, absent
+ * offline: parity unpinned), sensor self-noise at selfnoiseSNR
+ * (apply_self_noise, utils.py:1414-1431), energy VAD of each node's mic-0 wet
+ * speech.  Random numbers: counter-based (seed + scene, stream, index).
+ * Outputs (device): data, cleanspeech, cleannoise [S][sum M][T] float,
+ * vad [S][K][T] uint8.  Synchronises `stream`.                           */
+typedef struct danse_scene_cfg {
+  int32_t S, K;
+  const int32_t* M;         /* [K] sensors per node                            */
+  int32_t T;                /* samples per channel                             */
+  int32_t nIR;              /* IR taps (randIRsParams.duration * fs)           */
+  int64_t seed;             /* scene s uses seed + s                           */
+  double fs, snr, selfnoiseSNR, pauseDuration, pauseSpacing;
+  double vadEnergyDecrease_dB, vadWinLength;
+  const double* sroPpm;     /* [K] or NULL                                     */
+} danse_scene_cfg;
+const char* danse_scene_last_error(void);
+int danse_scene_generate(const danse_scene_cfg* cfg, float* data, float* cleanspeech, float* cleannoise, uint8_t* vad,
+                         void* stream);
 
 /* ---- T(z) few-samples compression (broadcastType 'fewSamples').
  * danse_tz_create: analysis window h, synthesis window f (N floats, host), the

@@ -285,7 +285,8 @@ class OnlineDANSE:
     """Restatement of ``d_core.danse`` (``d_core.py:26-102``) over
     ``DANSEvariables`` (``d_classes.py:478-2709``)."""
 
-    def __init__(self, scene, p, vadMinProp=0.5, yinOverride=None, keepHistory=True, maxRounds=None):
+    def __init__(self, scene, p, vadMinProp=0.5, yinOverride=None, keepHistory=True, maxRounds=None,
+                 sroEstimates=None):
         self.p = p
         self.scene = scene
         wasn = scene.wasn
@@ -300,6 +301,11 @@ class OnlineDANSE:
         self.T = wasn[0].data.shape[0]
         self.nIter = int((self.T - N) / Ns) + 1
         self.maxRounds = maxRounds
+        # estimateSROs 'DXCPPhaT' (the build's extension; the reference
+        # raises, quirk Q12): the per-iteration estimates [K][nIter][K - 1]
+        # come from outside (the device estimators) and take the place of the
+        # Oracle values in update_sro_estimates
+        self.extEst = sroEstimates
         self.seqNU = 'seq' in p.nodeUpdating
         self.h = p.winWOLAanalysis
         self.f = p.winWOLAsynthesis
@@ -712,9 +718,13 @@ class OnlineDANSE:
             self.SROsResiduals[k][i, :] = sroOut
         elif p.estimateSROs == 'CohDrift':
             self._cohdrift(k, i)
+        elif p.estimateSROs == 'DXCPPhaT':
+            self.SROsResiduals[k][i, :] = self.extEst[k][i, :]
         if p.compensateSROs:
             for q in range(len(self.neighbors[k])):
-                if p.estimateSROs == 'CohDrift':
+                if p.estimateSROs == 'DXCPPhaT':
+                    self.SROsEstimates[k][i, q] = self.extEst[k][i, q]
+                elif p.estimateSROs == 'CohDrift':
                     res = self.SROsResiduals[k][i, q]
                     if p.cohDrift.loop == 'closed':
                         self.SROsEstimates[k][i, q] += res / (1 + res) * p.cohDrift.alphaEps

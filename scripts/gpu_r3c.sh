@@ -4,9 +4,9 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${TAG:-r3c}
-timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_metrics.py tests/test_gpu_dxcp.py -m gpu -v -s \
+timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_metrics.py tests/test_gpu_dxcp.py tests/test_gpu_scene.py -m gpu -v -s \
   --timeout 300 --timeout-method thread -p no:cacheprovider \
-  -k "${PYTEST_K:-sro_nocomp or L256 or stoi or end_to_end or cl_dxcp or tdoa or dxcp or get_metrics}" > gpurun_out/pytest_$TAG.log 2>&1
+  -k "${PYTEST_K:-sro_nocomp or L256 or stoi or end_to_end or cl_dxcp or tdoa or dxcp or get_metrics or scene}" > gpurun_out/pytest_$TAG.log 2>&1
 rc=$?
 grep -E "passed|failed" gpurun_out/pytest_$TAG.log | tail -2
 grep -E "^FAILED" gpurun_out/pytest_$TAG.log | head -20

@@ -79,3 +79,49 @@ def test_dxcp_tdoa_correction():
         assert s0 == s1
         if t0 != 0.0 and abs(t0) < 4095:
             assert abs((t1 - t0) - tdoa * 16000) <= 1e-9, (i, t0, t1)
+
+
+def test_dxcp_in_the_loop_vs_oracle():
+    """estimateSROs 'DXCPPhaT' in the online engine (the build's extension;
+    the reference raises, quirk Q12): device DXCP-PhaT estimators per
+    (receiver, sender) on the local reference sensor and the received z
+    streams of an SRO-resampled scene (device scene generator).  The
+    estimates converge to the true relative SRO; the float64 oracle fed the
+    device's estimate sequence (update_sro_estimates with external values)
+    reproduces the filters and estimates at the usual tolerance."""
+    from danse_amd.core import danse_multi
+    from danse_amd.scene import make_scenes_device
+    from oracle import danse_ref_cpu as O
+    from _util import make_case_params
+    from golden_cases import BATTERY, _d
+    sros = [0.0, 120.0, -80.0]
+    M = [2, 2, 2]
+    case = dict(M=M, sros=sros, danse=_d(BATTERY, nodeUpdating='asy', compensateSROs=True, includeFSDflags=True,
+                                         estimateSROs='DXCPPhaT'))
+    dp, wp = make_case_params(case)
+    scenes, _ = make_scenes_device(M, 1, sigDur=12.0, seed=3, SROperNode=sros, host_signals=True)
+    sc = scenes[0]
+    for nd in sc.wasn:
+        for f in ('data', 'cleanspeech', 'cleannoise'):
+            setattr(nd, f, getattr(nd, f).astype(np.float64))
+    sc.get_vad_per_frame(dp.DFTsize, dp.Ns, wp.vadMinProportionActive)
+    dv = danse_multi([sc], dp)[0]
+    K, R = len(M), dv.nRounds
+    for k in range(K):
+        nb = [q for q in range(K) if q != k]
+        truth = (np.array([sros[q] for q in nb]) - sros[k]) * 1e-6
+        last = dv.SROsResiduals[k][R - 1]
+        print('node', k, 'DXCP', last * 1e6, 'true', truth * 1e6)
+        assert np.all(np.abs(last - truth) <= 10e-6), (k, last, truth)
+    ov = O.danse(sc, dp, vadMinProp=wp.vadMinProportionActive,
+                 sroEstimates=[dv.SROsResiduals[k] for k in range(K)])
+    errs = []
+    for k in range(K):
+        s0 = int(ov.startRound[k])
+        wg, wr = dv.wTilde[k][:, s0 + 1:R + 1, :], ov.wTilde[k][:, s0 + 1:R + 1, :]
+        errs.append((np.linalg.norm(wg - wr, axis=-1) / np.maximum(np.linalg.norm(wr, axis=-1), 1e-30)).ravel())
+    e = np.concatenate(errs)
+    st = dict(median=float(np.median(e)), p99=float(np.percentile(e, 99)))
+    de = float(np.max(np.abs(dv.d - ov.d)) / np.max(np.abs(ov.d)))
+    print('filters', st, 'd', de)
+    assert st['median'] <= 1e-5 and st['p99'] <= 1e-4 and de <= 1e-4
