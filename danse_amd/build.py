@@ -5,7 +5,7 @@ operator kernels), ``csrc/batch.hip`` (batch-mode engine), ``csrc/dxcp.hip`` (DX
 estimator), ``csrc/tz.hip`` (T(z) few-samples compression), ``csrc/metrics.hip``
 (SNR / fwSNRseg), ``csrc/stoi.hip`` ((e)STOI) and of
 ``csrc/update_class.hip`` once per filter-size class
-(``-DDANSE_DMAX=N``, N = 1..16 and 24..64 in steps of 8, see
+(``-DDANSE_DMAX=N``, N = 1..12, 16, 20 and 24..64 in steps of 8, see
 ``csrc/classes.hpp``), in parallel, then one
 ``hipcc -shared`` link.  Objects go to ``danse_amd/_obj/``; the library sits
 next to this file so that it travels with the repository snapshot to the GPU
@@ -24,7 +24,7 @@ CSRC = HERE / 'csrc'
 OBJ = HERE / '_obj'
 OUT = HERE / 'libdanse_mi355x.so'
 INC = HERE.parent / 'include'
-CLASSES = list(range(1, 13)) + [16, 24, 32, 40, 48, 56, 64]
+CLASSES = list(range(1, 13)) + [16, 20, 24, 32, 40, 48, 56, 64]
 LANE_MAX_D = 12   # csrc/classes.hpp kLaneMaxD
 FLAGS = ['--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC']
 

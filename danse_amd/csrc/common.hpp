@@ -40,6 +40,76 @@ DANSE_DEV void fms_cc(cf& acc, cf a, cf b) {
   acc.re = fmaf(-a.re, b.re, fmaf(-a.im, b.im, acc.re));
   acc.im = fmaf(-a.im, b.re, fmaf(a.re, b.im, acc.im));
 }
+// The same three operations as two v_pk_fma_f32 each, with the operand
+// halves picked and negated by op_sel / neg modifiers (clang materialises
+// the swapped and negated pairs with v_mov / v_xor instead: ~1 extra VALU
+// op per complex FMA).  Rounding is identical to the scalar forms above
+// (same inner / outer fma order per component).
+typedef float f2v __attribute__((ext_vector_type(2)));
+// acc += a * b
+DANSE_DEV void pk_fma_c(cf& acc, cf a, cf b) {
+  f2v c = {acc.re, acc.im};
+  const f2v x = {a.re, a.im}, y = {b.re, b.im};
+  asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[1,0,0]\n\t"
+      "v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[0,1,1]"
+      : "+v"(c)
+      : "v"(x), "v"(y));
+  acc = cf{c.x, c.y};
+}
+// acc -= a * conj(b)
+DANSE_DEV void pk_fms_cc(cf& acc, cf a, cf b) {
+  f2v c = {acc.re, acc.im};
+  const f2v x = {a.re, a.im}, y = {b.re, b.im};
+  asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[1,0,0]\n\t"
+      "v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[1,0,1] neg_lo:[1,0,0] neg_hi:[1,0,0]"
+      : "+v"(c)
+      : "v"(x), "v"(y));
+  acc = cf{c.x, c.y};
+}
+// acc += a * conj(b)
+DANSE_DEV void pk_fma_cc(cf& acc, cf a, cf b) {
+  f2v c = {acc.re, acc.im};
+  const f2v x = {a.re, a.im}, y = {b.re, b.im};
+  asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_hi:[1,0,0]\n\t"
+      "v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[1,0,1]"
+      : "+v"(c)
+      : "v"(x), "v"(y));
+  acc = cf{c.x, c.y};
+}
+// Generic packed complex multiply-accumulate: acc += (NEG ? -1 : 1) op(a) op(b),
+// op = conj where CA / CB.  Inner v_pk_fma_f32: the a.im terms
+// (lo: -a.im b.im, hi: a.im b.re, signs folded into neg_lo / neg_hi of
+// src0), outer: the a.re terms (lo: a.re b.re, hi: a.re b.im).
+#define DANSE_PK_CMAC(N1L, N1H, N2L, N2H)                                                                  \
+  asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[" #N1L ",0,0] neg_hi:[" #N1H \
+      ",0,0]\n\tv_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[0,1,1] neg_lo:[" #N2L ",0,0] neg_hi:[" #N2H ",0,0]" \
+      : "+v"(c)                                                                                            \
+      : "v"(x), "v"(y))
+template <bool CA, bool CB, bool NEG>
+DANSE_DEV void cmac(cf& acc, cf a, cf b) {
+  constexpr int sA = CA ? -1 : 1, sB = CB ? -1 : 1, s = NEG ? -1 : 1;
+  constexpr int code = ((-s * sA * sB) < 0 ? 8 : 0) | ((s * sA) < 0 ? 4 : 0) | (s < 0 ? 2 : 0) | ((s * sB) < 0 ? 1 : 0);
+  f2v c = {acc.re, acc.im};
+  const f2v x = {a.re, a.im}, y = {b.re, b.im};
+  if constexpr (code == 0) DANSE_PK_CMAC(0, 0, 0, 0);
+  else if constexpr (code == 1) DANSE_PK_CMAC(0, 0, 0, 1);
+  else if constexpr (code == 2) DANSE_PK_CMAC(0, 0, 1, 0);
+  else if constexpr (code == 3) DANSE_PK_CMAC(0, 0, 1, 1);
+  else if constexpr (code == 4) DANSE_PK_CMAC(0, 1, 0, 0);
+  else if constexpr (code == 5) DANSE_PK_CMAC(0, 1, 0, 1);
+  else if constexpr (code == 6) DANSE_PK_CMAC(0, 1, 1, 0);
+  else if constexpr (code == 7) DANSE_PK_CMAC(0, 1, 1, 1);
+  else if constexpr (code == 8) DANSE_PK_CMAC(1, 0, 0, 0);
+  else if constexpr (code == 9) DANSE_PK_CMAC(1, 0, 0, 1);
+  else if constexpr (code == 10) DANSE_PK_CMAC(1, 0, 1, 0);
+  else if constexpr (code == 11) DANSE_PK_CMAC(1, 0, 1, 1);
+  else if constexpr (code == 12) DANSE_PK_CMAC(1, 1, 0, 0);
+  else if constexpr (code == 13) DANSE_PK_CMAC(1, 1, 0, 1);
+  else if constexpr (code == 14) DANSE_PK_CMAC(1, 1, 1, 0);
+  else DANSE_PK_CMAC(1, 1, 1, 1);
+  acc = cf{c.x, c.y};
+}
+#undef DANSE_PK_CMAC
 DANSE_DEV cf cdiv_real(cf a, float s) {
   float r = 1.0f / s;
   return cf{a.re * r, a.im * r};

@@ -428,7 +428,7 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
       wOff += histW * F * fn.D;
       fn.liOff = liOff;
       if (c->gevd && fn.packed) liOff += (long long)F * (fn.D * (fn.D + 1) / 2 + fn.D);
-      else if (c->gevd && class_dmax(fn.D) <= 48) liOff += (long long)F * (64 * (class_dmax(fn.D) / 8) * (class_dmax(fn.D) / 8) + 64);
+      else if (c->gevd && class_grid(class_dmax(fn.D)) > 0) liOff += (long long)F * class_li_record(class_dmax(fn.D));
       eng->fns.push_back(fn);
     }
   }

@@ -8,7 +8,7 @@
 //
 // Register phases (the float64 block and the float32 Ryy block are never
 // live together): Rnn recursion (+ store) -> float64 Cholesky + inverse ->
-// Li in float32 -> Ryy recursion (+ store) -> congruence, tridiagonal,
+// Li in float32 (LDS) -> Ryy recursion (+ store) -> congruence, tridiagonal,
 // eigen part, back-transform.
 #pragma once
 #include "kernels.hpp"
@@ -20,47 +20,60 @@
 
 namespace danse {
 
-template <int NB, int RMAX>
+// G = 8: one bin per wave on the 8 x 8 lane grid; G = 4: four bins per wave
+// (bins f0 .. f0 + 3 of one scene / family-node), each on a 16-lane DPP row,
+// lane-layout vectors with vpl entries per lane (solver2d.hpp).
+template <int NB, int RMAX, int G = 8>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NB <= 5 ? DANSE_2D_WPE : 1)))
 update_kernel_2d(const UpdateArgs a) {
   using namespace t2d;
-  __shared__ LDS2<NB> S;
-  const int li = threadIdx.x;
-  const int p = li >> 3, q = li & 7;
+  constexpr int L = bin_lanes<G>(), W = 64 / L, V = vpl<NB, G>();
+  __shared__ LDS2<NB, G> Sall[W];
+  const int bw = threadIdx.x / L;
+  const int li = threadIdx.x % L;
+  LDS2<NB, G>& S = Sall[bw];
+  const int p = li / G, q = li % G;
   const int F = a.F;
-  const int f = blockIdx.x % F;
-  const int tt = blockIdx.x / F;
+  const int FG = (F + W - 1) / W;
+  const int fg = blockIdx.x % FG;
+  const int tt = blockIdx.x / FG;
+  const int f0 = fg * W + bw;
+  const bool fvalid = (W == 1) || f0 < F;   // the last group's tail bins compute on bin F-1, store nothing
+  const int f = (W == 1 || f0 < F) ? f0 : F - 1;
   const int fni = tt % a.nFN;
   const int s = tt / a.nFN;
   const FamNode d = a.fn[fni];
   const int D = d.D;
-  const bool act = li < D;
   const int r = a.r;
   const uint8_t fl = a.flags[(((long long)r * a.S + s) * kMaxFam + d.fam) * a.K + d.k];
   const int opY = fl & 3, opN = (fl >> 2) & 3;
   const bool pregiven = (fl & DANSE_FLAG_PREGIVEN) != 0;
   const bool solve = (fl & DANSE_FLAG_SOLVE) != 0 && !pregiven;
   const bool initslot = (fl & DANSE_FLAG_INITSLOT) != 0;
-  // factor cache (kernels.hpp li_reusable): per bin the float32 Li blocks in
-  // lane order [NB * NB][64] and g [64]
+  // factor cache (kernels.hpp li_reusable): per bin S.Ls (packed Li, float32)
+  // and g (solver2d.hpp li_record / li_store2d)
   const bool reuse = solve && li_reusable(a, d, s, opN);
-  cf* liC = a.liCache ? a.liCache + (long long)s * a.liStride + d.liOff + (long long)f * (64 * NB * NB + 64) : nullptr;
+  cf* liC = a.liCache ? a.liCache + (long long)s * a.liStride + d.liOff + (long long)f * li_record<NB, G>() : nullptr;
 
-  const cf y = load_y(a, d, s, f, li, act);
-  S.vb[li] = y;
+  cf y[V];
+  sfor<0, V>([&](auto vc) {
+    constexpr int v = decltype(vc)::value;
+    const int i = li + L * v;
+    y[v] = load_y(a, d, s, f, i, i < D);
+    S.vb[i] = y[v];
+  });
   t2d::wsync();
   cf yr[NB], yc[NB];
   sfor<0, NB>([&](auto sc) {
     constexpr int sb = decltype(sc)::value;
-    yr[sb] = S.vb[p + 8 * sb];
-    yc[sb] = S.vb[q + 8 * sb];
+    yr[sb] = S.vb[p + G * sb];
+    yc[sb] = S.vb[q + G * sb];
   });
   t2d::wsync();
   const double beta = a.beta[s * a.K + d.k];
   const long long matOff = (long long)s * a.scmStride + d.scmOff + (long long)f * D * D;
 
-  // ---- Rnn (float64): recursion, store, factor --------------------------
-  Blk<NB> Lf;
+  // ---- Rnn (float64): recursion, store, factor -> Li in S.Ls -------------
   bool ok = true;
   if (opN || (solve && !reuse)) {
     BlkD<NB> M;
@@ -70,7 +83,7 @@ update_kernel_2d(const UpdateArgs a) {
       constexpr int sb = decltype(sc)::value;
       sfor<0, NB>([&](auto tc) {
         constexpr int tb = decltype(tc)::value;
-        const int i = p + 8 * sb, c = q + 8 * tb;
+        const int i = p + G * sb, c = q + G * tb;
         const bool in = i < D && c < D;
         cd x = csel(in, a.Rnn[matOff + (in ? (long long)i * D + c : 0ll)], cd{0.0, 0.0});
         if (opN) {
@@ -79,37 +92,21 @@ update_kernel_2d(const UpdateArgs a) {
           x = cx * x;
           x.re = fma(cy, yy.re, x.re);
           x.im = fma(cy, yy.im, x.im);
-          if (in) a.Rnn[matOff + (long long)i * D + c] = x;
+          if (in && fvalid) a.Rnn[matOff + (long long)i * D + c] = x;
         }
         M.v[sb][tb] = x;
       });
     });
     if (solve && !reuse) {
-      ok = gevd2d_factor<NB>(M, Lf, S, li, D, d.ref);
-      if (liC) {
-        sfor<0, NB>([&](auto sc) {
-          sfor<0, NB>([&](auto tc) {
-            constexpr int sb = decltype(sc)::value, tb = decltype(tc)::value;
-            liC[(sb * NB + tb) * 64 + li] = Lf.v[sb][tb];
-          });
-        });
-        liC[64 * NB * NB + li] = S.g[li];
-      }
+      ok = gevd2d_factor<NB, G>(M, S, li, D, d.ref);
+      if (liC && fvalid) li_store2d<NB, G>(S, liC, li);
     }
   }
-  if (reuse) {
-    sfor<0, NB>([&](auto sc) {
-      sfor<0, NB>([&](auto tc) {
-        constexpr int sb = decltype(sc)::value, tb = decltype(tc)::value;
-        Lf.v[sb][tb] = liC[(sb * NB + tb) * 64 + li];
-      });
-    });
-    S.g[li] = liC[64 * NB * NB + li];
-    t2d::wsync();
-  }
+  if (reuse) li_load2d<NB, G>(S, liC, li);
 
   // ---- Ryy (float32): recursion, store, filter ---------------------------
-  cf w = cf{0.0f, 0.0f};
+  cf w[V];
+  sfor<0, V>([&](auto vc) { w[decltype(vc)::value] = cf{0.0f, 0.0f}; });
   if (opY || solve) {
     Blk<NB> A;
     const float by = (float)beta, cy = (opY == DANSE_OP_SET) ? (float)(1.0 / D) : (float)((1.0 - beta) / D);
@@ -117,18 +114,18 @@ update_kernel_2d(const UpdateArgs a) {
       constexpr int sb = decltype(sc)::value;
       sfor<0, NB>([&](auto tc) {
         constexpr int tb = decltype(tc)::value;
-        const int i = p + 8 * sb, c = q + 8 * tb;
+        const int i = p + G * sb, c = q + G * tb;
         const bool in = i < D && c < D;
         cf x = csel(in, a.Ryy[matOff + (in ? (long long)i * D + c : 0ll)], cf{0.0f, 0.0f});
         if (opY) {
           const cf yy = cy * mulc(yr[sb], yc[tb]);
           x = csel(opY == DANSE_OP_SET, yy, by * x + yy);
-          if (in) a.Ryy[matOff + (long long)i * D + c] = x;
+          if (in && fvalid) a.Ryy[matOff + (long long)i * D + c] = x;
         }
         A.v[sb][tb] = x;
       });
     });
-    if (solve) w = gevd2d_filter<NB, RMAX>(A, Lf, S, li, D, a.rank);
+    if (solve) gevd2d_filter<NB, RMAX, G>(A, S, li, D, a.rank, w);
   }
 
   const long long wBase = (long long)s * a.wStride + d.wOff;
@@ -136,29 +133,41 @@ update_kernel_2d(const UpdateArgs a) {
   const int slotNext = a.wHistory ? r + 1 : ((r + 1) & 1);
   cf* wPrev = a.wHist + wBase + ((long long)slotPrev * F + f) * D;
   cf* wNext = a.wHist + wBase + ((long long)slotNext * F + f) * D;
-  const int rowc = act ? li : 0;
-  if (pregiven || initslot) {
-    w = csel(act, wNext[rowc], cf{0.0f, 0.0f});
-  } else if (solve) {
-    if (!ok && li == 0) atomicOr(&a.diag[(s * a.K + d.k) * kMaxFam + d.fam], 1);
-  } else {
-    w = csel(act, wPrev[rowc], cf{0.0f, 0.0f});
-  }
-  if (act && !pregiven && !initslot) wNext[li] = w;
-  node_bin_tail(a, d, s, f, li, fl, pregiven, true, w, y, gsum<64>(csel(act, cmul(w, y), cf{0.0f, 0.0f})));
+  if (solve && !pregiven && !initslot && !ok && li == 0 && fvalid)
+    atomicOr(&a.diag[(s * a.K + d.k) * kMaxFam + d.fam], 1);
+  cf dsum;
+  sfor<0, V>([&](auto vc) {
+    constexpr int v = decltype(vc)::value;
+    const int i = li + L * v;
+    const bool act = i < D;
+    const int rowc = act ? i : 0;
+    if (pregiven || initslot) w[v] = csel(act, wNext[rowc], cf{0.0f, 0.0f});
+    else if (!solve) w[v] = csel(act, wPrev[rowc], cf{0.0f, 0.0f});
+    if (act && !pregiven && !initslot && fvalid) wNext[i] = w[v];
+    const cf t = csel(act, cmul(w[v], y[v]), cf{0.0f, 0.0f});
+    dsum = (v == 0) ? t : dsum + t;
+  });
+  const cf dh = gsum<L>(dsum);
+  sfor<0, V>([&](auto vc) {
+    constexpr int v = decltype(vc)::value;
+    node_bin_tail(a, d, s, f, li + L * v, fl, pregiven, fvalid, w[v], y[v], dh);
+  });
 }
 
 // Stand-alone GEVD filter update (danse_filter_update): float64 SCM pairs
-// [B][D][D], one bin per wavefront.
-template <int NB, int RMAX>
+// [B][D][D], one bin per wavefront (G = 8) or four per wavefront (G = 4).
+template <int NB, int RMAX, int G = 8>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NB <= 5 ? DANSE_2D_WPE : 1)))
 filter_update_kernel_2d(const cd* Ryy, const cd* Rnn, int B, int D, int rank, int ref, cf* w, int* diag) {
   using namespace t2d;
-  __shared__ LDS2<NB> S;
-  const int li = threadIdx.x;
-  const int p = li >> 3, q = li & 7;
-  const int b = blockIdx.x;
-  Blk<NB> Lf;
+  constexpr int L = bin_lanes<G>(), W = 64 / L, V = vpl<NB, G>();
+  __shared__ LDS2<NB, G> Sall[W];
+  const int bw = threadIdx.x / L, li = threadIdx.x % L;
+  LDS2<NB, G>& S = Sall[bw];
+  const int p = li / G, q = li % G;
+  const int b0 = blockIdx.x * W + bw;
+  const bool valid = (W == 1) || b0 < B;
+  const int b = (W == 1 || b0 < B) ? b0 : B - 1;
   bool ok;
   {
     BlkD<NB> M;
@@ -166,26 +175,30 @@ filter_update_kernel_2d(const cd* Ryy, const cd* Rnn, int B, int D, int rank, in
       constexpr int sb = decltype(sc)::value;
       sfor<0, NB>([&](auto tc) {
         constexpr int tb = decltype(tc)::value;
-        const int i = p + 8 * sb, c = q + 8 * tb;
+        const int i = p + G * sb, c = q + G * tb;
         const bool in = i < D && c < D;
         M.v[sb][tb] = csel(in, Rnn[(long long)b * D * D + (in ? i * D + c : 0)], cd{0.0, 0.0});
       });
     });
-    ok = gevd2d_factor<NB>(M, Lf, S, li, D, ref);
+    ok = gevd2d_factor<NB, G>(M, S, li, D, ref);
   }
   Blk<NB> A;
   sfor<0, NB>([&](auto sc) {
     constexpr int sb = decltype(sc)::value;
     sfor<0, NB>([&](auto tc) {
       constexpr int tb = decltype(tc)::value;
-      const int i = p + 8 * sb, c = q + 8 * tb;
+      const int i = p + G * sb, c = q + G * tb;
       const bool in = i < D && c < D;
       A.v[sb][tb] = csel(in, cfk(Ryy[(long long)b * D * D + (in ? i * D + c : 0)]), cf{0.0f, 0.0f});
     });
   });
-  const cf wv = gevd2d_filter<NB, RMAX>(A, Lf, S, li, D, rank);
-  if (li < D) w[(long long)b * D + li] = wv;
-  if (diag && li == 0) diag[b] = ok ? 0 : 1;
+  cf wv[V];
+  gevd2d_filter<NB, RMAX, G>(A, S, li, D, rank, wv);
+  sfor<0, V>([&](auto vc) {
+    const int i = li + L * decltype(vc)::value;
+    if (valid && i < D) w[(long long)b * D + i] = wv[decltype(vc)::value];
+  });
+  if (diag && valid && li == 0) diag[b] = ok ? 0 : 1;
 }
 
 }  // namespace danse

@@ -338,10 +338,10 @@ int danse_scene_generate(const danse_scene_cfg* c, float* data, float* cleanspee
     }
   }
   const int MT = (int)chanNode.size();
-  std::vector<double> epsRow((size_t)S * MT * 2);
+  // relative SRO per resampled row (s, channel): wS and wN are [S][MT][T] each
+  std::vector<double> epsRow((size_t)S * MT);
   for (int s = 0; s < S; ++s)
-    for (int ch = 0; ch < MT; ++ch)
-      for (int w = 0; w < 2; ++w) epsRow[((size_t)s * MT + ch) * 2 + w] = c->sroPpm ? c->sroPpm[chanNode[ch]] * 1e-6 : 0.0;
+    for (int ch = 0; ch < MT; ++ch) epsRow[(size_t)s * MT + ch] = c->sroPpm ? c->sroPpm[chanNode[ch]] * 1e-6 : 0.0;
   std::vector<void*> owned;
   auto cleanup = [&]() {
     for (void* p : owned) (void)hipFree(p);

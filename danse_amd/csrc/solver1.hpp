@@ -32,6 +32,13 @@ DANSE_DEV cf herm(const PTri<D>& X) {
   if constexpr (I >= J) return X.a[P(I, J)];
   else return conjg(X.a[P(J, I)]);
 }
+// acc += (NEG ? -1 : 1) herm(X)[i][j] op(b) (op = conj where CB), one packed
+// complex MAC with the conjugation folded into its modifiers
+template <int I, int J, bool CB, bool NEG, int D>
+DANSE_DEV void herm_mac(cf& acc, const PTri<D>& X, cf b) {
+  if constexpr (I >= J) cmac<false, CB, NEG>(acc, X.a[P(I, J)], b);
+  else cmac<true, CB, NEG>(acc, X.a[P(J, I)], b);
+}
 
 // Householder tridiagonalisation of the Hermitian A (packed lower), in
 // place: on exit A[i][i].re is the diagonal, b[i] = T[i][i-1] (complex) for
@@ -65,7 +72,7 @@ DANSE_DEV void tridiag(PTri<D>& A, cf (&u0)[D], cf (&b)[D]) {
       cf acc = cf{0.0f, 0.0f};
       sfor<j + 1, D>([&](auto kc) {
         constexpr int k = decltype(kc)::value;
-        fma_c(acc, herm<i, k>(A), u[k]);
+        herm_mac<i, k, false, false>(acc, A, u[k]);
       });
       p[i] = acc;
     });
@@ -83,8 +90,8 @@ DANSE_DEV void tridiag(PTri<D>& A, cf (&u0)[D], cf (&b)[D]) {
       sfor<j + 1, i + 1>([&](auto kc) {
         constexpr int k = decltype(kc)::value;
         cf t = A.a[P(i, k)];
-        fms_cc(t, u2[i], q[k]);
-        fms_cc(t, q[i], u2[k]);
+        cmac<false, true, true>(t, u2[i], q[k]);
+        cmac<false, true, true>(t, q[i], u2[k]);
         if constexpr (i == k) t.im = 0.0f;
         A.a[P(i, k)] = t;
       });
@@ -251,10 +258,10 @@ DANSE_DEV void gevd_eig(PTri<D>& A, int R, Fn&& fn) {
     sfor_down<(D >= 2 ? D - 2 : 0), 0>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
       cf s = cmul(u0[j], v[j + 1]);
-      sfor<j + 2, D>([&](auto ic) { s = s + cmul(A.a[P(decltype(ic)::value, j)], v[decltype(ic)::value]); });
+      sfor<j + 2, D>([&](auto ic) { cmac<true, false, false>(s, A.a[P(decltype(ic)::value, j)], v[decltype(ic)::value]); });
       const cf s2 = 2.0f * s;
-      fms_c(v[j + 1], u0[j], s2);
-      sfor<j + 2, D>([&](auto ic) { fms_c(v[decltype(ic)::value], A.a[P(decltype(ic)::value, j)], s2); });
+      cmac<false, false, true>(v[j + 1], u0[j], s2);
+      sfor<j + 2, D>([&](auto ic) { cmac<false, false, true>(v[decltype(ic)::value], A.a[P(decltype(ic)::value, j)], s2); });
     });
     fn(r, lam, v);
   });

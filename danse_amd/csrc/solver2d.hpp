@@ -29,6 +29,13 @@
 namespace danse {
 namespace t2d {
 
+// lanes per bin and lane-layout vector entries per lane (G = 8: one bin
+// per wave, one entry per lane; G = 4: four bins per wave, DM <= 32)
+template <int G>
+constexpr int bin_lanes() { return G * G; }
+template <int NB, int G>
+constexpr int vpl() { return (G * NB + G * G - 1) / (G * G); }
+
 template <int NB>
 struct BlkD {
   cd v[NB][NB];
@@ -38,30 +45,70 @@ struct Blk {
   cf v[NB][NB];
 };
 
-template <int NB>
+// LDS of one bin.  The float64 factor phase, the congruence and the float32
+// phases never overlap, so their scratch shares one union; inside the
+// float32 phases the pivot vectors of the tridiagonalisation, the inverse
+// iteration's rows and the layout-change vectors (y staging, back-transform)
+// are used one after the other and share a second one.  NB = 5: 16.3 KB per
+// wave at G = 8; G = 4: 19.9 KB for the wave's four bins, so a CU holds 8
+// waves (2 per SIMD, the VGPR limit) in both.
+template <int NB, int G = 8>
 struct LDS2 {
-  static constexpr int DM = 8 * NB;
-  cd cb64[2][DM];   // float64 pivot column (double-buffered)
-  cd rb64[2][DM];   // float64 pivot row
-  double invd[DM];  // 1 / L[j][j]
-  cf cb[2][DM];     // float32 pivot column
-  cf qb[2][DM];     // row -> column layout transpose of q
+  static constexpr int DM = G * NB;
+  static constexpr int VL = bin_lanes<G>() * vpl<NB, G>();   // lane-layout vectors
   union {
-    cf Ls[DM][DM + 1];   // Li (float32) during the congruence
-    cf U[DM][DM + 1];    // then the Householder vectors U[j][i]
-  } m;
-  float a[DM];        // tridiagonal: diagonal
-  cf b[DM];           //              subdiagonal b[i] = T[i][i-1]
-  float e2[DM];       //              |b[i+1]|^2
-  float ev[DM];       //              |b[i+1]|
-  cf phi[DM];         //              phases phi_i = prod_{k<=i} b_k / |b_k|
-  float4 fac[DM];     // inverse iteration: eliminated rows (d, du, dl2, rhs)
-  float xs[64];       //                    right-hand side of the next sweep
-  cf g[64];           // g = L^H e_ref (lane layout)
-  cf vb[64];          // lane layout -> row layout
-  cf wb[64];          // column layout -> lane layout
-  float x[kRMax][DM]; // tridiagonal eigenvectors (Gram-Schmidt, rank > 1)
+    struct {                // float64 factor phase (chol2d, trinv2d)
+      cd cb64[2][DM];       // pivot column (double-buffered)
+      cd rb64[2][DM];       // pivot row
+      double invd[DM];      // 1 / L[j][j]
+    };
+    struct {                // float32 phases (tridiagonalisation .. back-transform)
+      union {
+        struct {
+          cf cb[2][DM];     // pivot column
+          cf qb[2][DM];     // row -> column layout transpose of q
+        };
+        struct {
+          float4 fac[DM];   // inverse iteration: eliminated rows (d, du, dl2, rhs)
+          float xs[VL];     //                    right-hand side of the next sweep
+        };
+        struct {
+          cf vb[VL];        // lane layout -> row layout (y staging, Li^H v)
+          cf wb[VL];        // column layout -> lane layout
+        };
+      };
+      float a[DM];          // tridiagonal: diagonal
+      cf b[DM];             //              subdiagonal b[i] = T[i][i-1]
+      float e2[DM];         //              |b[i+1]|^2
+      float ev[DM];         //              |b[i+1]|
+      cf phi[DM];           //              phases phi_i = prod_{k<=i} b_k / |b_k|
+      float x[kRMax][DM];   // tridiagonal eigenvectors (Gram-Schmidt, rank > 1)
+    };
+    struct {                // congruence: one block column of A / block row of Z
+      cf cz[G][DM];
+    };
+  };
+  // Li (float32) from the factor to the back-transform, lower triangle packed
+  // by columns (ls_col); it never lives in registers, so the float32 phases
+  // hold one NB x NB block (the Ryy / C block) instead of two.
+  cf Ls[DM * (DM + 1) / 2];
+  // Householder vectors u_j (i > j), packed by j (u_row)
+  cf U[DM * (DM - 1) / 2];
+  cf g[VL];           // g = L^H e_ref (lane layout), written by the factor phase
 };
+
+// column-packed lower triangle: (i, c), i >= c, column c at c DM - c (c - 1) / 2
+template <int DM>
+DANSE_DEV int ls_col(int c) { return c * DM - ((c * (c - 1)) >> 1); }
+// Li[i][c] from LDS (zero above the diagonal; the load always stays in bounds)
+template <int DM>
+DANSE_DEV cf ls_get(const cf* Ls, int i, int c) {
+  const bool lo = i >= c;
+  return csel(lo, Ls[lo ? ls_col<DM>(c) + i - c : 0], cf{0.0f, 0.0f});
+}
+// Householder vector j, entries i = j + 1 .. DM - 1
+template <int DM>
+DANSE_DEV int u_row(int j) { return j * (DM - 1) - ((j * (j - 1)) >> 1) - j - 1; }
 
 // ---- cross-lane helpers ---------------------------------------------------
 // LDS hand-off inside the one-wave workgroup: LDS operations of a wavefront
@@ -79,42 +126,60 @@ DANSE_DEV double dpp_d(double x) {
   const int hi = __builtin_amdgcn_mov_dpp((int)(v >> 32), CTRL, 0xF, 0xF, true);
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
-// sum over the 8 lanes of my row group (lanes 8p .. 8p+7)
+// sum over the G lanes of my row group (lanes G p .. G p + G - 1 of the bin)
+template <int G>
 DANSE_DEV float sumq(float x) {
   x += dpp_x<0xB1>(x);    // quad_perm [1,0,3,2]
   x += dpp_x<0x4E>(x);    // quad_perm [2,3,0,1]
-  x += dpp_x<0x141>(x);   // row_half_mirror (quads 0/1 of each half-row)
+  if constexpr (G == 8) x += dpp_x<0x141>(x);   // row_half_mirror (quads 0/1 of each half-row)
   return x;
 }
-DANSE_DEV cf sumq(cf x) { return cf{sumq(x.re), sumq(x.im)}; }
+template <int G>
+DANSE_DEV cf sumq(cf x) { return cf{sumq<G>(x.re), sumq<G>(x.im)}; }
+template <int G>
 DANSE_DEV double sumq(double x) {
   x += dpp_d<0xB1>(x);
   x += dpp_d<0x4E>(x);
-  x += dpp_d<0x141>(x);
+  if constexpr (G == 8) x += dpp_d<0x141>(x);
   return x;
 }
-DANSE_DEV cd sumq(cd x) { return cd{sumq(x.re), sumq(x.im)}; }
-// sum over the 8 row groups (lanes q, q+8, ..., q+56)
+template <int G>
+DANSE_DEV cd sumq(cd x) { return cd{sumq<G>(x.re), sumq<G>(x.im)}; }
+// sum over the G row groups of the bin (lanes q, q + G, ...)
+template <int G>
 DANSE_DEV float sump(float x) {
-  x += dpp_x<0x128>(x);   // row_ror:8 == xor 8 inside a 16-lane row
-  x += __shfl_xor(x, 16);
-  x += __shfl_xor(x, 32);
+  if constexpr (G == 8) {
+    x += dpp_x<0x128>(x);   // row_ror:8 == xor 8 inside a 16-lane row
+    x += __shfl_xor(x, 16);
+    x += __shfl_xor(x, 32);
+  } else {
+    x += dpp_x<0x124>(x);   // row_ror:4
+    x += dpp_x<0x128>(x);   // row_ror:8: the four quads of the 16-lane row
+  }
   return x;
 }
-DANSE_DEV cf sump(cf x) { return cf{sump(x.re), sump(x.im)}; }
+template <int G>
+DANSE_DEV cf sump(cf x) { return cf{sump<G>(x.re), sump<G>(x.im)}; }
+// value of bin-local lane src (runtime, bin-uniform): v_readlane when the bin
+// is the whole wave, a bpermute inside the 16-lane row otherwise
+template <int G>
+DANSE_DEV double bin_rld(double x, int src) {
+  if constexpr (G == 8) return big::rld(x, src);
+  else return __shfl(x, (__lane_id() & ~15) | src);
+}
 
 // ---- float64 Cholesky, in place: M = L (lower, upper part zeroed) -----------
-template <int NB>
-DANSE_DEV bool chol2d(BlkD<NB>& M, LDS2<NB>& S, int li, int D) {
-  const int p = li >> 3, q = li & 7;
+template <int NB, int G = 8>
+DANSE_DEV bool chol2d(BlkD<NB>& M, LDS2<NB, G>& S, int li, int D) {
+  const int p = li / G, q = li % G;
   bool ok = true;
   int buf = 0;
   sfor<0, NB>([&](auto sjc) {
     constexpr int sj = decltype(sjc)::value;
-    for (int rj = 0; rj < 8; ++rj) {
-      const int j = 8 * sj + rj;
+    for (int rj = 0; rj < G; ++rj) {
+      const int j = G * sj + rj;
       if (j >= D) break;
-      const double p0 = big::rld(M.v[sj][sj].re, 9 * rj);   // lane (rj, rj)
+      const double p0 = bin_rld<G>(M.v[sj][sj].re, (G + 1) * rj);   // lane (rj, rj)
       ok = ok && (p0 > 1e-300);
       const double piv = p0 > 1e-300 ? p0 : 1e-300;
       const double inv = lane::rsqrt64(piv);
@@ -122,7 +187,7 @@ DANSE_DEV bool chol2d(BlkD<NB>& M, LDS2<NB>& S, int li, int D) {
       if (q == rj) {
         sfor<sj, NB>([&](auto sc) {
           constexpr int s = decltype(sc)::value;
-          const int i = p + 8 * s;
+          const int i = p + G * s;
           const cd v0 = M.v[s][sj];
           const cd v = csel(i == j, cd{piv * inv, 0.0}, csel(i > j, inv * v0, cd{0.0, 0.0}));
           M.v[s][sj] = v;
@@ -133,8 +198,8 @@ DANSE_DEV bool chol2d(BlkD<NB>& M, LDS2<NB>& S, int li, int D) {
       cd rv[NB], cv[NB];
       sfor<sj, NB>([&](auto sc) {
         constexpr int s = decltype(sc)::value;
-        rv[s] = S.cb64[buf][p + 8 * s];
-        cv[s] = S.cb64[buf][q + 8 * s];
+        rv[s] = S.cb64[buf][p + G * s];
+        cv[s] = S.cb64[buf][q + G * s];
       });
       sfor<sj, NB>([&](auto sc) {
         constexpr int s = decltype(sc)::value;
@@ -150,7 +215,7 @@ DANSE_DEV bool chol2d(BlkD<NB>& M, LDS2<NB>& S, int li, int D) {
     constexpr int s = decltype(sc)::value;
     sfor<0, NB>([&](auto tc) {
       constexpr int t = decltype(tc)::value;
-      if (p + 8 * s < q + 8 * t) M.v[s][t] = cd{0.0, 0.0};
+      if (p + G * s < q + G * t) M.v[s][t] = cd{0.0, 0.0};
     });
   });
   return ok;
@@ -162,20 +227,20 @@ DANSE_DEV bool chol2d(BlkD<NB>& M, LDS2<NB>& S, int li, int D) {
 //   X[i][c] -= L[i][k] X[k][c]   for i > k, c <= k      (X[i][k] replaces L[i][k])
 // Row k (owners p == rk) and column k of L (owners q == rk) are broadcast
 // through LDS, one barrier per step.
-template <int NB>
-DANSE_DEV void trinv2d(BlkD<NB>& M, LDS2<NB>& S, int li, int D) {
-  const int p = li >> 3, q = li & 7;
+template <int NB, int G = 8>
+DANSE_DEV void trinv2d(BlkD<NB>& M, LDS2<NB, G>& S, int li, int D) {
+  const int p = li / G, q = li % G;
   int buf = 0;
   sfor<0, NB>([&](auto skc) {
     constexpr int sk = decltype(skc)::value;
-    for (int rk = 0; rk < 8; ++rk) {
-      const int k = 8 * sk + rk;
+    for (int rk = 0; rk < G; ++rk) {
+      const int k = G * sk + rk;
       if (k >= D) break;
       const double ik = S.invd[k];
       if (p == rk) {
         sfor<0, NB>([&](auto tc) {
           constexpr int t = decltype(tc)::value;
-          const int c = q + 8 * t;
+          const int c = q + G * t;
           const cd v = csel(c == k, cd{ik, 0.0}, csel(c < k, ik * M.v[sk][t], cd{0.0, 0.0}));
           M.v[sk][t] = v;
           S.rb64[buf][c] = v;
@@ -184,7 +249,7 @@ DANSE_DEV void trinv2d(BlkD<NB>& M, LDS2<NB>& S, int li, int D) {
       if (q == rk) {
         sfor<sk, NB>([&](auto sc) {
           constexpr int s = decltype(sc)::value;
-          const int i = p + 8 * s;
+          const int i = p + G * s;
           S.cb64[buf][i] = csel(i > k, M.v[s][sk], cd{0.0, 0.0});
         });
       }
@@ -192,15 +257,15 @@ DANSE_DEV void trinv2d(BlkD<NB>& M, LDS2<NB>& S, int li, int D) {
       cd lc[NB], xr[NB];
       sfor<sk, NB>([&](auto sc) {
         constexpr int s = decltype(sc)::value;
-        lc[s] = S.cb64[buf][p + 8 * s];
+        lc[s] = S.cb64[buf][p + G * s];
       });
       sfor<0, sk + 1>([&](auto tc) {
         constexpr int t = decltype(tc)::value;
-        xr[t] = S.rb64[buf][q + 8 * t];
+        xr[t] = S.rb64[buf][q + G * t];
       });
       sfor<sk, NB>([&](auto sc) {
         constexpr int s = decltype(sc)::value;
-        const int i = p + 8 * s;
+        const int i = p + G * s;
         sfor<0, sk + 1>([&](auto tc) {
           constexpr int t = decltype(tc)::value;
           cd x = M.v[s][t];
@@ -214,120 +279,140 @@ DANSE_DEV void trinv2d(BlkD<NB>& M, LDS2<NB>& S, int li, int D) {
   });
 }
 
-// ---- phase 1: Rnn block (float64, destroyed) -> Li (float32 block), g in LDS
-template <int NB>
-DANSE_DEV bool gevd2d_factor(BlkD<NB>& M, Blk<NB>& Lf, LDS2<NB>& S, int li, int D, int ref) {
-  const int p = li >> 3, q = li & 7;
-  const bool ok = chol2d<NB>(M, S, li, D);
+// ---- phase 1: Rnn block (float64, destroyed) -> Li (float32, S.Ls), g in LDS
+template <int NB, int G = 8>
+DANSE_DEV bool gevd2d_factor(BlkD<NB>& M, LDS2<NB, G>& S, int li, int D, int ref) {
+  constexpr int DM = G * NB;
+  const int p = li / G, q = li % G;
+  constexpr int L = bin_lanes<G>(), V = vpl<NB, G>();
+  const bool ok = chol2d<NB, G>(M, S, li, D);
   // g = L^H e_ref: g_c = conj(L[ref][c]) (c <= ref; the upper part is zero)
-  S.g[li] = cf{0.0f, 0.0f};
+  sfor<0, V>([&](auto vc) { S.g[li + L * decltype(vc)::value] = cf{0.0f, 0.0f}; });
   wsync();
   {
-    // row ref of L: block row ref >> 3 (a select chain over the static
+    // row ref of L: block row ref / G (a select chain over the static
     // block index, no branches) on the row group p == ref & 7
-    const int sr = ref >> 3;
+    const int sr = ref / G;
     sfor<0, NB>([&](auto tc) {
       constexpr int t = decltype(tc)::value;
       cd v = M.v[0][t];
       sfor<1, NB>([&](auto sc) { v = csel(decltype(sc)::value == sr, M.v[decltype(sc)::value][t], v); });
-      if (p == (ref & 7)) S.g[q + 8 * t] = conjg(cfk(v));
+      if (p == (ref % G)) S.g[q + G * t] = conjg(cfk(v));
     });
   }
-  trinv2d<NB>(M, S, li, D);
-  sfor<0, NB>([&](auto sc) {
-    constexpr int s = decltype(sc)::value;
-    sfor<0, NB>([&](auto tc) {
-      constexpr int t = decltype(tc)::value;
-      Lf.v[s][t] = cfk(M.v[s][t]);
-    });
-  });
-  return ok;
-}
-
-// ---- C = Li A Li^H in place of A (float32); Li staged in LDS ---------------
-template <int NB>
-DANSE_DEV void congruence2d(Blk<NB>& A, const Blk<NB>& Lf, LDS2<NB>& S, int li, int D) {
-  const int p = li >> 3, q = li & 7;
-  // scipy.linalg.eigh reads the lower triangle: A[i][c] = conj(A[c][i]) for
-  // i < c (the SCMs are Hermitian except for the random init's residue).
-  // Element (c, i) lives on lane (q, p), register [t][s], and is never one
-  // that this loop rewrites.
-  {
-    const int tl = 8 * q + p;
-    sfor<0, NB>([&](auto sc) {
+  trinv2d<NB, G>(M, S, li, D);
+  sfor<0, NB>([&](auto tc) {
+    constexpr int t = decltype(tc)::value;
+    const int c = q + G * t;
+    const int col = ls_col<DM>(c) - c;
+    sfor<t, NB>([&](auto sc) {
       constexpr int s = decltype(sc)::value;
-      sfor<0, NB>([&](auto tc) {
-        constexpr int t = decltype(tc)::value;
-        const cf v = cf{__shfl(A.v[t][s].re, tl), __shfl(A.v[t][s].im, tl)};
-        A.v[s][t] = csel(p + 8 * s < q + 8 * t, conjg(v), A.v[s][t]);
-      });
-    });
-  }
-  // Li -> LDS (row-major, pitch DM + 1)
-  sfor<0, NB>([&](auto sc) {
-    constexpr int s = decltype(sc)::value;
-    sfor<0, NB>([&](auto tc) {
-      constexpr int t = decltype(tc)::value;
-      S.m.Ls[p + 8 * s][q + 8 * t] = Lf.v[s][t];
+      const int i = p + G * s;
+      if (s > t || i >= c) S.Ls[col + i] = cfk(M.v[s][t]);
     });
   });
   wsync();
-  // Z = A Li^H: Z[i][c] = sum_k A[i][k] conj(Li[c][k]), Li[c][k] = 0 for k > c
+  return ok;
+}
+
+// factor cache (kernels.hpp li_reusable): S.Ls and g as one contiguous
+// record per bin (li_record entries), copied with coalesced stores / loads
+template <int NB, int G = 8>
+constexpr int li_record() { return G * NB * (G * NB + 1) / 2 + bin_lanes<G>() * vpl<NB, G>(); }
+template <int NB, int G = 8>
+DANSE_DEV void li_store2d(const LDS2<NB, G>& S, cf* liC, int li) {
+  constexpr int NL = G * NB * (G * NB + 1) / 2, L = bin_lanes<G>();
+  for (int i = li; i < NL; i += L) liC[i] = S.Ls[i];
+  sfor<0, vpl<NB, G>()>([&](auto vc) { liC[NL + li + L * decltype(vc)::value] = S.g[li + L * decltype(vc)::value]; });
+}
+template <int NB, int G = 8>
+DANSE_DEV void li_load2d(LDS2<NB, G>& S, const cf* liC, int li) {
+  constexpr int NL = G * NB * (G * NB + 1) / 2, L = bin_lanes<G>();
+  for (int i = li; i < NL; i += L) S.Ls[i] = liC[i];
+  sfor<0, vpl<NB, G>()>([&](auto vc) { S.g[li + L * decltype(vc)::value] = liC[NL + li + L * decltype(vc)::value]; });
+  wsync();
+}
+
+// ---- C = Li A Li^H in place of A (float32); Li staged in LDS ---------------
+template <int NB, int G = 8>
+DANSE_DEV void congruence2d(Blk<NB>& A, LDS2<NB, G>& S, int li, int D) {
+  constexpr int DM = G * NB;
+  const int p = li / G, q = li % G;
+  // Z = A Li^H: Z[i][c] = sum_k A[i][k] conj(Li[c][k]), Li[c][k] = 0 for k > c.
+  // scipy.linalg.eigh reads the lower triangle, so A[i][k] = conj(A[k][i])
+  // for i < k (the SCMs are Hermitian except for the random init's residue).
+  // Block column sk of that Hermitian completion is staged in S.cz: entry
+  // (i, k = 8 sk + r) comes from lane (p, r) (i >= k) or, mirrored, from
+  // lane (r, q) (i < k); one LDS write pass per block, one read per k and
+  // block row instead of two bpermutes.
   Blk<NB> Z;
   sfor<0, NB>([&](auto sc) {
     sfor<0, NB>([&](auto tc) { Z.v[decltype(sc)::value][decltype(tc)::value] = cf{0.0f, 0.0f}; });
   });
   sfor<0, NB>([&](auto skc) {
     constexpr int sk = decltype(skc)::value;
-    for (int rk = 0; rk < 8; ++rk) {
-      const int k = 8 * sk + rk;
+    if (G * sk >= D) return;
+    wsync();   // the previous block's reads before this block's writes
+    sfor<0, NB>([&](auto sc) {
+      constexpr int s = decltype(sc)::value;
+      const int i = p + G * s;
+      if (i >= G * sk + q) S.cz[q][i] = A.v[s][sk];          // (i, 8 sk + q), lower
+      const int c = q + G * s;
+      if (c < G * sk + p) S.cz[p][c] = conjg(A.v[sk][s]);    // (c, 8 sk + p) from (8 sk + p, c)
+    });
+    wsync();
+    for (int rk = 0; rk < G; ++rk) {
+      const int k = G * sk + rk;
       if (k >= D) break;
-      const int src = (li & ~7) | rk;   // lane (p, rk) holds A[p + 8 s][k]
       cf ak[NB], lc[NB];
       sfor<0, NB>([&](auto sc) {
         constexpr int s = decltype(sc)::value;
-        ak[s] = cf{__shfl(A.v[s][sk].re, src), __shfl(A.v[s][sk].im, src)};
+        ak[s] = S.cz[rk][p + G * s];
       });
       sfor<sk, NB>([&](auto tc) {
         constexpr int t = decltype(tc)::value;
-        lc[t] = S.m.Ls[q + 8 * t][k];
+        lc[t] = ls_get<DM>(S.Ls, q + G * t, k);
       });
       sfor<0, NB>([&](auto sc) {
         constexpr int s = decltype(sc)::value;
         sfor<sk, NB>([&](auto tc) {
           constexpr int t = decltype(tc)::value;
-          cf z = Z.v[s][t];
-          z.re = fmaf(ak[s].re, lc[t].re, fmaf(ak[s].im, lc[t].im, z.re));
-          z.im = fmaf(ak[s].im, lc[t].re, fmaf(-ak[s].re, lc[t].im, z.im));
-          Z.v[s][t] = z;
+          pk_fma_cc(Z.v[s][t], ak[s], lc[t]);
         });
       });
     }
   });
-  // C = Li Z: C[i][c] = sum_k Li[i][k] Z[k][c], Li[i][k] = 0 for k > i  (into A)
+  // C = Li Z: C[i][c] = sum_k Li[i][k] Z[k][c], Li[i][k] = 0 for k > i  (into A);
+  // block row sk of Z staged in S.cz the same way
   sfor<0, NB>([&](auto sc) {
     sfor<0, NB>([&](auto tc) { A.v[decltype(sc)::value][decltype(tc)::value] = cf{0.0f, 0.0f}; });
   });
   sfor<0, NB>([&](auto skc) {
     constexpr int sk = decltype(skc)::value;
-    for (int rk = 0; rk < 8; ++rk) {
-      const int k = 8 * sk + rk;
+    if (G * sk >= D) return;
+    wsync();
+    sfor<0, NB>([&](auto tc) {
+      constexpr int t = decltype(tc)::value;
+      S.cz[p][q + G * t] = Z.v[sk][t];
+    });
+    wsync();
+    for (int rk = 0; rk < G; ++rk) {
+      const int k = G * sk + rk;
       if (k >= D) break;
-      const int src = rk * 8 + q;   // lane (rk, q) holds Z[k][q + 8 t]
       cf zk[NB], lr[NB];
       sfor<0, NB>([&](auto tc) {
         constexpr int t = decltype(tc)::value;
-        zk[t] = cf{__shfl(Z.v[sk][t].re, src), __shfl(Z.v[sk][t].im, src)};
+        zk[t] = S.cz[rk][q + G * t];
       });
       sfor<sk, NB>([&](auto sc) {
         constexpr int s = decltype(sc)::value;
-        lr[s] = S.m.Ls[p + 8 * s][k];
+        lr[s] = ls_get<DM>(S.Ls, p + G * s, k);
       });
       sfor<sk, NB>([&](auto sc) {
         constexpr int s = decltype(sc)::value;
         sfor<0, NB>([&](auto tc) {
           constexpr int t = decltype(tc)::value;
-          fma_c(A.v[s][t], lr[s], zk[t]);
+          pk_fma_c(A.v[s][t], lr[s], zk[t]);
         });
       });
     }
@@ -336,27 +421,26 @@ DANSE_DEV void congruence2d(Blk<NB>& A, const Blk<NB>& Lf, LDS2<NB>& S, int li, 
     constexpr int s = decltype(sc)::value;
     if (p == q) A.v[s][s].im = 0.0f;
   });
-  wsync();   // every Ls read before the Householder vectors overwrite it
 }
 
 // ---- Householder tridiagonalisation of the Hermitian block A (destroyed):
-// diagonal -> S.a, subdiagonal -> S.b, reflectors -> S.m.U[j][*]
-template <int NB>
-DANSE_DEV void tridiag2d(Blk<NB>& A, LDS2<NB>& S, int li, int D) {
-  constexpr int DM = 8 * NB;
-  const int p = li >> 3, q = li & 7;
+// diagonal -> S.a, subdiagonal -> S.b, reflectors -> S.U (u_row)
+template <int NB, int G = 8>
+DANSE_DEV void tridiag2d(Blk<NB>& A, LDS2<NB, G>& S, int li, int D) {
+  constexpr int DM = G * NB;
+  const int p = li / G, q = li % G;
   int buf = 0;
   cf ph = cf{1.0f, 0.0f};   // phi_j (wave-uniform)
   if (li == 0) S.phi[0] = ph;
   sfor<0, NB>([&](auto sjc) {
     constexpr int sj = decltype(sjc)::value;
-    for (int rj = 0; rj < 8; ++rj) {
-      const int j = 8 * sj + rj;
+    for (int rj = 0; rj < G; ++rj) {
+      const int j = G * sj + rj;
       if (j + 2 >= D) break;
       if (q == rj) {
         sfor<sj, NB>([&](auto sc) {
           constexpr int s = decltype(sc)::value;
-          const int i = p + 8 * s;
+          const int i = p + G * s;
           S.cb[buf][i] = csel(i > j, A.v[s][sj], cf{0.0f, 0.0f});
         });
         if (p == rj) S.a[j] = A.v[sj][sj].re;
@@ -365,13 +449,13 @@ DANSE_DEV void tridiag2d(Blk<NB>& A, LDS2<NB>& S, int li, int D) {
       cf xr[NB], xc[NB];
       sfor<sj, NB>([&](auto sc) {
         constexpr int s = decltype(sc)::value;
-        xr[s] = S.cb[buf][p + 8 * s];
-        xc[s] = S.cb[buf][q + 8 * s];
+        xr[s] = S.cb[buf][p + G * s];
+        xc[s] = S.cb[buf][q + G * s];
       });
       const cf x0 = S.cb[buf][j + 1];
       float n2 = 0.0f;
       sfor<sj, NB>([&](auto tc) { n2 += abs2(xc[decltype(tc)::value]); });
-      const float nrm2 = sumq(n2);
+      const float nrm2 = sumq<G>(n2);
       const float ax02 = abs2(x0);
       const float nx = fsqrt(nrm2);
       const float ax0 = fsqrt(ax02);
@@ -384,14 +468,15 @@ DANSE_DEV void tridiag2d(Blk<NB>& A, LDS2<NB>& S, int li, int D) {
       cf ur[NB], uc[NB];
       sfor<sj, NB>([&](auto sc) {
         constexpr int s = decltype(sc)::value;
-        ur[s] = invn * csel(p + 8 * s == j + 1, xr[s] + ne, xr[s]);
-        uc[s] = invn * csel(q + 8 * s == j + 1, xc[s] + ne, xc[s]);
+        ur[s] = invn * csel(p + G * s == j + 1, xr[s] + ne, xr[s]);
+        uc[s] = invn * csel(q + G * s == j + 1, xc[s] + ne, xc[s]);
       });
       if (q == 0) {
-        sfor<0, NB>([&](auto sc) {
+        const int ub = u_row<DM>(j);
+        sfor<sj, NB>([&](auto sc) {
           constexpr int s = decltype(sc)::value;
-          if constexpr (s < sj) S.m.U[j][p + 8 * s] = cf{0.0f, 0.0f};
-          else S.m.U[j][p + 8 * s] = ur[s];
+          const int i = p + G * s;
+          if (i > j) S.U[ub + i] = ur[s];
         });
       }
       // p = C u (rows > j); its column-layout copy through LDS gives
@@ -402,12 +487,12 @@ DANSE_DEV void tridiag2d(Blk<NB>& A, LDS2<NB>& S, int li, int D) {
         cf acc = cf{0.0f, 0.0f};
         sfor<sj, NB>([&](auto tc) {
           constexpr int t = decltype(tc)::value;
-          fma_c(acc, A.v[s][t], uc[t]);
+          pk_fma_c(acc, A.v[s][t], uc[t]);
         });
-        acc = sumq(acc);
-        acc = csel(p + 8 * s > j, acc, cf{0.0f, 0.0f});
+        acc = sumq<G>(acc);
+        acc = csel(p + G * s > j, acc, cf{0.0f, 0.0f});
         pr[s] = acc;
-        if (q == 0) S.qb[buf][p + 8 * s] = acc;
+        if (q == 0) S.qb[buf][p + G * s] = acc;
       });
       // phase of the subdiagonal: phi_{j+1} = phi_j b_{j+1} / |b_{j+1}|
       {
@@ -422,10 +507,10 @@ DANSE_DEV void tridiag2d(Blk<NB>& A, LDS2<NB>& S, int li, int D) {
       float kp = 0.0f;
       sfor<sj, NB>([&](auto tc) {
         constexpr int t = decltype(tc)::value;
-        pc[t] = S.qb[buf][q + 8 * t];
+        pc[t] = S.qb[buf][q + G * t];
         kp += cmul(uc[t], pc[t]).re;
       });
-      const float Kr = sumq(kp);
+      const float Kr = sumq<G>(kp);
       sfor<sj, NB>([&](auto tc) {
         constexpr int t = decltype(tc)::value;
         const cf qc = pc[t] - Kr * uc[t];
@@ -434,8 +519,8 @@ DANSE_DEV void tridiag2d(Blk<NB>& A, LDS2<NB>& S, int li, int D) {
           constexpr int s = decltype(sc)::value;
           const cf qrs = pr[s] - Kr * ur[s];
           cf x = A.v[s][t];
-          fms_cc(x, ur[s], q2c);
-          fms_cc(x, qrs, u2c);
+          pk_fms_cc(x, ur[s], q2c);
+          pk_fms_cc(x, qrs, u2c);
           A.v[s][t] = x;
         });
       });
@@ -447,7 +532,7 @@ DANSE_DEV void tridiag2d(Blk<NB>& A, LDS2<NB>& S, int li, int D) {
     constexpr int s = decltype(sc)::value;
     sfor<0, NB>([&](auto tc) {
       constexpr int t = decltype(tc)::value;
-      const int i = p + 8 * s, c = q + 8 * t;
+      const int i = p + G * s, c = q + G * t;
       if (i == c && i >= D - 2 && i < D) S.a[i] = A.v[s][t].re;
       if (i == D - 1 && c == D - 2) S.b[i] = A.v[s][t];
     });
@@ -462,11 +547,14 @@ DANSE_DEV void tridiag2d(Blk<NB>& A, LDS2<NB>& S, int li, int D) {
     if (li == 0) S.phi[D - 1] = ph;
   }
   // the tridiagonal for the eigen part: S.ev[i] = |b_{i+1}|, S.e2[i] = |b_{i+1}|^2
-  if (li < DM) {
-    const float e2 = (li + 1 < D) ? abs2(S.b[li + 1]) : 0.0f;
-    S.e2[li] = e2;
-    S.ev[li] = fsqrt(e2);
-  }
+  sfor<0, vpl<NB, G>()>([&](auto vc) {
+    const int i = li + bin_lanes<G>() * decltype(vc)::value;
+    if (i < DM) {
+      const float e2 = (i + 1 < D) ? abs2(S.b[i + 1]) : 0.0f;
+      S.e2[i] = e2;
+      S.ev[i] = fsqrt(e2);
+    }
+  });
   wsync();
 }
 
@@ -490,34 +578,47 @@ DANSE_DEV int sturm2d(const float* a, const float* e2, int D, float x, float piv
   return cnt;
 }
 
-// top-R eigenvalues by 64-point multisection (solver64.hpp::top_eigvals)
-template <int DM, int RMAX>
-DANSE_DEV void top_eigvals2d(const float* a, const float* e2, float ta, float te2, int li, int D, int R,
-                             float (&lam)[kRMax], float& tnorm) {
-  const bool act = li < D;
-  const float e2m = __shfl_up(te2, 1);
-  const float em = (li >= 1 && act) ? fsqrt(e2m) : 0.0f;
-  const float ep = (li + 1 < D) ? fsqrt(te2) : 0.0f;
-  const float lo0 = gmin<64>(act ? ta - em - ep : 3.0e38f);
-  const float hi0 = gmax<64>(act ? ta + em + ep : -3.0e38f);
-  const float e2max = gmax<64>((li + 1 < D) ? te2 : 0.0f);
-  tnorm = gmax<64>(act ? fabsf(ta) + em + ep : 0.0f);
+// top-R eigenvalues by (L)-point multisection over the bin's L lanes
+// (solver64.hpp::top_eigvals): 5 rounds of 64 points (G = 8), 8 rounds of
+// 16 points (G = 4); lane li holds the tridiagonal entries li + L v
+template <int DM, int RMAX, int G>
+DANSE_DEV void top_eigvals2d(const float* a, const float* e2, int li, int D, int R, float (&lam)[kRMax],
+                             float& tnorm) {
+  constexpr int L = bin_lanes<G>(), V = (DM + L - 1) / L;
+  float lo1 = 3.0e38f, hi1 = -3.0e38f, e2m1 = 0.0f, tn1 = 0.0f;
+  sfor<0, V>([&](auto vc) {
+    const int i = li + L * decltype(vc)::value;
+    const bool act = i < D;
+    const float ta = act ? a[i] : 0.0f;
+    const float te2 = (i + 1 < D) ? e2[i] : 0.0f;
+    const float em = (i >= 1 && act) ? fsqrt(e2[i >= 1 ? i - 1 : 0]) : 0.0f;
+    const float ep = (i + 1 < D) ? fsqrt(te2) : 0.0f;
+    lo1 = fminf(lo1, act ? ta - em - ep : 3.0e38f);
+    hi1 = fmaxf(hi1, act ? ta + em + ep : -3.0e38f);
+    e2m1 = fmaxf(e2m1, (i + 1 < D) ? te2 : 0.0f);
+    tn1 = fmaxf(tn1, act ? fabsf(ta) + em + ep : 0.0f);
+  });
+  const float lo0 = gmin<L>(lo1);
+  const float hi0 = gmax<L>(hi1);
+  const float e2max = gmax<L>(e2m1);
+  tnorm = gmax<L>(tn1);
   const float scale = fmaxf(fabsf(lo0), fabsf(hi0));
   const float pivmin = 1.0e-30f * fmaxf(1.0f, e2max);
   float lo = lo0 - (2.0f * 1.2e-7f * scale + pivmin);
   float hi = hi0 + (2.0f * 1.2e-7f * scale + pivmin);
+  constexpr int kRounds = (G == 8) ? 5 : 8;
   sfor<0, RMAX>([&](auto rc) {
     constexpr int r = decltype(rc)::value;
     if (r >= R) return;
     float al = lo, bl = hi;
     const int target = D - r;   // count(x) >= target  <=>  x > lambda_r
-    for (int it = 0; it < 5; ++it) {
-      const float step = (bl - al) * (1.0f / 65.0f);
+    for (int it = 0; it < kRounds; ++it) {
+      const float step = (bl - al) * (1.0f / (float)(L + 1));
       const float x = al + step * (float)(li + 1);
       const int cnt = sturm2d<DM>(a, e2, D, x, pivmin);
-      const uint64_t m = __ballot(cnt >= target);
+      const uint64_t m = gballot<L>(cnt >= target);
       if (m == 0ull) {
-        al = al + step * 64.0f;
+        al = al + step * (float)L;
       } else {
         const int first = __builtin_ctzll(m);
         const float na = al + step * (float)first;
@@ -530,18 +631,22 @@ DANSE_DEV void top_eigvals2d(const float* a, const float* e2, float ta, float te
   });
 }
 
-// Eigenvector x_li of the tridiagonal for eigenvalue lam: two sweeps of
-// inverse iteration with partial pivoting (solver64.hpp::tri_eigvec), the
-// elimination computed redundantly by every lane from LDS (wave-uniform
-// values, no readlane / lane-select chains), the eliminated rows kept in LDS
-// for the back substitution.
-template <int DM>
-DANSE_DEV float tri_eigvec2d(const float* a, const float* ev, float4* fac, float* xs, int li, int D, float lam,
-                             float pert, int r, const float (*prev)[DM]) {
-  float x = (li < D) ? 1.0f + 0.1f * (float)((li * 7919 + r * 104729) % 13) / 13.0f : 0.0f;
+// Eigenvector of the tridiagonal for eigenvalue lam (entries li + L v of
+// lane li): two sweeps of inverse iteration with partial pivoting
+// (solver64.hpp::tri_eigvec), the elimination computed redundantly by every
+// lane from LDS (bin-uniform values, no readlane / lane-select chains), the
+// eliminated rows kept in LDS for the back substitution.
+template <int DM, int G>
+DANSE_DEV void tri_eigvec2d(const float* a, const float* ev, float4* fac, float* xs, int li, int D, float lam,
+                            float pert, int r, const float (*prev)[DM], float (&x)[(DM + G * G - 1) / (G * G)]) {
+  constexpr int L = bin_lanes<G>(), V = (DM + L - 1) / L;
+  sfor<0, V>([&](auto vc) {
+    const int i = li + L * decltype(vc)::value;
+    x[decltype(vc)::value] = (i < D) ? 1.0f + 0.1f * (float)((i * 7919 + r * 104729) % 13) / 13.0f : 0.0f;
+  });
   for (int it = 0; it < 2; ++it) {
     if (it > 0) {
-      if (li < 64) xs[li] = x;
+      sfor<0, V>([&](auto vc) { xs[li + L * decltype(vc)::value] = x[decltype(vc)::value]; });
       wsync();
     }
     auto rhs = [&](int i) {
@@ -570,7 +675,8 @@ DANSE_DEV float tri_eigvec2d(const float* a, const float* ev, float4* fac, float
     });
     if (li == 0) fac[D - 1] = make_float4(dc, 0.0f, 0.0f, rc);
     wsync();
-    float xn1 = 0.0f, xn2 = 0.0f, sol = 0.0f;
+    float xn1 = 0.0f, xn2 = 0.0f, sol[V];
+    sfor<0, V>([&](auto vc) { sol[decltype(vc)::value] = 0.0f; });
     sfor_down<DM, 0>([&](auto ic) {
       constexpr int i = decltype(ic)::value;
       const float4 fr = fac[i];
@@ -578,40 +684,58 @@ DANSE_DEV float tri_eigvec2d(const float* a, const float* ev, float4* fac, float
       const float di = (fr.x == 0.0f) ? pert : fr.x;
       const float xi = acc * frcp(di);
       const bool on = i < D;
-      sol = (on && li == i) ? xi : sol;
+      sfor<0, V>([&](auto vc) {
+        constexpr int v = decltype(vc)::value;
+        sol[v] = (on && li + L * v == i) ? xi : sol[v];
+      });
       xn2 = on ? xn1 : xn2;
       xn1 = on ? xi : xn1;
     });
     for (int qq = 0; qq < r; ++qq) {
-      const float pq = (li < DM) ? prev[qq][li] : 0.0f;
-      const float dot = gsum<64>(pq * sol);
-      sol -= dot * pq;
+      float pq[V], dp = 0.0f;
+      sfor<0, V>([&](auto vc) {
+        constexpr int v = decltype(vc)::value;
+        const int i = li + L * v;
+        pq[v] = (i < DM) ? prev[qq][i < DM ? i : 0] : 0.0f;
+        dp = (v == 0) ? pq[v] * sol[v] : dp + pq[v] * sol[v];
+      });
+      const float dot = gsum<L>(dp);
+      sfor<0, V>([&](auto vc) { sol[decltype(vc)::value] -= dot * pq[decltype(vc)::value]; });
     }
-    const float mx0 = gmax<64>(fabsf(sol));
+    float am = 0.0f;
+    sfor<0, V>([&](auto vc) { am = (decltype(vc)::value == 0) ? fabsf(sol[0]) : fmaxf(am, fabsf(sol[decltype(vc)::value])); });
+    const float mx0 = gmax<L>(am);
     const float mx = (mx0 > 0.0f) ? mx0 : 1.0f;
-    sol *= frcp(mx);
-    const float nrm = gsum<64>(sol * sol);
-    x = sol * frsq(nrm);
+    float n2 = 0.0f;
+    sfor<0, V>([&](auto vc) {
+      constexpr int v = decltype(vc)::value;
+      sol[v] *= frcp(mx);
+      n2 = (v == 0) ? sol[v] * sol[v] : n2 + sol[v] * sol[v];
+    });
+    const float nrm = gsum<L>(n2);
+    sfor<0, V>([&](auto vc) { x[decltype(vc)::value] = sol[decltype(vc)::value] * frsq(nrm); });
     wsync();   // fac / xs reads before the next sweep rewrites them
   }
-  return x;
 }
 
 // ---- eigen part, back-transform, x = Li^H v,
-// w = sum_r (1 - 1/lambda_r) x_r (x_r^H Rnn e_ref)
-template <int NB, int RMAX>
-DANSE_DEV cf eigen2d(const Blk<NB>& Lf, LDS2<NB>& S, int li, int D, int R) {
-  constexpr int DM = 8 * NB;
-  const int p = li >> 3, q = li & 7;
-  const bool act = li < D;
-  const float ta = act ? S.a[li] : 0.0f;
-  const float te2 = (li + 1 < D) ? S.e2[li] : 0.0f;
+// w = sum_r (1 - 1/lambda_r) x_r (x_r^H Rnn e_ref); w[v] = entry li + L v
+template <int NB, int RMAX, int G = 8>
+DANSE_DEV void eigen2d(LDS2<NB, G>& S, int li, int D, int R, cf (&w)[vpl<NB, G>()]) {
+  constexpr int DM = G * NB, L = bin_lanes<G>(), V = vpl<NB, G>();
+  const int p = li / G, q = li % G;
   float lam[kRMax];
   float tnorm;
-  top_eigvals2d<DM, RMAX>(S.a, S.e2, ta, te2, li, D, R, lam, tnorm);
+  top_eigvals2d<DM, RMAX, G>(S.a, S.e2, li, D, R, lam, tnorm);
   const float pert = 1.2e-7f * fmaxf(tnorm, 1e-30f);
-  const cf gl = S.g[li];
-  const cf phl = csel(act, S.phi[act ? li : 0], cf{0.0f, 0.0f});
+  cf gl[V], phl[V];
+  sfor<0, V>([&](auto vc) {
+    constexpr int v = decltype(vc)::value;
+    const int i = li + L * v;
+    const bool act = i < D;
+    gl[v] = S.g[i];
+    phl[v] = csel(act, S.phi[act ? i : 0], cf{0.0f, 0.0f});
+  });
   cf wc[NB];
   sfor<0, NB>([&](auto tc) { wc[decltype(tc)::value] = cf{0.0f, 0.0f}; });
   sfor<0, RMAX>([&](auto rc) {
@@ -619,25 +743,46 @@ DANSE_DEV cf eigen2d(const Blk<NB>& Lf, LDS2<NB>& S, int li, int D, int R) {
     if constexpr (r > 0) {
       if (r >= R) return;
     }
-    const float x = tri_eigvec2d<DM>(S.a, S.ev, S.fac, S.xs, li, D, lam[r], pert, r, S.x);
-    cf v = x * phl;
+    float x[V];
+    tri_eigvec2d<DM, G>(S.a, S.ev, S.fac, S.xs, li, D, lam[r], pert, r, S.x, x);
+    cf vv[V];
+    sfor<0, V>([&](auto vc) { vv[decltype(vc)::value] = x[decltype(vc)::value] * phl[decltype(vc)::value]; });
     if (r + 1 < R) {
-      if (li < DM) S.x[r][li] = x;
+      sfor<0, V>([&](auto vc) {
+        const int i = li + L * decltype(vc)::value;
+        if (i < DM) S.x[r][i] = x[decltype(vc)::value];
+      });
       wsync();
     }
     for (int j = D - 3; j >= 0; --j) {
-      const cf u = (li < DM ? 1.0f : 0.0f) * S.m.U[j][li < DM ? li : 0];
-      const cf sdot = gsum<64>(cmul(u, v));
-      fms_c(v, 2.0f * u, sdot);
+      cf u[V], sd;
+      sfor<0, V>([&](auto vc) {
+        constexpr int v = decltype(vc)::value;
+        const int i = li + L * v;
+        const bool in = i > j && i < DM;
+        u[v] = csel(in, S.U[in ? u_row<DM>(j) + i : 0], cf{0.0f, 0.0f});
+        const cf t = cmul(u[v], vv[v]);
+        sd = (v == 0) ? t : sd + t;
+      });
+      const cf sdot = gsum<L>(sd);
+      sfor<0, V>([&](auto vc) { fms_c(vv[decltype(vc)::value], 2.0f * u[decltype(vc)::value], sdot); });
     }
-    const cf sr = gsum<64>(cmul(v, gl));
+    cf sg;
+    sfor<0, V>([&](auto vc) {
+      const cf t = cmul(vv[decltype(vc)::value], gl[decltype(vc)::value]);
+      sg = (decltype(vc)::value == 0) ? t : sg + t;
+    });
+    const cf sr = gsum<L>(sg);
     // x = Li^H v: x_c = sum_i conj(Li[i][c]) v_i (column layout)
-    S.vb[li] = v;
+    sfor<0, V>([&](auto vc) {
+      const int i = li + L * decltype(vc)::value;
+      if (i < DM) S.vb[i] = vv[decltype(vc)::value];
+    });
     wsync();
     cf vr[NB];
     sfor<0, NB>([&](auto sc) {
       constexpr int s = decltype(sc)::value;
-      vr[s] = S.vb[p + 8 * s];
+      vr[s] = S.vb[p + G * s];
     });
     const float coef = 1.0f - frcp(lam[r]);
     sfor<0, NB>([&](auto tc) {
@@ -645,9 +790,9 @@ DANSE_DEV cf eigen2d(const Blk<NB>& Lf, LDS2<NB>& S, int li, int D, int R) {
       cf acc = cf{0.0f, 0.0f};
       sfor<t, NB>([&](auto sc) {   // Li[i][c] = 0 for i < c
         constexpr int s = decltype(sc)::value;
-        acc = acc + cmul(Lf.v[s][t], vr[s]);
+        acc = acc + cmul(ls_get<DM>(S.Ls, p + G * s, q + G * t), vr[s]);
       });
-      acc = sump(acc);
+      acc = sump<G>(acc);
       wc[t] = wc[t] + coef * (acc * sr);
     });
     wsync();   // vb reads before the next rank's write
@@ -655,20 +800,22 @@ DANSE_DEV cf eigen2d(const Blk<NB>& Lf, LDS2<NB>& S, int li, int D, int R) {
   if (p == 0) {
     sfor<0, NB>([&](auto tc) {
       constexpr int t = decltype(tc)::value;
-      S.wb[q + 8 * t] = wc[t];
+      S.wb[q + G * t] = wc[t];
     });
   }
   wsync();
-  const cf w = S.wb[li];
-  return csel(act, w, cf{0.0f, 0.0f});
+  sfor<0, V>([&](auto vc) {
+    const int i = li + L * decltype(vc)::value;
+    w[decltype(vc)::value] = (i < D) ? S.wb[i < D ? i : 0] : cf{0.0f, 0.0f};
+  });
 }
 
-// ---- phase 2: A = Ryy block (float32, destroyed), Lf = Li -> w (lane layout)
-template <int NB, int RMAX>
-DANSE_DEV cf gevd2d_filter(Blk<NB>& A, const Blk<NB>& Lf, LDS2<NB>& S, int li, int D, int R) {
-  congruence2d<NB>(A, Lf, S, li, D);
-  tridiag2d<NB>(A, S, li, D);
-  return eigen2d<NB, RMAX>(Lf, S, li, D, R);
+// ---- phase 2: A = Ryy block (float32, destroyed), Li in S.Ls -> w[v] = entry li + L v
+template <int NB, int RMAX, int G = 8>
+DANSE_DEV void gevd2d_filter(Blk<NB>& A, LDS2<NB, G>& S, int li, int D, int R, cf (&w)[vpl<NB, G>()]) {
+  congruence2d<NB, G>(A, S, li, D);
+  tridiag2d<NB, G>(A, S, li, D);
+  eigen2d<NB, RMAX, G>(S, li, D, R, w);
 }
 
 }  // namespace t2d

@@ -150,7 +150,7 @@ DANSE_DEV void congruence(PTri<D>& A, const LM& Li) {
       cf acc = cf{0.0f, 0.0f};
       sfor<0, j + 1>([&](auto kc) {
         constexpr int k = decltype(kc)::value;
-        acc = acc + mulc(herm<i, k>(A), Li.template at<j, k>());
+        herm_mac<i, k, true, false>(acc, A, Li.template at<j, k>());
       });
       u[i] = acc;
     });
@@ -160,7 +160,7 @@ DANSE_DEV void congruence(PTri<D>& A, const LM& Li) {
       cf acc = cf{0.0f, 0.0f};
       sfor<0, i + 1>([&](auto kc) {
         constexpr int k = decltype(kc)::value;
-        fma_c(acc, Li.template at<i, k>(), u[k]);
+        cmac<false, false, false>(acc, Li.template at<i, k>(), u[k]);
       });
       if constexpr (i == j) acc.im = 0.0f;
       A.a[P(i, j)] = acc;
@@ -184,7 +184,7 @@ DANSE_DEV void gevd_filter_mixed(PTri<D>& A, const LM& Li, const cf (&g)[D], int
       cf x = cf{0.0f, 0.0f};
       sfor<i, D>([&](auto kc) {
         constexpr int k = decltype(kc)::value;
-        x = x + cmul(Li.template at<k, i>(), v[k]);
+        cmac<true, false, false>(x, Li.template at<k, i>(), v[k]);
       });
       fma_c(wv[i], x, cs);
     });

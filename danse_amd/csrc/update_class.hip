@@ -6,7 +6,7 @@
 #include "kernels_lane.hpp"
 
 #ifndef DANSE_DMAX
-#error "compile with -DDANSE_DMAX=<1..12, 16..64 step 8>"
+#error "compile with -DDANSE_DMAX=<1..12, 16, 20, 24..64 step 8>"
 #endif
 
 namespace danse {
@@ -14,9 +14,15 @@ namespace danse {
 namespace {
 constexpr int kD = DANSE_DMAX;
 constexpr int kG = class_group(kD);
-// GEVD of the wavefront classes up to 48 on the 8 x 8 lane grid (kernels_2d.hpp)
-constexpr bool k2D = (kG == 64) && kD <= 48;
-constexpr int kNB = k2D ? kD / 8 : 2;
+static_assert(class_dmax(kD) == kD, "DANSE_DMAX is not a class size");
+// GEVD of the wavefront classes up to 48 on a lane grid (kernels_2d.hpp):
+// 4 x 4 (four bins per wave) for DMAX 16 / 20, 8 x 8 above
+constexpr int kGrid = class_grid(kD);
+constexpr bool k2D = (kG == 64) && kGrid > 0;
+constexpr int kNB = k2D ? kD / kGrid : 2;
+constexpr int kBinsPerWave = (kGrid == 4) ? 4 : 1;
+// the row-per-lane kernels (MWF of D > 12) unroll over multiples of 8
+constexpr int kDBig = ((kD + 7) / 8) * 8;
 static_assert(kD >= 1 && kD <= kMaxDMax, "class out of range");
 }  // namespace
 
@@ -34,13 +40,14 @@ void DANSE_CAT(launch_update_d, DANSE_DMAX)(const UpdateArgs& a, hipStream_t st)
   } else if constexpr (kG == 64) {
     const unsigned grid = (unsigned)(a.S * a.nFN * a.F);
     if (!a.gevd) {
-      hipLaunchKernelGGL((update_kernel_big<kD, 1, false>), dim3(grid), dim3(64), 0, st, a);
+      hipLaunchKernelGGL((update_kernel_big<kDBig, 1, false>), dim3(grid), dim3(64), 0, st, a);
     } else if constexpr (k2D) {
-      if (r1) hipLaunchKernelGGL((update_kernel_2d<kNB, 1>), dim3(grid), dim3(64), 0, st, a);
-      else hipLaunchKernelGGL((update_kernel_2d<kNB, kRMax>), dim3(grid), dim3(64), 0, st, a);
+      const unsigned g2 = (unsigned)(a.S * a.nFN * ((a.F + kBinsPerWave - 1) / kBinsPerWave));
+      if (r1) hipLaunchKernelGGL((update_kernel_2d<kNB, 1, kGrid>), dim3(g2), dim3(64), 0, st, a);
+      else hipLaunchKernelGGL((update_kernel_2d<kNB, kRMax, kGrid>), dim3(g2), dim3(64), 0, st, a);
     } else {
-      if (r1) hipLaunchKernelGGL((update_kernel_big<kD, 1, true>), dim3(grid), dim3(64), 0, st, a);
-      else hipLaunchKernelGGL((update_kernel_big<kD, kRMax, true>), dim3(grid), dim3(64), 0, st, a);
+      if (r1) hipLaunchKernelGGL((update_kernel_big<kDBig, 1, true>), dim3(grid), dim3(64), 0, st, a);
+      else hipLaunchKernelGGL((update_kernel_big<kDBig, kRMax, true>), dim3(grid), dim3(64), 0, st, a);
     }
   }
 }
@@ -59,21 +66,22 @@ void DANSE_CAT(launch_filter_update_d, DANSE_DMAX)(const cd* Ryy, const cd* Rnn,
   } else if constexpr (kG == 64) {
     const unsigned grid = (unsigned)B;
     if (!gevd) {
-      hipLaunchKernelGGL((filter_update_kernel_big<kD, 1, false>), dim3(grid), dim3(64), 0, st, Ryy, Rnn, B, D, gevd,
+      hipLaunchKernelGGL((filter_update_kernel_big<kDBig, 1, false>), dim3(grid), dim3(64), 0, st, Ryy, Rnn, B, D, gevd,
                          rank, ref, w, diag);
     } else if constexpr (k2D) {
+      const unsigned g2 = (unsigned)((B + kBinsPerWave - 1) / kBinsPerWave);
       if (r1)
-        hipLaunchKernelGGL((filter_update_kernel_2d<kNB, 1>), dim3(grid), dim3(64), 0, st, Ryy, Rnn, B, D, rank, ref,
-                           w, diag);
-      else
-        hipLaunchKernelGGL((filter_update_kernel_2d<kNB, kRMax>), dim3(grid), dim3(64), 0, st, Ryy, Rnn, B, D, rank,
+        hipLaunchKernelGGL((filter_update_kernel_2d<kNB, 1, kGrid>), dim3(g2), dim3(64), 0, st, Ryy, Rnn, B, D, rank,
                            ref, w, diag);
+      else
+        hipLaunchKernelGGL((filter_update_kernel_2d<kNB, kRMax, kGrid>), dim3(g2), dim3(64), 0, st, Ryy, Rnn, B, D,
+                           rank, ref, w, diag);
     } else {
       if (r1)
-        hipLaunchKernelGGL((filter_update_kernel_big<kD, 1, true>), dim3(grid), dim3(64), 0, st, Ryy, Rnn, B, D, gevd,
+        hipLaunchKernelGGL((filter_update_kernel_big<kDBig, 1, true>), dim3(grid), dim3(64), 0, st, Ryy, Rnn, B, D, gevd,
                            rank, ref, w, diag);
       else
-        hipLaunchKernelGGL((filter_update_kernel_big<kD, kRMax, true>), dim3(grid), dim3(64), 0, st, Ryy, Rnn, B, D,
+        hipLaunchKernelGGL((filter_update_kernel_big<kDBig, kRMax, true>), dim3(grid), dim3(64), 0, st, Ryy, Rnn, B, D,
                            gevd, rank, ref, w, diag);
     }
   }

@@ -86,7 +86,7 @@ def test_get_metrics_vs_reference(golden_dir):
             v, r = getattr(m[key], fld), float(g[f'{key}_{fld}'])
             assert abs(v - r) <= 1e-9 * max(1.0, abs(r)), (key, fld, v, r)
     with pytest.raises(NotImplementedError):
-        DM.get_metrics(**get_metrics_inputs(case), fs=case['fs'], metricsToPlot=['stoi'])
+        DM.get_metrics(**get_metrics_inputs(case), fs=case['fs'], metricsToPlot=['pesq'])
 
 
 # ---- (e)STOI (csrc/stoi.hip, danse_stoi) ----------------------------------
