@@ -239,7 +239,7 @@ def make_scenes_device(nSensorPerNode, S, sigDur=10.0, fs=16000.0, seed=0, snr=5
                                   st)
     if rc != 0:
         raise L.DanseError((lib.danse_scene_last_error() or b'').decode() or f'error {rc}')
-    vad = out['vad'].cpu().numpy()
+    vad = out['vad'].cpu().numpy()   # 0/1 (uint8 on the device; float64 per node, as make_scene)
     host = {key: out[key].cpu().numpy() for key in ('data', 'cleanspeech', 'cleannoise')} if host_signals else None
     base = np.concatenate(([0], np.cumsum(M)[:-1])).astype(int)
     scenes = []
@@ -251,6 +251,6 @@ def make_scenes_device(nSensorPerNode, S, sigDur=10.0, fs=16000.0, seed=0, snr=5
             sig = {key: (host[key][s, sl].T if host is not None else None) for key in ('data', 'cleanspeech', 'cleannoise')}
             wasn.append(SceneNode(index=k, nSensors=M[k], fs=fsSRO, timeStamps=np.arange(T) / fsSRO,
                                   neighborsIdx=[q for q in range(K) if q != k], sro=float(sros[k]),
-                                  vad=vad[s, k][:, None], **sig))
+                                  vad=vad[s, k][:, None].astype(np.float64), **sig))
         scenes.append(Scene(wasn=wasn, fs=fs, seed=seed + s))
     return scenes, out
