@@ -237,6 +237,8 @@ def main():
         # single-WASN lines: config B at S=1 and the
         # north_star headline shape N2 (online K=32 x 8, D=39) at S=1
         extra['B_S1'] = run_online(args, wl, 1, rank, world, local, dist, traffic=False)
+        # the latency layout for one WASN: D = 11 on the 4 x 4 lane-grid solver
+        extra['B_S1_grid'] = run_online(args, wl, 1, rank, world, local, dist, traffic=False, small_grid=True)
         extra['N2'] = run_online(args, WORKLOADS['N2'], 1, rank, world, local, dist)
     cpu = {}
     if rank == 0 and not args.no_cpu_baseline:
@@ -267,7 +269,7 @@ def main():
             line['extra_lines'] = {}
             for key, r in extra.items():
                 c = cpu.get(key)
-                if key == 'B_S1':
+                if key in ('B_S1', 'B_S1_grid'):
                     c = cpu.get('B')
                 line['extra_lines'][key] = {
                     'value': r['value'], 'unit': 'frame-updates/s', 'ms_per_step': r['ms_per_step'],
@@ -299,7 +301,7 @@ def cpu_child(workload, seconds, rounds):
         return {'error': (cp.stderr or '')[-500:]}
 
 
-def run_online(args, wl, S, rank, world, local, dist, traffic=True, pmc_child=False):
+def run_online(args, wl, S, rank, world, local, dist, traffic=True, pmc_child=False, small_grid=False):
     """One online-engine measurement: S scenes per GPU of workload wl.  A
     step is one full pass of the engine (state reset + every round: WOLA
     analysis, compression, z synthesis, SCM update, GEVD filter update,
@@ -346,7 +348,7 @@ def run_online(args, wl, S, rank, world, local, dist, traffic=True, pmc_child=Fa
                 print(f'# {i + 1}/{len(seeds)} scenes generated', file=sys.stderr, flush=True)
     tScene = time.time() - t0
     eng = DanseEngine(scenes, dp, vadMinProp=wp.vadMinProportionActive, device=local, keepHistory=True,
-                      nodeRange=(k0, k1), yDevice=yDev)
+                      nodeRange=(k0, k1), yDevice=yDev, smallDGrid=small_grid)
     R, F = eng.R, eng.F
     stream = torch.cuda.current_stream()
 
@@ -435,7 +437,8 @@ def run_online(args, wl, S, rank, world, local, dist, traffic=True, pmc_child=Fa
             'frac': tfs / FP32_VALU_PEAK_TFS if valu else gbs / HBM_PEAK_GBS,
             'traffic': (tr or {}).get('bytes_per_launch'),
             'traffic_detail': tr,
-            'kernel': update_kernel_name(max(Dk), gevd=bool(wl.get('gevd', True))), 'avg_launch_ms': avg_ms,
+            'kernel': ('update_kernel_2d (4 x 4 grid)' if small_grid and max(Dk) <= 12
+                       else update_kernel_name(max(Dk), gevd=bool(wl.get('gevd', True)))), 'avg_launch_ms': avg_ms,
             'alg_bytes_per_launch': float(byts.mean()), 'alg_flops_per_launch': float(flops.mean()),
             'hbm_GBs': gbs, 'hbm_frac': gbs / HBM_PEAK_GBS, 'valu_TFs': tfs, 'valu_frac': tfs / FP32_VALU_PEAK_TFS}
     return {

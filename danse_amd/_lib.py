@@ -54,7 +54,7 @@ class DanseCfg(ctypes.Structure):
         ('fsTab', _p_i32), ('zStreamLen', _c_i32), ('scmInitPerBin', _c_i32),
         ('cohDrift', _c_i32), ('cdSegLength', _c_i32), ('cdStart', _c_i32), ('cdEvery', _c_i32),
         ('cdCompensate', _c_i32), ('cdNIter', _c_i32), ('cdAlpha', ctypes.c_double), ('cdAlphaEps', ctypes.c_double),
-        ('cEnd', _p_i32), ('cPhase', ctypes.POINTER(ctypes.c_double)), ('dxcp', _c_i32),
+        ('cEnd', _p_i32), ('cPhase', ctypes.POINTER(ctypes.c_double)), ('dxcp', _c_i32), ('smallDGrid', _c_i32),
     ]
 
 

@@ -31,10 +31,12 @@ def prep_for_danse(p, wasnObj):
     return p, wasnObj
 
 
-def danse_multi(scenes, p, device=0, graph=True, keepHistory=True, yin='data', pregiven=None):
+def danse_multi(scenes, p, device=0, graph=True, keepHistory=True, yin='data', pregiven=None, smallDGrid=False):
     """Run the online engine on S same-shape scenes at once; returns one
-    output object per scene."""
-    eng = DanseEngine(scenes, p, device=device, keepHistory=keepHistory, yin=yin, pregiven=pregiven)
+    output object per scene.  smallDGrid: the latency layout (GEVD filter
+    dimensions <= 12 on the 4 x 4 lane-grid solver, DanseEngine)."""
+    eng = DanseEngine(scenes, p, device=device, keepHistory=keepHistory, yin=yin, pregiven=pregiven,
+                      smallDGrid=smallDGrid)
     try:
         eng.run(graph=graph)
         return eng.outputs()

@@ -422,12 +422,15 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
       if (fn.D > kMaxDMax) return fail(eng, "filter dimension > 64 not supported");
       if (c->gevd && c->rank > fn.D) return fail(eng, "GEVD rank larger than a filter dimension");
       fn.scmOff = scmOff;
-      fn.packed = class_packed(fn.D) ? 1 : 0;
+      // smallDGrid: GEVD of D <= 12 on the 4 x 4 grid class 16 (full storage)
+      const bool gridSmall = c->smallDGrid && c->gevd && fn.D <= kLaneMaxD;
+      fn.packed = (class_packed(fn.D) && !gridSmall) ? 1 : 0;
       scmOff += fn.packed ? (long long)F * fn.D * (fn.D + 1) / 2 : (long long)F * fn.D * fn.D;
       fn.wOff = wOff;
       wOff += histW * F * fn.D;
       fn.liOff = liOff;
       if (c->gevd && fn.packed) liOff += (long long)F * (fn.D * (fn.D + 1) / 2 + fn.D);
+      else if (c->gevd && gridSmall) liOff += (long long)F * class_li_record(16);
       else if (c->gevd && class_grid(class_dmax(fn.D)) > 0) liOff += (long long)F * class_li_record(class_dmax(fn.D));
       eng->fns.push_back(fn);
     }
@@ -451,6 +454,10 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
   for (size_t i = 0; i < eng->fns.size(); ++i) {
     int G, DM;
     pick_class(eng->fns[i].D, G, DM);
+    if (!eng->fns[i].packed && DM <= kLaneMaxD) {   // smallDGrid (above)
+      G = class_group(16);
+      DM = 16;
+    }
     Class* cl = nullptr;
     for (auto& x : eng->classes)
       if (x.G == G && x.DMAX == DM) cl = &x;

@@ -119,7 +119,7 @@ class DanseEngine:
     """
 
     def __init__(self, scenes, p, vadMinProp=0.5, device=0, keepHistory=True, nodeRange=None,
-                 pregiven=None, yin='data', yDevice=None):
+                 pregiven=None, yin='data', yDevice=None, smallDGrid=False):
         import torch
         self.torch = torch
         self.lib = L.load_library()
@@ -146,6 +146,9 @@ class DanseEngine:
             raise NotImplementedError('desSigProcessingType conv (T(z) estimate) on the device path')
         self.device = device
         self.keepHistory = keepHistory
+        # latency layout: GEVD filter dimensions <= 12 on the 4 x 4 lane-grid
+        # solver (four bins per wave) instead of one bin per lane
+        self.smallDGrid = bool(smallDGrid)
         self.k0, self.k1 = nodeRange if nodeRange is not None else (0, K)
         self.nIter = int((self.T - self.N) / self.Ns) + 1
         neighbors = [list(n.neighborsIdx) for n in sc0.wasn]
@@ -518,6 +521,7 @@ class DanseEngine:
                                         _ptr(self._tgt0, ctypes.c_float))
         c.scmInit = _ptr(self._scm, ctypes.c_double)
         c.keepHistory = int(bool(self.keepHistory))
+        c.smallDGrid = int(self.smallDGrid)
         c.zLag = _ptr(self._zLag, ctypes.c_uint8)
         c.zPhase = _ptr(self._zPhase, ctypes.c_double)
         self._fsTab = np.ascontiguousarray(self.rt.fsTab, dtype=np.int32) if self.fewSamples else None

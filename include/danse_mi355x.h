@@ -127,6 +127,11 @@ typedef struct danse_cfg {
    * cdCompensate the sender's phase loses eps Ns after every update.
    * wholeChunk broadcasts; exclusive with cohDrift.  0 = off.             */
   int32_t dxcp;
+  /* Latency layout for small batches: 1 = the GEVD filter dimensions D <= 12
+   * run on the 4 x 4 lane-grid solver (four bins per wavefront, full
+   * [F][D][D] SCM storage) instead of one bin per lane: 16x the wavefronts,
+   * for one or a few WASNs per GPU.  0 = one bin per lane (throughput).   */
+  int32_t smallDGrid;
 } danse_cfg;
 
 typedef struct danse_engine danse_engine;

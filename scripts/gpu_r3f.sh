@@ -11,7 +11,9 @@ timeout -k 10 1000 python -u -m pytest tests -m gpu -v -s --timeout 300 --timeou
 rc=$?
 grep -E "passed|failed" gpurun_out/pytest_gpu_$TAG.log | tail -2
 grep -E "^FAILED" gpurun_out/pytest_gpu_$TAG.log | head -20
-[ "$rc" = "0" ] || exit $rc
+# a parity failure (rc 1) is reported but does not hold back the measurements;
+# anything else (a crash, a time limit) ends the call here
+[ "$rc" -le 1 ] || exit $rc
 timeout -k 10 900 python bench.py > gpurun_out/bench_full_$TAG.log 2>&1 || { tail -20 gpurun_out/bench_full_$TAG.log; exit 1; }
 tail -1 gpurun_out/bench_full_$TAG.log | cut -c1-300
 timeout -k 10 600 python bench.py --workload C --steps 2 --warmup 1 --cpu-seconds 10 > gpurun_out/bench_C_$TAG.log 2>&1 || { tail -20 gpurun_out/bench_C_$TAG.log; exit 1; }
@@ -20,4 +22,4 @@ for W in B N2 C; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof${W}_$TAG -o kt --output-format csv -- python bench.py --workload $W --steps 1 --warmup 1 --no-cpu-baseline --no-traffic --no-extra > gpurun_out/prof${W}_$TAG.log 2>&1 || { tail -20 gpurun_out/prof${W}_$TAG.log; exit 1; }
   find gpurun_out/prof${W}_$TAG -name "*kernel_stats.csv" | head -1 | xargs head -4 | cut -d, -f1-4
 done
-exit 0
+exit $rc

@@ -45,13 +45,16 @@ B_SHAPE = [dict(name=f'online_B_shape_K8x4_{nu}', M=[4] * 8, dur=4.0, seed=31,
                 danse=dict(BATTERY, nodeUpdating=nu)) for nu in ('asy', 'seq')]
 
 
+@pytest.mark.parametrize('grid', [False, True], ids=['lane', 'grid4'])
 @pytest.mark.parametrize('case', B_SHAPE, ids=lambda c: c['name'])
-def test_config_B_shape_vs_oracle(case):
-    """K = 8 x 4 (D = 11), 4 s: the lane-per-bin kernel class the bench times."""
+def test_config_B_shape_vs_oracle(case, grid):
+    """K = 8 x 4 (D = 11), 4 s: the lane-per-bin kernel class the bench times
+    (lane), and the latency layout on the 4 x 4 lane-grid solver (grid4,
+    smallDGrid: full SCM storage, four bins per wave, the factor cache)."""
     from danse_amd.core import danse_multi
     from oracle import danse_ref_cpu as O
     sc, dp, wp = _scene_params(case)
-    dv = danse_multi([sc], dp)[0]
+    dv = danse_multi([sc], dp, smallDGrid=grid)[0]
     ov = O.danse(sc, dp, vadMinProp=wp.vadMinProportionActive)
     assert np.array_equal(dv.startRound, ov.startRound)
     assert np.array_equal(dv.nInternalFilterUps, ov.nInternalFilterUps)
