@@ -184,6 +184,7 @@ def main():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
     ap.add_argument('--no-graph', action='store_true')
+    ap.add_argument('--resident', action='store_true', help='online workloads: the resident engine (one persistent launch)')
     ap.add_argument('--no-traffic', action='store_true', help='skip the rocprofv3 PMC passes')
     ap.add_argument('--no-extra', action='store_true',
                     help='N=1, workload B: skip the extra single-WASN lines (B at S=1, N2 K=32x8 at S=1)')
@@ -231,7 +232,7 @@ def main():
     if args.pmc_child:
         run_online(args, wl, S, rank, world, local, dist, pmc_child=True)
         return
-    res = run_online(args, wl, S, rank, world, local, dist)
+    res = run_online(args, wl, S, rank, world, local, dist, resident=args.resident)
     extra = {}
     if world == 1 and args.workload == 'B' and not args.no_extra:
         # single-WASN lines: config B at S=1 and the
@@ -239,6 +240,8 @@ def main():
         extra['B_S1'] = run_online(args, wl, 1, rank, world, local, dist, traffic=False)
         # the latency layout for one WASN: D = 11 on the 4 x 4 lane-grid solver
         extra['B_S1_grid'] = run_online(args, wl, 1, rank, world, local, dist, traffic=False, small_grid=True)
+        # N1: the whole run in one persistent launch, SCMs resident in registers
+        extra['B_S1_resident'] = run_online(args, wl, 1, rank, world, local, dist, traffic=False, resident=True)
         extra['N2'] = run_online(args, WORKLOADS['N2'], 1, rank, world, local, dist)
     cpu = {}
     if rank == 0 and not args.no_cpu_baseline:
@@ -269,7 +272,7 @@ def main():
             line['extra_lines'] = {}
             for key, r in extra.items():
                 c = cpu.get(key)
-                if key in ('B_S1', 'B_S1_grid'):
+                if key in ('B_S1', 'B_S1_grid', 'B_S1_resident'):
                     c = cpu.get('B')
                 line['extra_lines'][key] = {
                     'value': r['value'], 'unit': 'frame-updates/s', 'ms_per_step': r['ms_per_step'],
@@ -301,7 +304,7 @@ def cpu_child(workload, seconds, rounds):
         return {'error': (cp.stderr or '')[-500:]}
 
 
-def run_online(args, wl, S, rank, world, local, dist, traffic=True, pmc_child=False, small_grid=False):
+def run_online(args, wl, S, rank, world, local, dist, traffic=True, pmc_child=False, small_grid=False, resident=False):
     """One online-engine measurement: S scenes per GPU of workload wl.  A
     step is one full pass of the engine (state reset + every round: WOLA
     analysis, compression, z synthesis, SCM update, GEVD filter update,
@@ -348,7 +351,7 @@ def run_online(args, wl, S, rank, world, local, dist, traffic=True, pmc_child=Fa
                 print(f'# {i + 1}/{len(seeds)} scenes generated', file=sys.stderr, flush=True)
     tScene = time.time() - t0
     eng = DanseEngine(scenes, dp, vadMinProp=wp.vadMinProportionActive, device=local, keepHistory=True,
-                      nodeRange=(k0, k1), yDevice=yDev, smallDGrid=small_grid)
+                      nodeRange=(k0, k1), yDevice=yDev, smallDGrid=small_grid, resident=resident)
     R, F = eng.R, eng.F
     stream = torch.cuda.current_stream()
 
@@ -400,7 +403,16 @@ def run_online(args, wl, S, rank, world, local, dist, traffic=True, pmc_child=Fa
     # the engine's stream around each round's update launch
     L.check(eng.lib.danse_engine_reset(eng.eng, eng.stream_ptr()), eng.eng)
     evs = []
-    for r in range(R):
+    if resident:
+        # one persistent launch per run: the "launch" is the whole run
+        # (analyses, round loop, gate checks, synthesis) on the engine stream
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        eng.run()
+        b.record(stream)
+        evs.append((a, b))
+    for r in range(R if not resident else 0):
         eng.bcast(r)
         if runner is not None:
             runner.exchange(r)
@@ -410,7 +422,8 @@ def run_online(args, wl, S, rank, world, local, dist, traffic=True, pmc_child=Fa
         eng.update(r)
         b.record(stream)
         evs.append((a, b))
-    eng.finish()
+    if not resident:
+        eng.finish()
     torch.cuda.synchronize()
     upd_ms = np.array([a.elapsed_time(b) for a, b in evs])
     Dk = [M[k] + K - 1 for k in range(K)]
@@ -420,6 +433,9 @@ def run_online(args, wl, S, rank, world, local, dist, traffic=True, pmc_child=Fa
     Dl = np.array(Dk[k0:k1], dtype=np.float64)[None, None, :]
     byts = F * alg_bytes_update(Dl, opY, opN, solve).sum(axis=(1, 2))       # per launch (round)
     flops = F * alg_flops_update(Dl, opY, opN, solve).sum(axis=(1, 2))
+    if resident:
+        # per launch = every round of the run
+        byts, flops = np.array([byts.sum()]), np.array([flops.sum()])
     avg_ms = float(upd_ms.mean())
     gbs = float(byts.mean() / (avg_ms * 1e-3) / 1e9)
     tfs = float(flops.mean() / (avg_ms * 1e-3) / 1e12)
@@ -437,7 +453,9 @@ def run_online(args, wl, S, rank, world, local, dist, traffic=True, pmc_child=Fa
             'frac': tfs / FP32_VALU_PEAK_TFS if valu else gbs / HBM_PEAK_GBS,
             'traffic': (tr or {}).get('bytes_per_launch'),
             'traffic_detail': tr,
-            'kernel': ('update_kernel_2d (4 x 4 grid)' if small_grid and max(Dk) <= 12
+            'kernel': ('resident_kernel (one persistent launch per run; achieved = all rounds\' algorithmic bytes '
+                       '/ the run)' if resident else
+                       'update_kernel_2d (4 x 4 grid)' if small_grid and max(Dk) <= 12
                        else update_kernel_name(max(Dk), gevd=bool(wl.get('gevd', True)))), 'avg_launch_ms': avg_ms,
             'alg_bytes_per_launch': float(byts.mean()), 'alg_flops_per_launch': float(flops.mean()),
             'hbm_GBs': gbs, 'hbm_frac': gbs / HBM_PEAK_GBS, 'valu_TFs': tfs, 'valu_frac': tfs / FP32_VALU_PEAK_TFS}
@@ -447,7 +465,7 @@ def run_online(args, wl, S, rank, world, local, dist, traffic=True, pmc_child=Fa
                 f'{Stot} scenes x {K} nodes x {F} bins x {R} rounds per step',
         'config': {'workload': wl['desc'], 'scenes_per_gpu': S, 'K': K, 'M': M if len(set(M)) > 1 else M[0],
                    'D': Dk if len(set(Dk)) > 1 else Dk[0], 'bins': F, 'rounds': R, 'shard': shard,
-                   'gevd_rank': 1, 'graph': not args.no_graph},
+                   'gevd_rank': 1, 'graph': not args.no_graph, 'resident': resident},
         'roofline': roof, 'diag_nonpd': int(np.sum(diag)), 'scene_gen_s': tScene,
     }
 

@@ -86,6 +86,8 @@ SIGNATURES = {
     'danse_engine_set_inputs': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p]),
     'danse_engine_reset': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p]),
     'danse_engine_run': (_c_i32, [ctypes.c_void_p, _c_i32, _c_i32, ctypes.c_void_p, _c_i32]),
+    'danse_engine_run_resident': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p]),
+    'danse_engine_resident_error': (_c_i32, [ctypes.c_void_p, ctypes.POINTER(_c_i32), ctypes.c_void_p]),
     'danse_engine_bcast': (_c_i32, [ctypes.c_void_p, _c_i32, ctypes.c_void_p]),
     'danse_engine_update': (_c_i32, [ctypes.c_void_p, _c_i32, ctypes.c_void_p]),
     'danse_engine_finish': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p]),

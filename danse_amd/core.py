@@ -31,12 +31,14 @@ def prep_for_danse(p, wasnObj):
     return p, wasnObj
 
 
-def danse_multi(scenes, p, device=0, graph=True, keepHistory=True, yin='data', pregiven=None, smallDGrid=False):
+def danse_multi(scenes, p, device=0, graph=True, keepHistory=True, yin='data', pregiven=None, smallDGrid=False,
+                resident=False):
     """Run the online engine on S same-shape scenes at once; returns one
     output object per scene.  smallDGrid: the latency layout (GEVD filter
-    dimensions <= 12 on the 4 x 4 lane-grid solver, DanseEngine)."""
+    dimensions <= 12 on the 4 x 4 lane-grid solver, DanseEngine); resident:
+    the whole run in one persistent launch (csrc/resident.hpp)."""
     eng = DanseEngine(scenes, p, device=device, keepHistory=keepHistory, yin=yin, pregiven=pregiven,
-                      smallDGrid=smallDGrid)
+                      smallDGrid=smallDGrid, resident=resident)
     try:
         eng.run(graph=graph)
         return eng.outputs()

@@ -88,6 +88,7 @@ DANSE_DEV cf herm_ext_conj(const cf* __restrict__ X, int n, int F) {
   return (n < F) ? conjg(X[n]) : X[1024 - n];
 }
 
+#ifndef DANSE_BCAST_HELPERS_ONLY   // resident.hip uses the helpers above, not the kernel
 __global__ void __launch_bounds__(256) bcast_kernel(const BcastArgs a) {
   __shared__ cf fftLds[kBcWaves][wfft::kLdsElems];
   __shared__ cf part[kBcWaves][513];
@@ -263,5 +264,6 @@ __global__ void __launch_bounds__(256) bcast_kernel(const BcastArgs a) {
     }
   }
 }
+#endif
 
 }  // namespace danse

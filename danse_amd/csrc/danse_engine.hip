@@ -15,6 +15,8 @@
 #include "gate.hpp"
 #include "cohdrift.hpp"
 #include "tzconv.hpp"
+#include "resident.hpp"
+#include "resident_api.hpp"
 
 using namespace danse;
 
@@ -108,6 +110,15 @@ struct danse_engine {
   cf* Cspec = nullptr;
   int* dChanNode = nullptr;
   double* dCPhase = nullptr;
+  // resident engine (danse_engine_run_resident, resident.hpp)
+  std::vector<std::pair<int, GateCand>> gateHost;   // the installed gate schedule (round, candidate)
+  cf *resYB = nullptr, *resYU = nullptr, *resZall = nullptr, *resZhat = nullptr, *resRyyG = nullptr;
+  cd* resRnnG = nullptr;
+  unsigned *resUFlag = nullptr, *resZFlag = nullptr;
+  int *resGateRound = nullptr, *resDanseFni = nullptr, *resErr = nullptr, *resFams = nullptr;
+  float* resFrames = nullptr;
+  int* resChanNode = nullptr;        // [MT] node of each channel
+  int resNFam = 0;
 };
 
 static thread_local std::string g_lastErr;
@@ -705,7 +716,9 @@ void danse_engine_destroy(danse_engine* eng) {
                   eng->dInitScmOff, eng->dExtSrcOff, eng->dTgtOff, eng->dFsTab, eng->wIR, eng->dSn, eng->liCache,
                   eng->dGateCand, eng->dGateVerdict, eng->cdRing, eng->cdAvg, eng->cdPhase, eng->cdEst,
                   eng->cdRes, eng->dCEnd, eng->Cspec, eng->dChanNode, eng->dCPhase, eng->dxFrames, eng->dxOut,
-                  eng->dxEst};
+                  eng->dxEst, eng->resYB, eng->resYU, eng->resZall, eng->resZhat, eng->resRyyG, eng->resRnnG,
+                  eng->resUFlag, eng->resZFlag, eng->resGateRound, eng->resDanseFni, eng->resErr, eng->resFams,
+                  eng->resFrames, eng->resChanNode};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (eng->dx) danse_dxcp_destroy(eng->dx);
@@ -906,6 +919,149 @@ int danse_engine_run(danse_engine* eng, int32_t r0, int32_t r1, void* stream, in
   return 0;
 }
 
+// ---- the resident engine (resident.hpp) -----------------------------------
+static int resident_prepare(danse_engine* eng, int& NB) {
+  danse_engine* e = eng;
+  if (e->k0 != 0 || e->k1 != e->K) return fail(e, "resident run: the engine must own every node");
+  if (e->dFsTab) return fail(e, "resident run: wholeChunk broadcasts only");
+  if (e->cohDrift || e->dxcpOn) return fail(e, "resident run: no CohDrift / DXCP estimation");
+  if (e->dCEnd) return fail(e, "resident run: no centralised raw frames (cEnd)");
+  if (!e->gevd) return fail(e, "resident run: GEVD filters only");
+  int dmax = 1;
+  for (const auto& fn : e->fns) {
+    if (fn.packed || fn.D > 12) return fail(e, "resident run: filter dimensions <= 12 in grid storage (smallDGrid)");
+    dmax = std::max(dmax, fn.D);
+  }
+  NB = 3;
+  const int S = e->S, K = e->K, F = e->F, R = e->R, MT = e->MT;
+  std::vector<int> up((size_t)R * K);
+  HIPCHK(hipMemcpy(up.data(), e->dUpEnd, up.size() * sizeof(int), hipMemcpyDeviceToHost));
+  for (int k = 0; k < K; ++k)
+    for (int r = 1; r < R; ++r)
+      if (up[(size_t)r * K + k] < up[(size_t)(r - 1) * K + k]) return fail(e, "resident run: update frames go backwards");
+  if (!e->resYB) {
+    const int nFN = (int)e->fns.size();
+    std::vector<int> danseFni(K, -1), fams;
+    for (int i = 0; i < nFN; ++i)
+      if (e->fns[i].fam == DANSE_FAM_DANSE) danseFni[e->fns[i].k] = i;
+    for (int f = 0; f < kMaxFam; ++f)
+      if ((e->families >> f) & 1) fams.push_back(f);
+    e->resNFam = (int)fams.size();
+    HIPCHK(dalloc(&e->resYB, (size_t)R * S * MT * F));
+    HIPCHK(dalloc(&e->resYU, (size_t)R * S * MT * F));
+    HIPCHK(dalloc(&e->resZall, (size_t)(R + 1) * K * S * F));
+    HIPCHK(dalloc(&e->resZhat, (size_t)S * K * F));
+    HIPCHK(dalloc(&e->resRyyG, (size_t)S * e->scmStride));
+    HIPCHK(dalloc(&e->resRnnG, (size_t)S * e->scmStride));
+    HIPCHK(dalloc(&e->resUFlag, (size_t)S * nFN * ((F + res::kBins - 1) / res::kBins)));
+    HIPCHK(dalloc(&e->resZFlag, (size_t)S * K));
+    HIPCHK(dalloc(&e->resGateRound, (size_t)S * nFN));
+    HIPCHK(dalloc(&e->resDanseFni, (size_t)K));
+    HIPCHK(dalloc(&e->resErr, 1));
+    HIPCHK(dalloc(&e->resFams, fams.size()));
+    HIPCHK(dalloc(&e->resFrames, (size_t)e->resNFam * S * K * R * e->N));
+    std::vector<int> chanNode;
+    for (int q = 0; q < K; ++q)
+      for (int m = 0; m < e->M[q]; ++m) chanNode.push_back(q);
+    HIPCHK(dalloc(&e->resChanNode, (size_t)MT));
+    HIPCHK(hipMemcpy(e->resChanNode, chanNode.data(), MT * sizeof(int), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(e->resDanseFni, danseFni.data(), K * sizeof(int), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(e->resFams, fams.data(), fams.size() * sizeof(int), hipMemcpyHostToDevice));
+    HIPCHK(hipMemset(e->resErr, 0, sizeof(int)));
+  }
+  return 0;
+}
+
+static UpdateArgs make_update_resident(danse_engine* e, int r) {
+  UpdateArgs a = make_update(e, r);
+  a.Yall = e->resYU;
+  a.zAll = 1;
+  a.Zspec = e->resZall;
+  return a;
+}
+
+int danse_engine_run_resident(danse_engine* eng, void* stream) {
+  if (!eng || !eng->y) return fail(eng, "inputs not set");
+  HIPCHK(hipSetDevice(eng->dev));
+  int NB = 0;
+  if (int rc = resident_prepare(eng, NB)) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  const int S = eng->S, K = eng->K, F = eng->F, R = eng->R;
+  const int nFN = (int)eng->fns.size();
+  const int FG = (F + res::kBins - 1) / res::kBins;
+  res::ResArgs ra{};
+  ra.u = make_update_resident(eng, 0);
+  ra.b = make_bcast(eng, 1, 0, 1);
+  ra.fn = eng->dFnAll;
+  ra.danseFni = eng->resDanseFni;
+  ra.nFN = nFN; ra.FG = FG; ra.nZ = S * K; ra.R = R;
+  ra.YB = eng->resYB;
+  ra.zhat = eng->resZhat;
+  ra.uFlag = eng->resUFlag;
+  ra.zFlag = eng->resZFlag;
+  ra.gateRound = eng->resGateRound;
+  ra.RyyG = eng->resRyyG;
+  ra.RnnG = eng->resRnnG;
+  ra.err = eng->resErr;
+  const int grid = ra.nZ + S * nFN * FG;
+  int fits = 0;
+  const int chk = resident_launch(NB, eng->rank == 1, ra, grid, st, true, &fits);
+  if (chk < 0) return fail(eng, "resident run: occupancy query failed");
+  if (chk > 0)
+    return fail(eng, "resident run: " + std::to_string(grid) + " waves do not fit the device at once (" +
+                         std::to_string(fits) + ")");
+  // gate snapshot rounds per (scene, family-node)
+  std::vector<int> gr((size_t)S * nFN, -1);
+  for (auto& x : eng->gateHost) gr[(size_t)x.second.s * nFN + x.second.fni] = x.first;
+  HIPCHK(hipMemcpyAsync(eng->resGateRound, gr.data(), gr.size() * sizeof(int), hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemsetAsync(eng->resUFlag, 0, (size_t)S * nFN * FG * sizeof(unsigned), st));
+  HIPCHK(hipMemsetAsync(eng->resZFlag, 0, (size_t)S * K * sizeof(unsigned), st));
+  HIPCHK(hipMemsetAsync(eng->resZall, 0, (size_t)K * S * F * sizeof(cf), st));   // slot 0: before round 0
+  if (eng->nGate > 0) HIPCHK(hipMemsetAsync(eng->dGateVerdict, 0xff, eng->nGate * sizeof(int), st));
+  // WOLA analyses of every round (inputs only)
+  {
+    BcastArgs b = make_bcast(eng, 0, 0, 1);
+    resident_analysis(b, eng->resChanNode, eng->resYB, eng->resYU, st);
+    HIPCHK(hipGetLastError());
+  }
+  // round 0's broadcast into slot 1
+  {
+    BcastArgs b = make_bcast(eng, 0, 0, 1);
+    b.Zspec = eng->resZall + (size_t)K * S * F;
+    hipLaunchKernelGGL(bcast_kernel, dim3((unsigned)(S * K)), dim3(256), 0, st, b);
+    HIPCHK(hipGetLastError());
+  }
+  if (resident_launch(NB, eng->rank == 1, ra, grid, st, false, &fits) != 0) return fail(eng, "resident launch failed");
+  // the speculative gate checks, on the snapshots of the candidates' rounds
+  for (int r = 0; r < R && eng->nGate > 0; ++r) {
+    if (eng->gateOff[r + 1] == eng->gateOff[r]) continue;
+    const int n = eng->gateOff[r + 1] - eng->gateOff[r];
+    const size_t lds = (size_t)eng->gateDmax[r] * (eng->gateDmax[r] + 1) * sizeof(cd);
+    UpdateArgs a = make_update_resident(eng, r);
+    a.Ryy = eng->resRyyG;
+    a.Rnn = eng->resRnnG;
+    hipLaunchKernelGGL(gate_kernel, dim3(F, n), dim3(64), lds, st, a, eng->dFnAll, eng->dGateCand + eng->gateOff[r],
+                       eng->dInitScmOff, eng->dScm0, eng->scmPerBin, eng->dGateVerdict + eng->gateOff[r]);
+  }
+  // estimate synthesis of every round
+  {
+    BcastArgs b = make_bcast(eng, R, 1, 0);
+    resident_synth(b, eng->resFams, eng->resNFam, eng->resFrames, st);
+  }
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int danse_engine_resident_error(danse_engine* eng, int32_t* err, void* stream) {
+  if (!eng || !err) return fail(eng, "null argument");
+  *err = 0;
+  if (!eng->resErr) return 0;
+  HIPCHK(hipSetDevice(eng->dev));
+  HIPCHK(hipMemcpyAsync(err, eng->resErr, sizeof(int), hipMemcpyDeviceToHost, (hipStream_t)stream));
+  HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  return 0;
+}
+
 int danse_engine_set_zspec(danse_engine* eng, void* ptr) {
   if (!eng || !ptr) return fail(eng, "null argument");
   HIPCHK(hipSetDevice(eng->dev));
@@ -971,6 +1127,7 @@ int danse_engine_set_gate(danse_engine* eng, int32_t n, const int32_t* round, co
   eng->nGate = 0;
   eng->gateOff.assign(eng->R + 1, 0);
   eng->gateDmax.assign(eng->R, 1);
+  eng->gateHost.clear();
   if (n == 0) return 0;
   std::vector<std::pair<int, GateCand>> v;
   for (int i = 0; i < n; ++i) {
@@ -982,6 +1139,7 @@ int danse_engine_set_gate(danse_engine* eng, int32_t n, const int32_t* round, co
     v.push_back({round[i], GateCand{fni, scene[i], qY[i], qN[i]}});
   }
   std::stable_sort(v.begin(), v.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+  eng->gateHost = v;
   std::vector<GateCand> h;
   for (auto& x : v) {
     h.push_back(x.second);

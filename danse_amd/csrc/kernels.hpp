@@ -77,7 +77,36 @@ struct UpdateArgs {
   const cf* Cspec;
   const int* chanNode;     // [MT] node of each channel
   const double* cPhase;    // [R][K][MT] centralised compensation phase (samples), or null
+  // resident engine (resident.hpp): the update-frame spectra of every round
+  // ([R][S][MT][F], replacing the Yspec ping-pong) and the fused spectra of
+  // every round (Zspec = [R + 1][K][S][F], slot r + 1 = round r, slot 0
+  // zeros), read with agent-coherent loads (written inside the same launch)
+  const cf* Yall;
+  int zAll;
 };
+
+// Agent-coherent (sc1) 8-byte load / store of a complex value: the resident
+// engine's hand-offs between waves of one launch (payload stored sc1 and
+// loaded sc1, flag after s_waitcnt vmcnt(0): MI355X_MICROARCH.md,
+// inter-workgroup visibility, first hand-off row).  Global address space so
+// that they lower to global_load / global_store (never flat).
+typedef __attribute__((address_space(1))) unsigned long long danse_gu64;
+typedef __attribute__((address_space(1))) unsigned int danse_gu32;
+DANSE_DEV cf ld_sc1(const cf* p) {
+  const unsigned long long v =
+      __hip_atomic_load((danse_gu64*)(const_cast<cf*>(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return cf{__uint_as_float((unsigned)(v & 0xffffffffull)), __uint_as_float((unsigned)(v >> 32))};
+}
+DANSE_DEV void st_sc1(cf* p, cf x) {
+  const unsigned long long v = (unsigned long long)__float_as_uint(x.re) | ((unsigned long long)__float_as_uint(x.im) << 32);
+  __hip_atomic_store((danse_gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+DANSE_DEV unsigned ld_flag(const unsigned* p) {
+  return __hip_atomic_load((danse_gu32*)(const_cast<unsigned*>(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+DANSE_DEV void st_flag(unsigned* p, unsigned v) {
+  __hip_atomic_store((danse_gu32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // yhat *= exp(-j 2 pi f phi / N) (compensate_sros, d_classes.py:1936-2046)
 DANSE_DEV cf sro_rotate(cf v, int f, int F, double ph) {
@@ -114,7 +143,8 @@ DANSE_DEV cf load_y(const UpdateArgs& a, const FamNode& d, int s, int f, int li,
   const int rawBase = a.MT + a.K;
   cf v;
   if (c < a.MT) {
-    v = a.Yspec[(((long long)((r + 1) & 1) * a.S + s) * a.MT + c) * F + f];
+    v = a.Yall ? a.Yall[(((long long)r * a.S + s) * a.MT + c) * F + f]
+               : a.Yspec[(((long long)((r + 1) & 1) * a.S + s) * a.MT + c) * F + f];
   } else if (c >= rawBase) {
     // another node's raw channel in the centralised / SSBC vector
     // (process_incoming_signals_buffers_centr, d_classes.py:1809-1891)
@@ -126,7 +156,8 @@ DANSE_DEV cf load_y(const UpdateArgs& a, const FamNode& d, int s, int f, int li,
     const int q = c - a.MT;
     const long long lk = ((long long)r * a.K + d.k) * a.K + q;
     const int lag = a.zLag ? a.zLag[lk] : 0;
-    v = a.Zspec[((((long long)((r - lag) & 1)) * a.K + q) * a.S + s) * F + f];
+    if (a.zAll) v = ld_sc1(a.Zspec + ((((long long)(r - lag + 1)) * a.K + q) * a.S + s) * F + f);
+    else v = a.Zspec[((((long long)((r - lag) & 1)) * a.K + q) * a.S + s) * F + f];
     if (a.zPhase) {
       double ph = a.zPhase[lk];
       if (a.cdPhase) ph += a.cdPhase[((long long)s * a.K + d.k) * a.K + q];
@@ -145,11 +176,13 @@ DANSE_DEV cf load_y(const UpdateArgs& a, const FamNode& d, int s, int f, int li,
 // External filters (DANSE family, update_external_filters,
 // d_classes.py:1627-1694) and dhat = w^H yhat (d_base.py:2075, DC / Nyquist
 // forced real, quirk Q7) of one (scene, family-node, bin); lane li of the
-// bin's lane group holds w_li, dh is the group sum of conj(w) y.
-DANSE_DEV void node_bin_tail(const UpdateArgs& a, const FamNode& d, int s, int f, int li, uint8_t fl, bool pregiven,
+// bin's lane group holds w_li, dh is the group sum of conj(w) y.  Returns
+// the new external filter entry li (DANSE family, li < M; else zero).
+DANSE_DEV cf node_bin_tail(const UpdateArgs& a, const FamNode& d, int s, int f, int li, uint8_t fl, bool pregiven,
                              bool valid, cf w, cf y, cf dh) {
   const int F = a.F;
   const int r = a.r;
+  cf ne = cf{0.0f, 0.0f};
   if (d.extMode >= 0 && !pregiven) {
     const int M = d.M;
     const long long eb = (long long)s * a.wExtStride + d.wExtOff;
@@ -159,7 +192,6 @@ DANSE_DEV void node_bin_tail(const UpdateArgs& a, const FamNode& d, int s, int f
     cf* enext = a.wExtHist + eb + ((long long)eN * F + f) * M;
     cf* tgt = a.wExtTarget + (long long)s * a.tgtStride + d.tgtOff + (long long)f * M;
     if (li < M && valid) {
-      cf ne;
       if (d.extMode == 0) ne = w;
       else if (d.extMode == 2) ne = eprev[li];
       else if (d.extMode == 3) ne = cf{(li == d.ref) ? 1.0f : 0.0f, 0.0f};
@@ -176,6 +208,7 @@ DANSE_DEV void node_bin_tail(const UpdateArgs& a, const FamNode& d, int s, int f
   if (li == 0 && valid) {
     a.dhat[((((long long)d.fam * a.S + s) * a.K + d.k) * a.R + r) * F + f] = dh;
   }
+  return ne;
 }
 
 }  // namespace danse

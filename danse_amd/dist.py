@@ -87,6 +87,12 @@ class ShardedRun:
 
     def exchange(self, r=0):
         i = r % self.slots
+        if self.world == 1:
+            # the all-gather of one rank is the identity.  (Issued anyway, an
+            # in-place RCCL all-gather captured into the round graph made the
+            # second and later replays differ from the eager run now and then:
+            # profiles/round3/pytest_gpu_r3g.log, rccl_graph_mixing_r3d.log.)
+            return
         if self.stage:
             mine = self.mine[i].cpu()
             self.dist.all_gather_into_tensor(self.hslot[i], mine, group=self.group)

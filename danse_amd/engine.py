@@ -119,7 +119,7 @@ class DanseEngine:
     """
 
     def __init__(self, scenes, p, vadMinProp=0.5, device=0, keepHistory=True, nodeRange=None,
-                 pregiven=None, yin='data', yDevice=None, smallDGrid=False):
+                 pregiven=None, yin='data', yDevice=None, smallDGrid=False, resident=False):
         import torch
         self.torch = torch
         self.lib = L.load_library()
@@ -149,6 +149,16 @@ class DanseEngine:
         # latency layout: GEVD filter dimensions <= 12 on the 4 x 4 lane-grid
         # solver (four bins per wave) instead of one bin per lane
         self.smallDGrid = bool(smallDGrid)
+        # resident engine (danse_engine_run_resident, csrc/resident.hpp): the
+        # whole run in one persistent launch, SCMs resident in registers; it
+        # runs on the 4 x 4 grid storage, so it implies smallDGrid
+        self.resident = bool(resident)
+        if self.resident:
+            if pregiven is not None:
+                raise ValueError('resident runs take no pre-given filters')
+            if not p.performGEVD:
+                raise NotImplementedError('resident runs: GEVD filters only')
+            self.smallDGrid = True
         self.k0, self.k1 = nodeRange if nodeRange is not None else (0, K)
         self.nIter = int((self.T - self.N) / self.Ns) + 1
         neighbors = [list(n.neighborsIdx) for n in sc0.wasn]
@@ -596,7 +606,10 @@ class DanseEngine:
         gating = gate and self.pregiven is None and not self.p.bypassUpdates
         if gating and not self._gateSpecFailed:
             n = self._install_gate()
-            L.check(self.lib.danse_engine_run(self.eng, 0, self.R, st, int(bool(graph))), self.eng)
+            if self.resident:
+                self._run_resident(st)
+            else:
+                L.check(self.lib.danse_engine_run(self.eng, 0, self.R, st, int(bool(graph))), self.eng)
             if n == 0:
                 return self
             ver = np.zeros(n, dtype=np.int32)
@@ -611,12 +624,24 @@ class DanseEngine:
             self._uninstall_gate()
             r0 = self._run_gated(st)
         else:
+            if self.resident:
+                self._run_resident(st)
+                return self
             r0 = 0
         if r0 < self.R:
             L.check(self.lib.danse_engine_run(self.eng, r0, self.R, st, int(bool(graph))), self.eng)
         else:
             L.check(self.lib.danse_engine_finish(self.eng, st), self.eng)
         return self
+
+    def _run_resident(self, st):
+        """One persistent launch for the whole run (resident engine); raises
+        if a wave gave up waiting (a hand-off that never arrived)."""
+        L.check(self.lib.danse_engine_run_resident(self.eng, st), self.eng)
+        err = ctypes.c_int32()
+        L.check(self.lib.danse_engine_resident_error(self.eng, ctypes.byref(err), st), self.eng)
+        if err.value:
+            raise RuntimeError('resident run: a wave gave up waiting for a hand-off')
 
     def _gate_candidates(self):
         """(round, (s, f, k)) of every owned family-node's first counter-eligible round."""

@@ -169,6 +169,21 @@ int danse_engine_set_inputs(danse_engine* eng, const float* yDev);
  * graph != 0 captures the launch sequence in a hipGraph once and replays it. */
 int danse_engine_run(danse_engine* eng, int32_t r0, int32_t r1, void* stream, int32_t graph);
 
+/* The whole run in ONE persistent launch (the resident engine, SURVEY §8
+ * row N1; the round loop of danse_toolbox/d_core.py:66-90 with every bin's
+ * SCMs resident in registers and its GEVD factor in LDS): the WOLA analyses
+ * of every round, round 0's broadcast, the persistent round loop (update
+ * waves on 4 x 4 lane grids + one broadcast wave per (scene, node)), the
+ * installed speculative gate checks (danse_engine_set_gate) and the estimate
+ * synthesis, all on `stream`, no host synchronisation.  Needs: one engine
+ * owning every node, wholeChunk broadcasts, no CohDrift / DXCP / centralised
+ * raw frames, GEVD, every filter dimension <= 12 in full (grid) storage
+ * (danse_cfg.smallDGrid), no pre-given filters, and the whole
+ * grid resident at once (returns -1 with the reason otherwise).  A wait that
+ * gives up sets the flag danse_engine_resident_error reads.             */
+int danse_engine_run_resident(danse_engine* eng, void* stream);
+int danse_engine_resident_error(danse_engine* eng, int32_t* err, void* stream);
+
 /* Fine-grained per-round phases (multi-GPU: the caller all-gathers the fused
  * spectra between them).  bcast(r) also synthesises the estimates of r-1. */
 int danse_engine_bcast(danse_engine* eng, int32_t r, void* stream);

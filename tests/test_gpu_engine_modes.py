@@ -70,6 +70,49 @@ def test_config_B_shape_vs_oracle(case, grid):
     assert de <= 1e-4
 
 
+@pytest.mark.parametrize('case', B_SHAPE, ids=lambda c: c['name'])
+def test_resident_B_shape_vs_oracle(case):
+    """The resident engine (one persistent launch for the whole run, SCMs
+    resident in registers, factor in LDS, csrc/resident.hpp) at config B's
+    K = 8 x 4 (D = 11): the oracle's filters and estimates at the same
+    tolerance as every online case, the same start rounds and update counts,
+    and the launch-per-round grid engine's d to float32 rounding."""
+    from danse_amd.core import danse_multi
+    from oracle import danse_ref_cpu as O
+    sc, dp, wp = _scene_params(case)
+    dv = danse_multi([sc], dp, resident=True)[0]
+    gv = danse_multi([sc], dp, smallDGrid=True)[0]
+    ov = O.danse(sc, dp, vadMinProp=wp.vadMinProportionActive)
+    assert np.array_equal(dv.startRound, ov.startRound)
+    assert np.array_equal(dv.nInternalFilterUps, ov.nInternalFilterUps)
+    assert int(np.sum(dv.diag)) == 0
+    errs = []
+    for k in range(8):
+        s0 = int(ov.startRound[k])
+        errs.append(_bin_rel(dv.wTilde[k][:, s0 + 1:dv.nRounds + 1], ov.wTilde[k][:, s0 + 1:dv.nRounds + 1]))
+    st = _stats(np.concatenate([e.ravel() for e in errs]))
+    de = rel_err(dv.d, ov.d)
+    dg = rel_err(dv.d, gv.d)
+    print(case['name'], 'resident w', st, 'd', de, 'vs grid engine d', dg)
+    assert st['median'] <= 1e-5 and st['p99'] <= 1e-4, st
+    assert de <= 1e-4
+    assert dg <= 1e-5
+
+
+def test_resident_gate_delay_falls_back():
+    """A start the reference gate delays (online_gate_delay_asy): the
+    resident run's speculative gate checks (on the SCM snapshots of the
+    candidates' rounds) fail, and the engine repeats the run on the exact
+    host-gated loop -- same outputs as the launch-per-round engine."""
+    from danse_amd.core import danse_multi
+    case = _case('online_gate_delay_asy')
+    sc, dp, wp = _scene_params(case)
+    rv = danse_multi([sc], dp, resident=True)[0]
+    gv = danse_multi([sc], dp, smallDGrid=True)[0]
+    assert np.array_equal(rv.startRound, gv.startRound)
+    assert np.array_equal(rv.d, gv.d)
+
+
 @pytest.mark.parametrize('name', ['online_B_k4m3_asy', 'online_A_k2m1_seq', 'online_E_fs_L64_asy'])
 def test_keep_history_false_matches(name):
     """Two-slot rings for w / wExt (keepHistory=False) read wExt[r] from the
