@@ -118,6 +118,8 @@ struct danse_engine {
   int *resGateRound = nullptr, *resDanseFni = nullptr, *resErr = nullptr, *resFams = nullptr;
   float* resFrames = nullptr;
   int* resChanNode = nullptr;        // [MT] node of each channel
+  unsigned long long* resTrace = nullptr;   // DANSE_RESIDENT_TRACE diagnostics
+  size_t resTraceBytes = 0;
   int resNFam = 0;
 };
 
@@ -718,7 +720,7 @@ void danse_engine_destroy(danse_engine* eng) {
                   eng->cdRes, eng->dCEnd, eng->Cspec, eng->dChanNode, eng->dCPhase, eng->dxFrames, eng->dxOut,
                   eng->dxEst, eng->resYB, eng->resYU, eng->resZall, eng->resZhat, eng->resRyyG, eng->resRnnG,
                   eng->resUFlag, eng->resZFlag, eng->resGateRound, eng->resDanseFni, eng->resErr, eng->resFams,
-                  eng->resFrames, eng->resChanNode};
+                  eng->resFrames, eng->resChanNode, eng->resTrace};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (eng->dx) danse_dxcp_destroy(eng->dx);
@@ -927,6 +929,7 @@ static int resident_prepare(danse_engine* eng, int& NB) {
   if (e->cohDrift || e->dxcpOn) return fail(e, "resident run: no CohDrift / DXCP estimation");
   if (e->dCEnd) return fail(e, "resident run: no centralised raw frames (cEnd)");
   if (!e->gevd) return fail(e, "resident run: GEVD filters only");
+  if (2 * e->Ns != e->N || e->Ns > 512) return fail(e, "resident run: 50 % frame overlap (Ns = N / 2 = 512) only");
   int dmax = 1;
   for (const auto& fn : e->fns) {
     if (fn.packed || fn.D > 12) return fail(e, "resident run: filter dimensions <= 12 in grid storage (smallDGrid)");
@@ -1004,6 +1007,16 @@ int danse_engine_run_resident(danse_engine* eng, void* stream) {
   ra.RnnG = eng->resRnnG;
   ra.err = eng->resErr;
   const int grid = ra.nZ + S * nFN * FG;
+  if (std::getenv("DANSE_RESIDENT_TRACE")) {
+    const size_t nb = (size_t)R * grid * 2 * sizeof(unsigned long long);
+    if (eng->resTraceBytes != nb) {
+      if (eng->resTrace) (void)hipFree(eng->resTrace);
+      HIPCHK(hipMalloc((void**)&eng->resTrace, nb));
+      eng->resTraceBytes = nb;
+    }
+    HIPCHK(hipMemsetAsync(eng->resTrace, 0, nb, st));
+    ra.trace = eng->resTrace;
+  }
   int fits = 0;
   const int chk = resident_launch(NB, eng->rank == 1, ra, grid, st, true, &fits);
   if (chk < 0) return fail(eng, "resident run: occupancy query failed");
@@ -1049,6 +1062,15 @@ int danse_engine_run_resident(danse_engine* eng, void* stream) {
     resident_synth(b, eng->resFams, eng->resNFam, eng->resFrames, st);
   }
   HIPCHK(hipGetLastError());
+  return 0;
+}
+
+// diagnostics: the DANSE_RESIDENT_TRACE wall-clock marks of the last
+// resident run ([R][grid][2] uint64, 100 MHz), bytes = 0 if none
+int danse_engine_resident_trace(danse_engine* eng, void* dst, size_t* bytes) {
+  if (!eng || !bytes) return fail(eng, "null argument");
+  if (dst && eng->resTrace) HIPCHK(hipMemcpy(dst, eng->resTrace, std::min(*bytes, eng->resTraceBytes), hipMemcpyDeviceToHost));
+  *bytes = eng->resTraceBytes;
   return 0;
 }
 

@@ -173,6 +173,10 @@ DANSE_DEV cf load_y(const UpdateArgs& a, const FamNode& d, int s, int f, int li,
   return csel(act, v, cf{0.0f, 0.0f});
 }
 
+// Relaxed external filter entry b wExt[i] + (1 - b) target (one function
+// for every caller, so that every caller rounds it alike)
+DANSE_DEV cf ext_relax(float be, cf ep, cf tg) { return be * ep + (1.0f - be) * tg; }
+
 // External filters (DANSE family, update_external_filters,
 // d_classes.py:1627-1694) and dhat = w^H yhat (d_base.py:2075, DC / Nyquist
 // forced real, quirk Q7) of one (scene, family-node, bin); lane li of the
@@ -198,7 +202,7 @@ DANSE_DEV cf node_bin_tail(const UpdateArgs& a, const FamNode& d, int s, int f, 
       else {
         const float be = a.betaExt[s * a.K + d.k];
         const cf tg = tgt[li];
-        ne = be * eprev[li] + (1.0f - be) * tg;
+        ne = ext_relax(be, eprev[li], tg);
         if (fl & DANSE_FLAG_EXT_TARGET) tgt[li] = (1.0f - a.alphaExt) * tg + a.alphaExt * w;
       }
       enext[li] = ne;

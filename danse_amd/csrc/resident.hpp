@@ -64,7 +64,14 @@ struct ResArgs {
   cf* RyyG;
   cd* RnnG;
   int* err;                   // [1]: a wait gave up
+  unsigned long long* trace;  // diagnostics (DANSE_RESIDENT_TRACE): [R][grid][2] wall clock after the
+                              // wait / at the publish of every wave and round, or null
 };
+
+DANSE_DEV void trace_mark(const ResArgs& ra, int r, int slot) {
+  if (ra.trace && __lane_id() == 0)
+    ra.trace[((long long)r * gridDim.x + blockIdx.x) * 2 + slot] = wall_clock64();
+}
 
 // Wave-uniform wait until flags[0 .. n) >= target (each lane polls every
 // 64th flag with sc1 loads).  False if it gave up.
@@ -88,20 +95,44 @@ DANSE_DEV void publish(unsigned* flag, unsigned v) {
 }
 
 // ---- the Z wave of (scene s, node k): rounds 1 .. R - 1 (round 0's
-// broadcast is the ordinary bcast_kernel before the launch)
-DANSE_DEV void z_role(const ResArgs& ra, int s, int k, cf* L, float* zq) {
+// broadcast is the ordinary bcast_kernel before the launch).  Everything it
+// re-reads every round stays on the chip: the FFT twiddles and the window
+// values of its lanes in registers, the OLA state (the previous z frame,
+// zPrev of bcast_kernel) in LDS, double-buffered by round parity; from HBM
+// it reads only the fused spectrum and writes the stream and the spectra.
+DANSE_DEV void z_role(const ResArgs& ra, int s, int k, cf* L, float* zqb, float* nvL) {
   const BcastArgs& a = ra.b;
   const int N = a.N, Ns = a.Ns, F = a.F, K = a.K, S = a.S;
   const float sqNs = sqrtf((float)Ns);
   const float invSqNs = 1.0f / sqNs;
   const float sc = sqNs / (float)N;
-  const int l = __lane_id();
+  const int l0 = __lane_id();
   const unsigned* uf = ra.uFlag + ((long long)s * ra.nFN + ra.danseFni[k]) * ra.FG;
   const cf* zh = ra.zhat + ((long long)s * K + k) * F;
-  float* zpv = a.zPrev + ((long long)s * K + k) * N;
   float* zs = a.zStream + ((long long)s * K + k) * a.zLen;
+  wfft::TwReg tw;
+  tw.load(a.tw);
+  float hA[16], hS[16];   // (the OLA normalisation goes to LDS: registers are the limit here)
+#pragma unroll
+  for (int j = 0; j < 16; ++j) hA[j] = a.hA[l0 + 64 * j];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) hS[c] = a.hS[wfft::out_index(c)];
+  for (int n = l0; n < Ns; n += 64) nvL[n] = a.normVal[n];
+  // round 0's z frame (bcast_kernel left it in zPrev) -> buffer 0
+  {
+    const float* zpv = a.zPrev + ((long long)s * K + k) * N;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) zqb[l0 + 64 * j] = zpv[l0 + 64 * j];
+  }
   for (int r = 1; r < ra.R; ++r) {
+    // (lane index laundered per round, as in the update waves: no
+    // lane-derived addresses hoisted out of the round loop)
+    int l = l0, zo = (r & 1) * 1024;
+    asm volatile("" : "+v"(l), "+v"(zo));
+    float* zq = zqb + zo;                  // this round's frame
+    const float* zp = zqb + (1024 - zo);   // the previous round's
     if (!wait_all(uf, ra.FG, (unsigned)r, ra.err)) return;
+    trace_mark(ra, r, 0);
     // z synthesis: sqrt(Ns) * real(ifft(herm-ext(zhat))) * f, OLA with the previous frame
     cf v[16];
 #pragma unroll
@@ -112,42 +143,34 @@ DANSE_DEV void z_role(const ResArgs& ra, int s, int k, cf* L, float* zq) {
       if (nn == 0 || nn == F - 1) z.im = 0.0f;
       v[j] = (n < F) ? conjg(z) : z;
     }
-    wfft::fft1024(v, L, a.tw);
+    wfft::fft1024_tw(v, L, tw);
     bool nz = false;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) nz = nz || (zpv[l + 64 * j] != 0.0f);
+    for (int j = 0; j < 16; ++j) nz = nz || (zp[l + 64 * j] != 0.0f);
     const bool prevNZ = __ballot(nz) != 0ull;
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
       const int n = wfft::out_index(c);
-      float zc = sc * v[c].re * a.hS[n];
+      float zc = sc * v[c].re * hS[c];
       if (prevNZ) {
-        float t = (n < N - Ns) ? zpv[n + Ns] : 0.0f;
+        float t = (n < N - Ns) ? zp[n + Ns] : 0.0f;
         t += zc;
-        if (n < Ns) t = t / a.normVal[n];
+        if (n < Ns) t = t / nvL[n];
         zc = t;
       }
       zq[n] = zc;
     }
     wfft::wave_sync();
+    // the z frame the receivers consume at round r: stream [(r-1)Ns, (r+1)Ns)
+    // = the previous frame's first Ns samples, then this one's
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       const int n = l + 64 * j;
-      zpv[n] = zq[n];
+      const float t = (n < Ns) ? zp[n] : zq[n - Ns];
       if (n < Ns) zs[(long long)r * Ns + n] = zq[n];
+      v[j] = cf{t * hA[j], 0.0f};
     }
-    // the z frame the receivers consume at round r: stream [(r+1)Ns - N, (r+1)Ns)
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int n = l + 64 * j;
-      const long long idx = (long long)(r + 1) * Ns - N + n;
-      float t;
-      if (idx < 0) t = 0.0f;
-      else if (idx >= (long long)r * Ns) t = zq[idx - (long long)r * Ns];
-      else t = zs[idx];
-      v[j] = cf{t * a.hA[n], 0.0f};
-    }
-    wfft::fft1024(v, L, a.tw);
+    wfft::fft1024_tw(v, L, tw);
     cf* Zs = const_cast<cf*>(ra.u.Zspec) + (((long long)(r + 1) * K + k) * S + s) * F;
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
@@ -155,14 +178,44 @@ DANSE_DEV void z_role(const ResArgs& ra, int s, int k, cf* L, float* zq) {
       if (f < F) st_sc1(Zs + f, invSqNs * v[c]);
     }
     publish(ra.zFlag + (long long)s * K + k, (unsigned)r);
+    trace_mark(ra, r, 1);
   }
 }
 
 template <int NB>
 constexpr int lds_bytes() {
   constexpr int u = (int)sizeof(t2d::LDS2<NB, kG>) * kBins + (int)sizeof(cf) * kBins * 16 * t2d::vpl<NB, kG>();
-  constexpr int z = (int)sizeof(cf) * wfft::kLdsElems + (int)sizeof(float) * 1024;
+  constexpr int z = (int)sizeof(cf) * wfft::kLdsElems + (int)sizeof(float) * (2048 + 512);
   return u > z ? u : z;
+}
+
+// The fused spectrum of round r + 1 for this wave's bins from the new
+// external filter entries ne (lane li: mic li + L v) and the prefetched
+// broadcast-frame spectra: bcast.hpp phase 1 + the part[] sum of phase 2 in
+// the same order (per broadcast wave w the mics m = w, w + 4, ..., then the
+// four partial sums left to right).  Stored sc1 for the Z wave.
+template <int V>
+DANSE_DEV void fused_next(const ResArgs& ra, const UpdateArgs& a, const FamNode& d, int s, int f, int li, bool fvalid,
+                          int r, cf* zt, const cf (&ne)[V], const cf (&yb)[V]) {
+  constexpr int L = 16;
+  if (r + 1 >= ra.R) return;
+  const int M = d.M;
+  sfor<0, V>([&](auto vc) {
+    constexpr int v = decltype(vc)::value;
+    const int m = li + L * v;
+    if (m < M) zt[m] = cmul(ne[v], yb[v]);
+  });
+  t2d::wsync();
+  if (li == 0 && fvalid) {
+    cf z = cf{0.0f, 0.0f};
+    for (int wv = 0; wv < kBcWaves; ++wv) {
+      cf part = cf{0.0f, 0.0f};
+      for (int m = wv; m < M; m += kBcWaves) part = part + zt[m];
+      z = (wv == 0) ? part : z + part;
+    }
+    st_sc1(ra.zhat + ((long long)s * a.K + d.k) * a.F + f, z);
+  }
+  t2d::wsync();
 }
 
 template <int NB, int RMAX>
@@ -176,8 +229,8 @@ resident_kernel(const ResArgs ra) {
 #ifndef RES_NOZ
   if (id < ra.nZ) {
     const int K = ra.b.K;
-    z_role(ra, id / K, id % K, reinterpret_cast<cf*>(smem),
-           reinterpret_cast<float*>(smem + sizeof(cf) * wfft::kLdsElems));
+    float* zqb = reinterpret_cast<float*>(smem + sizeof(cf) * wfft::kLdsElems);
+    z_role(ra, id / K, id % K, reinterpret_cast<cf*>(smem), zqb, zqb + 2048);
     return;
   }
 #endif
@@ -231,9 +284,46 @@ resident_kernel(const ResArgs ra) {
     LDS2<NB, G>& S = *reinterpret_cast<LDS2<NB, G>*>(smem + sOff);
     const int p = li / G, q = li % G;
     if (r > 0 && !wait_all(ra.zFlag + (long long)s * K, K, (unsigned)r, ra.err)) break;
+    trace_mark(ra, r, 0);
+    // the next round's broadcast-frame spectra of this node's mics (for the
+    // fused spectrum at the end of the round): issued now, used after the solve
+    cf ybPre[V];
+    sfor<0, V>([&](auto vc) {
+      constexpr int v = decltype(vc)::value;
+      const int m = li + L * v;
+      const bool use = isDanse && r + 1 < ra.R && m < d.M;
+      const int ch = a.chanList[d.chanOff + (use ? m : 0)];
+      ybPre[v] = use ? ra.YB[(((long long)(r + 1) * a.S + s) * a.MT + ch) * F + f] : cf{0.0f, 0.0f};
+    });
     const uint8_t fl = a.flags[(((long long)r * a.S + s) * kMaxFam + d.fam) * K + d.k];
     const int opY = fl & 3, opN = (fl >> 2) & 3;
     const bool pregiven = (fl & DANSE_FLAG_PREGIVEN) != 0;
+    // Relaxed (and kept / reference-only) external filters do not depend on
+    // this round's solve: wExt[r + 1] = b wExt[r] + (1 - b) target, with the
+    // target as it stood before this round (d_classes.py:1627-1694).  So
+    // the fused spectrum of round r + 1 is formed and published FIRST, and
+    // the broadcast of round r + 1 runs while this round's solve does.
+    const bool early = isDanse && !pregiven && d.extMode != DANSE_EXT_COPY;
+    if (early) {
+      const long long eb = (long long)s * a.wExtStride + d.wExtOff;
+      const cf* eprev = a.wExtHist + eb + ((long long)(a.wExtHistory ? r : (r & 1)) * F + f) * d.M;
+      const cf* tgt = a.wExtTarget + (long long)s * a.tgtStride + d.tgtOff + (long long)f * d.M;
+      const float be = a.betaExt[s * K + d.k];
+      cf neE[V];
+      sfor<0, V>([&](auto vc) {
+        constexpr int v = decltype(vc)::value;
+        const int m = li + L * v;
+        const bool in = m < d.M;
+        const int mm = in ? m : 0;
+        cf ne;
+        if (d.extMode == DANSE_EXT_KEEP) ne = eprev[mm];
+        else if (d.extMode == DANSE_EXT_REFONLY) ne = cf{(m == d.ref) ? 1.0f : 0.0f, 0.0f};
+        else ne = ext_relax(be, eprev[mm], tgt[mm]);
+        neE[v] = ne;
+      });
+      fused_next(ra, a, d, s, f, li, fvalid, r, zt, neE, ybPre);
+      publish(myFlag, (unsigned)(r + 1));
+    }
     const bool solve = (fl & DANSE_FLAG_SOLVE) != 0 && !pregiven;
     const bool initslot = (fl & DANSE_FLAG_INITSLOT) != 0;
     if (opN) liValid = false;
@@ -342,35 +432,12 @@ resident_kernel(const ResArgs ra) {
       ne[v] = node_bin_tail(a, d, s, f, li + L * v, fl, pregiven, fvalid, w[v], y[v], dh);
     });
 
-    // ---- fused spectrum of round r + 1 (bcast.hpp phase 1 + the part[]
-    // sum of phase 2, in the same order: per broadcast wave w the mics
-    // m = w, w + 4, ..., then the four partial sums left to right)
-#ifndef RES_NOZH
-    if (isDanse && r + 1 < ra.R) {
-      const int M = d.M;
-      sfor<0, V>([&](auto vc) {
-        constexpr int v = decltype(vc)::value;
-        const int m = li + L * v;
-        if (m < M) {
-          const int ch = a.chanList[d.chanOff + m];
-          const cf Yb = ra.YB[(((long long)(r + 1) * a.S + s) * a.MT + ch) * F + f];
-          zt[m] = cmul(ne[v], Yb);
-        }
-      });
-      t2d::wsync();
-      if (li == 0 && fvalid) {
-        cf z = cf{0.0f, 0.0f};
-        for (int wv = 0; wv < kBcWaves; ++wv) {
-          cf part = cf{0.0f, 0.0f};
-          for (int m = wv; m < M; m += kBcWaves) part = part + zt[m];
-          z = (wv == 0) ? part : z + part;
-        }
-        st_sc1(ra.zhat + ((long long)s * K + d.k) * F + f, z);
-      }
-      t2d::wsync();
+    if (!early) {
+      // wExt[r + 1] = w[r + 1] (EXT_COPY): after the solve
+      if (isDanse) fused_next(ra, a, d, s, f, li, fvalid, r, zt, ne, ybPre);
+      publish(myFlag, (unsigned)(r + 1));
     }
-#endif
-    publish(myFlag, (unsigned)(r + 1));
+    trace_mark(ra, r, 1);
   }
 
   // final SCMs back to HBM (the engine's state after the run)

@@ -93,14 +93,15 @@ DANSE_DEV void wave_sync() {
 // a wave is 512 contiguous bytes), then [a][c] = W64^(a c) (4 x 16).
 constexpr int kTwElems = 16 * 64 + 4 * 16;
 
-// Forward FFT of the wave's 1024 points (layout above).  lds: this wave's
-// kLdsElems-complex scratch.  tw: the kTwElems table above.
-DANSE_DEV void fft1024(cf (&v)[16], cf* lds, const cf* __restrict__ tw) {
+// Forward FFT of the wave's 1024 points (layout above), the twiddles from
+// TW: tw1(k1) = W1024^(l k1), k1 = 1..15, and tw2(c) = W64^(a c), c = 1..15.
+template <typename TW>
+DANSE_DEV void fft1024_tw(cf (&v)[16], cf* lds, const TW& tw) {
   const int l = __lane_id();
   // A: DFT over j, twiddle W1024^(l k1)
   dft16(v);
 #pragma unroll
-  for (int k1 = 1; k1 < 16; ++k1) v[k1] = v[k1] * tw[k1 * 64 + l];
+  for (int k1 = 1; k1 < 16; ++k1) v[k1] = v[k1] * tw.tw1(k1);
   wave_sync();   // the previous FFT's reads of lds are done
 #pragma unroll
   for (int k1 = 0; k1 < 16; ++k1) lds[k1 * kPitch + l] = v[k1];
@@ -111,7 +112,7 @@ DANSE_DEV void fft1024(cf (&v)[16], cf* lds, const cf* __restrict__ tw) {
   for (int b = 0; b < 16; ++b) v[b] = lds[k1 * kPitch + 4 * b + a];
   dft16(v);
 #pragma unroll
-  for (int c = 1; c < 16; ++c) v[c] = v[c] * tw[16 * 64 + a * 16 + c];
+  for (int c = 1; c < 16; ++c) v[c] = v[c] * tw.tw2(c);
   // C: 4-point DFT over a across the quad.  Stage 1 pairs a, a ^ 2
   // (a1 = a >> 1 becomes e0, twiddle W4^(a0 e0)), stage 2 pairs a, a ^ 1
   // (a0 becomes e1).
@@ -125,6 +126,28 @@ DANSE_DEV void fft1024(cf (&v)[16], cf* lds, const cf* __restrict__ tw) {
     v[c] = hi0 ? q - t : t + q;
   }
 }
+
+// twiddles read from the kTwElems table in memory
+struct TwMem {
+  const cf* __restrict__ tw;
+  DANSE_DEV cf tw1(int k1) const { return tw[k1 * 64 + __lane_id()]; }
+  DANSE_DEV cf tw2(int c) const { return tw[16 * 64 + (__lane_id() & 3) * 16 + c]; }
+};
+// twiddles held in registers (a persistent wave that transforms every round)
+struct TwReg {
+  cf t1[16], t2[16];
+  DANSE_DEV void load(const cf* __restrict__ tw) {
+#pragma unroll
+    for (int i = 1; i < 16; ++i) {
+      t1[i] = tw[i * 64 + __lane_id()];
+      t2[i] = tw[16 * 64 + (__lane_id() & 3) * 16 + i];
+    }
+  }
+  DANSE_DEV cf tw1(int k1) const { return t1[k1]; }
+  DANSE_DEV cf tw2(int c) const { return t2[c]; }
+};
+
+DANSE_DEV void fft1024(cf (&v)[16], cf* lds, const cf* __restrict__ tw) { fft1024_tw(v, lds, TwMem{tw}); }
 
 // Frequency index of output element c on this lane.
 DANSE_DEV int out_index(int c) {

@@ -183,6 +183,11 @@ int danse_engine_run(danse_engine* eng, int32_t r0, int32_t r1, void* stream, in
  * gives up sets the flag danse_engine_resident_error reads.             */
 int danse_engine_run_resident(danse_engine* eng, void* stream);
 int danse_engine_resident_error(danse_engine* eng, int32_t* err, void* stream);
+/* Diagnostics: with DANSE_RESIDENT_TRACE set, the last resident run's
+ * per-(round, wave) wall-clock marks ([R][waves][2] uint64, 100 MHz: after
+ * the wait, at the publish); *bytes in: capacity of dst (may be NULL), out:
+ * the size. */
+int danse_engine_resident_trace(danse_engine* eng, void* dst, size_t* bytes);
 
 /* Fine-grained per-round phases (multi-GPU: the caller all-gathers the fused
  * spectra between them).  bcast(r) also synthesises the estimates of r-1. */
