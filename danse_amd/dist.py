@@ -127,9 +127,15 @@ class ShardedRun:
             g = torch.cuda.CUDAGraph()
             side = torch.cuda.Stream(device=self.zbuf.device)
             side.wait_stream(torch.cuda.current_stream(self.zbuf.device))
+            # the state reset (memsets + two kernels) stays OUT of the graph:
+            # captured, its memset nodes were not re-applied from the second
+            # replay on (the second replay started from the previous run's
+            # streams and estimates: profiles/round3/pytest_gpu_r3g.log)
             with torch.cuda.graph(g, stream=side):
-                self._rounds(reset, gate)
+                self._rounds(False, gate)
             self._graphs[key] = g
+        if reset:
+            self.eng.reset()
         g.replay()
 
     def _all_ok(self, ok):

@@ -9,8 +9,10 @@
     verdicts are all-reduced and every rank repeats the run exactly;
   - CohDrift SRO estimation on a sharded engine (each rank estimates for its
     own receivers from the all-gathered fused spectra);
-* world size 1 over RCCL: the round sequence (bcast, all-gather, gate,
-  update) captured into a CUDA graph and replayed equals the eager run.
+* world size 1 over RCCL: the round sequence (bcast, gate, update; the
+  all-gather of one rank is the identity and is not issued, see
+  ``ShardedRun.exchange``) captured into a CUDA graph and replayed equals the
+  eager run.
 """
 import os
 import sys
