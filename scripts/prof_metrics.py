@@ -1,5 +1,5 @@
-"""fwSNRseg on 64 pairs of 10 s signals (the E battery's per-scene metric
-batch) for a rocprofv3 kernel-statistics run."""
+"""fwSNRseg and eSTOI on 64 pairs of 10 s signals (the E battery's
+per-scene metric batch) for a rocprofv3 kernel-statistics run."""
 import sys
 from pathlib import Path
 
@@ -16,3 +16,7 @@ for _ in range(3):
     per, mean = DM.fwsnrseg_batch(c, e, 16000.0)
 torch.cuda.synchronize()
 print('frames', per.shape, 'mean[0]', float(mean[0]))
+for _ in range(3):
+    st = DM.stoi_batch(c, e, 16000, extended=True)
+torch.cuda.synchronize()
+print('estoi[0]', float(np.asarray(st.cpu() if hasattr(st, 'cpu') else st).ravel()[0]))

@@ -181,6 +181,12 @@ BIG_CASES = [
     # classes (D = 15, centralised 24): the lower-triangle reading of eigh
     dict(name='online_big_init_random', M=[12, 6, 3, 3], dur=3.0, seed=24,
          danse=dict(next(c for c in ONLINE_CASES if c['name'] == 'online_init_random_asy')['danse'])),
+    # the GEVD of classes 56 and 64 (D 49..64, update_kernel_big: row per
+    # lane, runtime pivot loops) next to lane-class nodes
+    dict(name='online_big_D51_asy', M=[48, 2, 2, 2], dur=6.0, seed=25,
+         danse=dict(ONLINE_CASES[1]['danse'], nodeUpdating='asy')),
+    dict(name='online_big_D60_seq_r2', M=[57, 2, 2, 2], dur=6.0, seed=26,
+         danse=dict(ONLINE_CASES[1]['danse'], nodeUpdating='seq', GEVDrank=2)),
 ]
 
 
