@@ -72,6 +72,13 @@ WORKLOADS = {
     'C': dict(M=[4] * 16, dur=10.0, nodeUpdating='asy', scenes=8, sros=[float(x) for x in np.linspace(0, 200, 16)],
               extra=dict(compensateSROs=True, includeFSDflags=True, estimateSROs='CohDrift', cohdrift_ls=True),
               desc='C: GEVD-DANSE r1, K=16 x 4 mics (D=19), SROs 0..200 ppm, CohDrift estimation + compensation, asy, 10 s'),
+    # BASELINE.json configs[2] as named: DXCP-PhaT SRO estimation (the
+    # device estimators per (receiver, sender) pair on the received z
+    # streams, danse_cfg.dxcp) + compensation, K = 16 x 4, SROs 0..200 ppm
+    'C_dxcp': dict(M=[4] * 16, dur=10.0, nodeUpdating='asy', scenes=8, sros=[float(x) for x in np.linspace(0, 200, 16)],
+                   extra=dict(compensateSROs=True, includeFSDflags=True, estimateSROs='DXCPPhaT'),
+                   desc='C: GEVD-DANSE r1, K=16 x 4 mics (D=19), SROs 0..200 ppm, DXCP-PhaT estimation + '
+                        'compensation, asy, 10 s'),
     'B_seq': dict(M=[4] * 8, dur=10.0, nodeUpdating='seq', scenes=31, desc='B (seq): GEVD-DANSE r1, K=8 x 4 mics, seq, 10 s'),
     'small': dict(M=[2] * 4, dur=3.0, nodeUpdating='asy', desc='small smoke workload K=4 x 2, 3 s'),
     # BASELINE.json configs[4] scene shape (tests/battery20230919_perf_asfctofL.py:14-88):
@@ -711,9 +718,15 @@ def cpu_baseline(M, wl, dp, wp, seconds, rounds=None):
     starts = _gate_rounds(sc, D)
     R = rounds or (int((sc.wasn[0].data.shape[0] - dp.DFTsize) / dp.Ns) + 1)
     r0 = int(starts.min())
+    kw = {}
+    dxcp = getattr(dp, 'estimateSROs', 'Oracle') == 'DXCPPhaT'
+    if dxcp:
+        # the DANSE part with external (zero) SRO estimates; the DXCP-PhaT
+        # estimators are timed on their own below (oracle/dxcp_ref.py)
+        kw['sroEstimates'] = [np.zeros((R + 1, K - 1)) for _ in range(K)]
     # t_round: rounds 1..n of the real run (round 0 carries the set-up)
     npre = int(max(3, min(r0 - 1, 12)))
-    probe = O.OnlineDANSE(sc, dp, vadMinProp=wp.vadMinProportionActive, maxRounds=npre + 1)
+    probe = O.OnlineDANSE(sc, dp, vadMinProp=wp.vadMinProportionActive, maxRounds=npre + 1, **kw)
     probe.run()
     rt = probe.roundTimes
     t_round = (rt[-1][1] - rt[1][1]) / max(rt[-1][0] - rt[1][0], 1)
@@ -737,7 +750,7 @@ def cpu_baseline(M, wl, dp, wp, seconds, rounds=None):
     if budget <= 2.0 * seconds and R - rlast - 2 >= 1:
         nwin = int(max(1, min(R - rlast - 2, seconds / max(t_round + K * t_solve_sample, 1e-3))))
         # (the window skips the gate round itself, whose Hermitian/PSD/rank check costs one more eigh)
-        ov = O.OnlineDANSE(sc, dp, vadMinProp=wp.vadMinProportionActive, maxRounds=rlast + 1 + nwin)
+        ov = O.OnlineDANSE(sc, dp, vadMinProp=wp.vadMinProportionActive, maxRounds=rlast + 1 + nwin, **kw)
         ov.run()
         rt = dict(ov.roundTimes)
         t_post = (rt[rlast + 1 + nwin] - rt[rlast + 1]) / nwin
@@ -750,6 +763,24 @@ def cpu_baseline(M, wl, dp, wp, seconds, rounds=None):
                   f'{F} bins x D={D} ({nrep} reps)')
         sampled = rt[-1][1] - rt[0][1] + t_solve * nrep
     total = R * t_round + float(np.sum(np.maximum(R - starts, 0))) * t_solve
+    if dxcp:
+        # DXCP-PhaT (the reference's DXCPPhaT class, restated): one estimator
+        # per (receiver, sender), fed a 2048-sample block every 4 rounds
+        from oracle import dxcp_ref as X
+        est = X.DXCPPhaT()
+        rng = np.random.default_rng(0)
+        blk = rng.standard_normal((X.FRAME, 2))
+        for _ in range(8):
+            est.process_data(blk)
+        t = time.perf_counter()
+        nb = 0
+        while nb < 8 or time.perf_counter() - t < 1.0:
+            est.process_data(blk)
+            nb += 1
+        t_dx = (time.perf_counter() - t) / nb
+        nfed = R * dp.Ns // X.FRAME
+        total += K * (K - 1) * nfed * t_dx
+        method += f'; DXCP-PhaT {K * (K - 1)} estimators x {nfed} blocks at {t_dx * 1e3:.2f} ms per block'
     cores, threads, env = _threads()
     return {'value': K * F * R / total, 'unit': 'frame-updates/s', 'cores': threads, 'kind': 'port',
             'sample': f'float64 oracle (reference algorithm, per-bin scipy eigh), one process, default BLAS threads '
