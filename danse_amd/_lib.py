@@ -87,6 +87,8 @@ SIGNATURES = {
     'danse_engine_reset': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p]),
     'danse_engine_run': (_c_i32, [ctypes.c_void_p, _c_i32, _c_i32, ctypes.c_void_p, _c_i32]),
     'danse_engine_run_resident': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p]),
+    'danse_engine_set_cond': (_c_i32, [ctypes.c_void_p, _c_i32]),
+    'danse_engine_cond': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
     'danse_engine_resident_error': (_c_i32, [ctypes.c_void_p, ctypes.POINTER(_c_i32), ctypes.c_void_p]),
     'danse_engine_resident_trace': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_size_t)]),
     'danse_engine_bcast': (_c_i32, [ctypes.c_void_p, _c_i32, ctypes.c_void_p]),

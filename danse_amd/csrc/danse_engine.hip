@@ -17,6 +17,7 @@
 #include "tzconv.hpp"
 #include "resident.hpp"
 #include "resident_api.hpp"
+#include "cond.hpp"
 
 using namespace danse;
 
@@ -121,6 +122,9 @@ struct danse_engine {
   unsigned long long* resTrace = nullptr;   // DANSE_RESIDENT_TRACE diagnostics
   size_t resTraceBytes = 0;
   int resNFam = 0;
+  // condition numbers of Ryy (cond.hpp), every condEvery-th iteration
+  int condEvery = 0;
+  double* condHist = nullptr;   // [S][nFN][R][F]
 };
 
 static thread_local std::string g_lastErr;
@@ -720,7 +724,7 @@ void danse_engine_destroy(danse_engine* eng) {
                   eng->cdRes, eng->dCEnd, eng->Cspec, eng->dChanNode, eng->dCPhase, eng->dxFrames, eng->dxOut,
                   eng->dxEst, eng->resYB, eng->resYU, eng->resZall, eng->resZhat, eng->resRyyG, eng->resRnnG,
                   eng->resUFlag, eng->resZFlag, eng->resGateRound, eng->resDanseFni, eng->resErr, eng->resFams,
-                  eng->resFrames, eng->resChanNode, eng->resTrace};
+                  eng->resFrames, eng->resChanNode, eng->resTrace, eng->condHist};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (eng->dx) danse_dxcp_destroy(eng->dx);
@@ -776,6 +780,14 @@ static void launch_update(danse_engine* e, int r, hipStream_t st) {
     a.fn = cl.dev;
     a.famNodeId = cl.devIds;
     launch_update_class(cl.DMAX, a, st);   // D > kMaxDMax rejected at create time
+  }
+  if (e->condEvery > 0 && (r + 1) % e->condEvery == 0) {
+    // (saved when i - last >= every, last starting at -1: d_classes.py:2128-2130)
+    int dm = 1;
+    for (const auto& fn : e->fns) dm = std::max(dm, fn.D);
+    const size_t lds = (size_t)dm * (dm + 1) * sizeof(cd);
+    hipLaunchKernelGGL(cond_kernel, dim3(e->F, e->S * (int)e->fns.size()), dim3(64), lds, st, make_update(e, r),
+                       e->dFnAll, (int)e->fns.size(), e->condHist);
   }
   if (e->cohDrift) {
     CohDriftArgs c{};
@@ -1062,6 +1074,34 @@ int danse_engine_run_resident(danse_engine* eng, void* stream) {
     resident_synth(b, eng->resFams, eng->resNFam, eng->resFrames, st);
   }
   HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int danse_engine_set_cond(danse_engine* eng, int32_t every) {
+  if (!eng || every < 0) return fail(eng, "bad condition-number interval");
+  HIPCHK(hipSetDevice(eng->dev));
+  if (eng->graphExec) {   // the captured run changes
+    (void)hipGraphExecDestroy(eng->graphExec);
+    eng->graphExec = nullptr;
+  }
+  eng->condEvery = every;
+  if (every > 0 && !eng->condHist) {
+    const size_t n = (size_t)eng->S * eng->fns.size() * eng->R * eng->F;
+    HIPCHK(dalloc(&eng->condHist, n));
+    std::vector<double> nan(n, std::nan(""));
+    HIPCHK(hipMemcpy(eng->condHist, nan.data(), n * sizeof(double), hipMemcpyHostToDevice));
+  }
+  return 0;
+}
+
+int danse_engine_cond(danse_engine* eng, double* dst, size_t bytes) {
+  if (!eng || !dst) return fail(eng, "null argument");
+  if (!eng->condHist) return fail(eng, "condition numbers are not enabled (danse_engine_set_cond)");
+  const size_t n = (size_t)eng->S * eng->fns.size() * eng->R * eng->F;
+  if (bytes < n * sizeof(double)) return fail(eng, "destination too small");
+  HIPCHK(hipSetDevice(eng->dev));
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(dst, eng->condHist, n * sizeof(double), hipMemcpyDeviceToHost));
   return 0;
 }
 

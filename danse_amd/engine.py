@@ -22,7 +22,6 @@ Control-byte derivation restates, per round i and node k:
 from __future__ import annotations
 
 import ctypes
-import warnings
 from dataclasses import dataclass
 
 import numpy as np
@@ -234,6 +233,12 @@ class DanseEngine:
                     y[s, base[k]:base[k] + self.M[k], :] = arr.T
             self.y = torch.from_numpy(y).to(f'cuda:{device}')
         L.check(self.lib.danse_engine_set_inputs(self.eng, ctypes.c_void_p(self.y.data_ptr())), self.eng)
+        # condition numbers of Ryy (ConditionNumbers, d_classes.py:19-130,2126-2186)
+        self.condEvery = int(p.saveConditionNumberEvery) if getattr(p, 'saveConditionNumber', False) else 0
+        if self.condEvery:
+            if self.resident:
+                raise NotImplementedError('condition numbers on the resident engine')
+            L.check(self.lib.danse_engine_set_cond(self.eng, self.condEvery), self.eng)
         if pregiven is not None:
             self._load_pregiven(pregiven)
         self._load_init_history()
@@ -884,8 +889,7 @@ class DanseEngine:
                     full[:, :R + 1, :] = np.transpose(e[s], (1, 0, 2))
                 res[s].wTildeExt[k] = full
         diag = self.diagnostics()
-        if getattr(p, 'saveConditionNumber', False):
-            warnings.warn('saveConditionNumber: condition-number histories are not computed (dv.condNumbers = None)')
+        cond = self._cond_numbers() if self.condEvery else None
         # yinSTFT / yCentrBatch (d_classes.py:915-930): the whole-signal STFT of
         # the engine's inputs on the device, [S][F][nseg][Mtot]
         nseg = stft_frames(self.T, self.N, self.Ns)
@@ -924,9 +928,7 @@ class DanseEngine:
             r.computeCentralised = bool(p.computeCentralised)
             r.computeLocal = bool(p.computeLocal)
             r.computeSingleSensorBroadcast = bool(p.computeSingleSensorBroadcast)
-            # per-bin cond(Ryy) histories (d_classes.py:2127-2200, a debugging
-            # plot) are not computed on the device path
-            r.condNumbers = None
+            r.condNumbers = cond[s] if cond is not None else None
             r.startUpdates = self.startRound[s, 0] >= 0
             r.startRound = self.startRound[s, 0].copy()
             r.nInternalFilterUps = self.nSolves[s, 0].astype(np.float64)
@@ -942,6 +944,37 @@ class DanseEngine:
             r.nIter = nI
             r.nRounds = R
         return res
+
+    def _cond_numbers(self):
+        """Per scene, the reference's ConditionNumbers fields
+        (d_classes.py:19-130, 965-984): cn_Ryy{DANSE,Local,Centr}[k] (F,
+        saves) and iter_cn_*[k] (the iterations), for the owned nodes."""
+        import types
+        S, K, F, R = self.S, self.K, self.F, self.R
+        nOwn = self.k1 - self.k0
+        nFN = len(self.fams) * nOwn
+        h = np.empty(S * nFN * R * F)
+        L.check(self.lib.danse_engine_cond(self.eng, h.ctypes.data_as(ctypes.c_void_p), h.nbytes), self.eng)
+        h = h.reshape(S, nFN, R, F)
+        it = [r for r in range(R) if (r + 1) % self.condEvery == 0]
+        names = {L.FAM_DANSE: 'DANSE', L.FAM_LOCAL: 'Local', L.FAM_CENTR: 'Centr'}
+        out = []
+        for s in range(S):
+            cn = types.SimpleNamespace()
+            for nm in names.values():
+                setattr(cn, f'cn_Ryy{nm}', [np.empty((F, 0)) for _ in range(K)])
+                setattr(cn, f'iter_cn_Ryy{nm}', [[] for _ in range(K)])
+            cn.cn_RyyDANSEcomputed = True
+            cn.cn_RyyLocalComputed = bool(self.p.computeLocal)
+            cn.cn_RyyCentrComputed = bool(self.p.computeCentralised)
+            for fi, fam in enumerate(self.fams):
+                if fam not in names:
+                    continue
+                for j, k in enumerate(range(self.k0, self.k1)):
+                    getattr(cn, f'cn_Ryy{names[fam]}')[k] = h[s, fi * nOwn + j][it].T.copy()
+                    getattr(cn, f'iter_cn_Ryy{names[fam]}')[k] = list(it)
+            out.append(cn)
+        return out
 
     def close(self):
         if getattr(self, 'eng', None):

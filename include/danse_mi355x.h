@@ -189,6 +189,16 @@ int danse_engine_resident_error(danse_engine* eng, int32_t* err, void* stream);
  * the size. */
 int danse_engine_resident_trace(danse_engine* eng, void* dst, size_t* bytes);
 
+/* Condition numbers of Ryy (ConditionNumbers.get_new_cond_number,
+ * d_classes.py:19-130,2126-2186; saveConditionNumber /
+ * saveConditionNumberEvery): with every > 0, after the update of every round
+ * r with (r + 1) % every == 0, np.linalg.cond of every (scene, family-node,
+ * bin)'s Ryy (DANSE, local, centralised; NaN for SSBC).  danse_engine_cond
+ * copies [S][family-nodes in engine order][R][F] float64 (NaN where not
+ * saved) to host memory. */
+int danse_engine_set_cond(danse_engine* eng, int32_t every);
+int danse_engine_cond(danse_engine* eng, double* dst, size_t bytes);
+
 /* Fine-grained per-round phases (multi-GPU: the caller all-gathers the fused
  * spectra between them).  bcast(r) also synthesises the estimates of r-1. */
 int danse_engine_bcast(danse_engine* eng, int32_t r, void* stream);

@@ -20,6 +20,7 @@ full-sample-drift flags, and the batch engine (``d_batch.py``).
 from __future__ import annotations
 
 import copy
+import types
 
 import numpy as np
 import scipy.linalg as sla
@@ -384,6 +385,11 @@ class OnlineDANSE:
             self.centr.append(fam(self.Mtot, p.computeCentralised, refC))
             self.local.append(fam(self.M[k], p.computeLocal))
         self.i = np.zeros(K, dtype=int)
+        # condition numbers (d_classes.py:965-984)
+        self.condNumbers = types.SimpleNamespace(
+            **{f: [np.empty((self.F, 0)) for _ in range(K)] for f in ('cn_RyyDANSE', 'cn_RyyLocal', 'cn_RyyCentr')},
+            **{f: [[] for _ in range(K)] for f in ('iter_cn_RyyDANSE', 'iter_cn_RyyLocal', 'iter_cn_RyyCentr')})
+        self._cnLast = [[-1] * K for _ in range(3)]
         self.numUpdatesRyy = np.zeros(K, dtype=int)
         self.numUpdatesRnn = np.zeros(K, dtype=int)
         self.d = np.zeros((self.T, K))
@@ -699,6 +705,7 @@ class OnlineDANSE:
                 self._scm_update(k, self.centr[k], yCHat, self.centrVAD[i])
             if p.computeSingleSensorBroadcast:
                 self._scm_update(k, self.ssbc[k], ySHat, vad)
+            self._cond_numbers(k, i)
             self._check_covmats(k, tCurr)
             if not skipUpdate and not bypass:
                 self._perform_update(k, skipUpdateCentr)
@@ -754,6 +761,27 @@ class OnlineDANSE:
             _, dh = desired_sig_chunk(self.ssbc[k].w[:, i + 1, :], ySHat, self.f, nf, self.dSSBC[sl, k])
             self.dHatSSBC[:, i, k] = dh
         self.i[k] += 1
+
+    # ---- condition numbers (d_classes.py:2126-2186, ConditionNumbers
+    # .get_new_cond_number / compute_condition_numbers, d_classes.py:19-130):
+    # np.linalg.cond of every bin's Ryy after the frame's update, every
+    # saveConditionNumberEvery iterations, per family ----
+    def _cond_numbers(self, k, i):
+        p = self.p
+        if not getattr(p, 'saveConditionNumber', False):
+            return
+        cn = self.condNumbers
+        fams = [('DANSE', self.danse[k], 'cn_RyyDANSE', 'iter_cn_RyyDANSE', self._cnLast[0])]
+        if p.computeLocal:
+            fams.append(('local', self.local[k], 'cn_RyyLocal', 'iter_cn_RyyLocal', self._cnLast[1]))
+        if p.computeCentralised:
+            fams.append(('centralised', self.centr[k], 'cn_RyyCentr', 'iter_cn_RyyCentr', self._cnLast[2]))
+        for _, fam, fc, fi, last in fams:
+            if i - last[k] >= p.saveConditionNumberEvery:
+                c = np.array([np.linalg.cond(fam.Ryy[kappa]) for kappa in range(fam.Ryy.shape[0])])
+                getattr(cn, fc)[k] = np.concatenate((getattr(cn, fc)[k], c[:, np.newaxis]), axis=1)
+                getattr(cn, fi)[k].append(i)
+                last[k] = i
 
     # ---- spatial_covariance_matrix_update + conditional_scm_updating (2048-2267) ----
     def _scm_update(self, k, s: _SCMSet, y, vad):

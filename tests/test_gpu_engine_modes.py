@@ -330,3 +330,35 @@ def test_cohdrift_sro_estimates_vs_oracle():
         ed = np.asarray(dv.SROsEstimates[k])
         eo = np.asarray(ov.SROsEstimates[k])[:ed.shape[0]]
         assert float(np.max(np.abs(ed - eo))) <= 2e-3 * max(float(np.max(np.abs(eo))), 1e-12)
+
+
+def test_condition_numbers_vs_oracle():
+    """saveConditionNumber (ConditionNumbers, d_classes.py:19-130,2126-2186):
+    np.linalg.cond of every bin's Ryy after every saveConditionNumberEvery-th
+    update, DANSE and local families, against the oracle's float64 SCMs.  The
+    device SCMs are float32 (Ryy), so the comparison is in
+    log10 and only where the oracle's matrix is not numerically singular
+    (cond < 1e6; the first-frame basis is rank one)."""
+    from danse_amd.core import danse_multi
+    from oracle import danse_ref_cpu as O
+    case = dict(name='cond_k4m3', M=[3, 3, 3, 3], dur=2.0, seed=41,
+                danse=dict(BATTERY, nodeUpdating='asy', computeLocal=True, saveConditionNumber=True,
+                           saveConditionNumberEvery=3))
+    sc, dp, wp = _scene_params(case)
+    dv = danse_multi([sc], dp)[0]
+    ov = O.danse(sc, dp, vadMinProp=wp.vadMinProportionActive)
+    cn, co = dv.condNumbers, ov.condNumbers
+    errs = []
+    for fam in ('DANSE', 'Local'):
+        for k in range(4):
+            it_d, it_o = getattr(cn, f'iter_cn_Ryy{fam}')[k], getattr(co, f'iter_cn_Ryy{fam}')[k]
+            n = min(len(it_d), len(it_o))
+            assert n > 10 and list(it_d[:n]) == list(it_o[:n]), (fam, k)
+            a = getattr(cn, f'cn_Ryy{fam}')[k][:, :n]
+            b = getattr(co, f'cn_Ryy{fam}')[k][:, :n]
+            ok = np.isfinite(b) & (b < 1e6)
+            assert np.array_equal(np.isfinite(a[ok]), np.ones(int(ok.sum()), dtype=bool))
+            errs.append(np.abs(np.log10(a[ok]) - np.log10(b[ok])))
+    e = np.concatenate(errs)
+    print('cond log10 error median', np.median(e), 'p99', np.percentile(e, 99), 'max', e.max(), 'n', e.size)
+    assert np.median(e) <= 1e-5 and np.percentile(e, 99) <= 1e-3, (np.median(e), np.percentile(e, 99))
