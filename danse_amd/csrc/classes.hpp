@@ -35,6 +35,7 @@ constexpr bool class_packed(int D) { return D <= kLaneMaxD; }
 
 #define DANSE_DECLARE_CLASS(N)                                                                      \
   void launch_update_d##N(const UpdateArgs& a, hipStream_t st);                                     \
+  bool launch_split_solve_d##N(const UpdateArgs& a, int nItems, hipStream_t st);                    \
   void launch_filter_update_d##N(const cd* Ryy, const cd* Rnn, int B, int D, int gevd, int rank,   \
                                  int ref, cf* w, int* diag, hipStream_t st);
 DANSE_FOR_EACH_CLASS(DANSE_DECLARE_CLASS)
@@ -49,6 +50,19 @@ inline bool launch_update_class(int DMAX, const UpdateArgs& a, hipStream_t st) {
     default: return false;
   }
 }
+
+inline bool launch_split_solve_class(int DMAX, const UpdateArgs& a, int nItems, hipStream_t st) {
+  switch (DMAX) {
+#define DANSE_CASE(N) \
+  case N: return launch_split_solve_d##N(a, nItems, st);
+    DANSE_FOR_EACH_CLASS(DANSE_CASE)
+#undef DANSE_CASE
+    default: return false;
+  }
+}
+// the lane classes with a split-solve kernel (update_class.hip)
+constexpr bool class_split(int DMAX) { return DMAX >= 9 && DMAX <= kLaneMaxD; }
+constexpr long long class_split_li_record() { return 12LL * 13 / 2 + 16; }   // li_record<3, 4>
 
 inline bool launch_filter_update_class(int DMAX, const cd* Ryy, const cd* Rnn, int B, int D, int gevd, int rank,
                                        int ref, cf* w, int* diag, hipStream_t st) {

@@ -31,6 +31,11 @@ struct Class {
   std::vector<int> ids;
   FamNode* dev = nullptr;
   int* devIds = nullptr;
+  // split solves (lane classes D 9..12, UpdateArgs.splitSolve): per round the
+  // items that solve, [R][S * nFN] (the first solveCount[r] of a row used)
+  bool split = false;
+  int* dSolveItems = nullptr;
+  std::vector<int> solveCount;
 };
 
 template <typename T>
@@ -364,6 +369,26 @@ const char* danse_last_error(const danse_engine* eng) {
   return g_lastErr.c_str();
 }
 
+// The split classes' per-round lists of solving (scene, family-node) items.
+static int build_split_lists(danse_engine* eng, const uint8_t* flags) {
+  const int S = eng->S, K = eng->K, R = eng->R;
+  for (auto& cl : eng->classes) {
+    if (!cl.split) continue;
+    const int n = (int)cl.host.size();
+    std::vector<int> items((size_t)R * S * n, 0);
+    cl.solveCount.assign(R, 0);
+    for (int r = 0; r < R; ++r)
+      for (int t = 0; t < S * n; ++t) {
+        const FamNode& d = cl.host[t % n];
+        const uint8_t fl = flags[(((size_t)r * S + t / n) * kMaxFam + d.fam) * K + d.k];
+        if ((fl & DANSE_FLAG_SOLVE) && !(fl & DANSE_FLAG_PREGIVEN)) items[(size_t)r * S * n + cl.solveCount[r]++] = t;
+      }
+    if (!cl.dSolveItems) HIPCHK(dalloc(&cl.dSolveItems, items.size()));
+    HIPCHK(hipMemcpy(cl.dSolveItems, items.data(), items.size() * sizeof(int), hipMemcpyHostToDevice));
+  }
+  return 0;
+}
+
 int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
   danse_engine* eng = nullptr;
   if (!c || !out) return fail(nullptr, "null argument");
@@ -446,7 +471,10 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
       fn.wOff = wOff;
       wOff += histW * F * fn.D;
       fn.liOff = liOff;
-      if (c->gevd && fn.packed) liOff += (long long)F * (fn.D * (fn.D + 1) / 2 + fn.D);
+      // (a split class's grid solves keep their own per-bin record in the region)
+      if (c->gevd && fn.packed)
+        liOff += (long long)F * std::max<long long>(fn.D * (fn.D + 1) / 2 + fn.D,
+                                                    class_split(class_dmax(fn.D)) ? class_split_li_record() : 0);
       else if (c->gevd && gridSmall) liOff += (long long)F * class_li_record(16);
       else if (c->gevd && class_grid(class_dmax(fn.D)) > 0) liOff += (long long)F * class_li_record(class_dmax(fn.D));
       eng->fns.push_back(fn);
@@ -548,6 +576,14 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
     HIPCHK(dalloc(&cl.devIds, cl.ids.size()));
     HIPCHK(hipMemcpy(cl.dev, cl.host.data(), cl.host.size() * sizeof(FamNode), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(cl.devIds, cl.ids.data(), cl.ids.size() * sizeof(int), hipMemcpyHostToDevice));
+  }
+  {
+    // split solves: on by default for the GEVD of the lane classes D 9..12
+    // (DANSE_LANE_SPLIT=0 turns them off)
+    const char* sp = std::getenv("DANSE_LANE_SPLIT");
+    const bool on = c->gevd && !(sp && std::atoi(sp) == 0);
+    for (auto& cl : eng->classes) cl.split = on && cl.G == 1 && class_split(cl.DMAX);
+    if (int rc = build_split_lists(eng, c->flags)) return rc;
   }
   const size_t MT = (size_t)eng->MT;
   HIPCHK(dalloc(&eng->Yspec, 2 * S * MT * F));
@@ -731,6 +767,7 @@ void danse_engine_destroy(danse_engine* eng) {
   for (auto& cl : eng->classes) {
     if (cl.dev) (void)hipFree(cl.dev);
     if (cl.devIds) (void)hipFree(cl.devIds);
+    if (cl.dSolveItems) (void)hipFree(cl.dSolveItems);
   }
   delete eng;
 }
@@ -779,7 +816,12 @@ static void launch_update(danse_engine* e, int r, hipStream_t st) {
     a.nFN = (int)cl.host.size();
     a.fn = cl.dev;
     a.famNodeId = cl.devIds;
+    a.splitSolve = cl.split ? 1 : 0;
     launch_update_class(cl.DMAX, a, st);   // D > kMaxDMax rejected at create time
+    if (cl.split && cl.solveCount[r] > 0) {
+      a.solveItems = cl.dSolveItems + (size_t)r * e->S * cl.host.size();
+      launch_split_solve_class(cl.DMAX, a, cl.solveCount[r], st);
+    }
   }
   if (e->condEvery > 0 && (r + 1) % e->condEvery == 0) {
     // (saved when i - last >= every, last starting at -1: d_classes.py:2128-2130)
@@ -1247,7 +1289,11 @@ int danse_engine_set_flags(danse_engine* eng, const uint8_t* flags, void* stream
   const size_t nb = (size_t)eng->R * eng->S * kMaxFam * eng->K;
   HIPCHK(hipMemcpyAsync(eng->dFlags, flags, nb, hipMemcpyHostToDevice, (hipStream_t)stream));
   HIPCHK(hipStreamSynchronize((hipStream_t)stream));
-  return 0;
+  if (eng->graphExec) {   // the split solves' launch sizes follow the flags
+    (void)hipGraphExecDestroy(eng->graphExec);
+    eng->graphExec = nullptr;
+  }
+  return build_split_lists(eng, flags);
 }
 
 int danse_engine_zspec(danse_engine* eng, void** ptr, size_t* bytes) {

@@ -83,6 +83,11 @@ struct UpdateArgs {
   // zeros), read with agent-coherent loads (written inside the same launch)
   const cf* Yall;
   int zAll;
+  // lane classes, split solves (kernels_2d.hpp PK): the lane kernel skips the
+  // (scene, family-node) items that solve this round; the packed-storage
+  // lane-grid kernel runs them, one launch item per entry of solveItems
+  int splitSolve;
+  const int* solveItems;   // this round's solving items (s * nFN + fni)
 };
 
 // Agent-coherent (sc1) 8-byte load / store of a complex value: the resident

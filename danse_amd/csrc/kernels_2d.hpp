@@ -23,7 +23,12 @@ namespace danse {
 // G = 8: one bin per wave on the 8 x 8 lane grid; G = 4: four bins per wave
 // (bins f0 .. f0 + 3 of one scene / family-node), each on a 16-lane DPP row,
 // lane-layout vectors with vpl entries per lane (solver2d.hpp).
-template <int NB, int RMAX, int G = 8>
+// PK: the SCMs of a lane class (packed lower triangles, bin-minor,
+// kernels_lane.hpp) for the split solves (UpdateArgs.splitSolve): launch item
+// b / FG is solveItems[b / FG]; the upper entries of a lane's blocks are the
+// conjugates of the stored lower ones, only the lower ones are written back,
+// and the diagonals are kept real as the lane kernel keeps them.
+template <int NB, int RMAX, int G = 8, bool PK = false>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NB <= 5 ? DANSE_2D_WPE : 1)))
 update_kernel_2d(const UpdateArgs a) {
   using namespace t2d;
@@ -36,7 +41,7 @@ update_kernel_2d(const UpdateArgs a) {
   const int F = a.F;
   const int FG = (F + W - 1) / W;
   const int fg = blockIdx.x % FG;
-  const int tt = blockIdx.x / FG;
+  const int tt = PK ? a.solveItems[blockIdx.x / FG] : blockIdx.x / FG;
   const int f0 = fg * W + bw;
   const bool fvalid = (W == 1) || f0 < F;   // the last group's tail bins compute on bin F-1, store nothing
   const int f = (W == 1 || f0 < F) ? f0 : F - 1;
@@ -72,6 +77,17 @@ update_kernel_2d(const UpdateArgs a) {
   t2d::wsync();
   const double beta = a.beta[s * a.K + d.k];
   const long long matOff = (long long)s * a.scmStride + d.scmOff + (long long)f * D * D;
+  // entry (i, c) of the SCM (both in range): full rows, or the packed lower
+  // triangle of the lane classes ([D(D+1)/2][F], bin-minor)
+  auto ent = [&](int i, int c) -> long long {
+    if constexpr (PK) {
+      const int hi = i >= c ? i : c, lo = i >= c ? c : i;
+      return (long long)s * a.scmStride + d.scmOff + (long long)(hi * (hi + 1) / 2 + lo) * F + f;
+    } else {
+      return matOff + (long long)i * D + c;
+    }
+  };
+  const long long safe = PK ? ent(0, 0) : matOff;   // (an in-bounds address for the padding entries)
 
   // ---- Rnn (float64): recursion, store, factor -> Li in S.Ls -------------
   bool ok = true;
@@ -85,14 +101,18 @@ update_kernel_2d(const UpdateArgs a) {
         constexpr int tb = decltype(tc)::value;
         const int i = p + G * sb, c = q + G * tb;
         const bool in = i < D && c < D;
-        cd x = csel(in, a.Rnn[matOff + (in ? (long long)i * D + c : 0ll)], cd{0.0, 0.0});
+        cd x = csel(in, a.Rnn[in ? ent(i, c) : safe], cd{0.0, 0.0});
+        if constexpr (PK) {
+          if (i < c) x = conjg(x);
+          if (i == c) x.im = 0.0;
+        }
         if (opN) {
           cd yy = cd{0.0, 0.0};
           fma_cc(yy, cdk(yr[sb]), cdk(yc[tb]));
           x = cx * x;
           x.re = fma(cy, yy.re, x.re);
-          x.im = fma(cy, yy.im, x.im);
-          if (in && fvalid) a.Rnn[matOff + (long long)i * D + c] = x;
+          x.im = (PK && i == c) ? 0.0 : fma(cy, yy.im, x.im);
+          if (in && fvalid && (!PK || i >= c)) a.Rnn[ent(i, c)] = x;
         }
         M.v[sb][tb] = x;
       });
@@ -116,11 +136,15 @@ update_kernel_2d(const UpdateArgs a) {
         constexpr int tb = decltype(tc)::value;
         const int i = p + G * sb, c = q + G * tb;
         const bool in = i < D && c < D;
-        cf x = csel(in, a.Ryy[matOff + (in ? (long long)i * D + c : 0ll)], cf{0.0f, 0.0f});
+        cf x = csel(in, a.Ryy[in ? ent(i, c) : safe], cf{0.0f, 0.0f});
+        if constexpr (PK) {
+          if (i < c) x = conjg(x);
+        }
         if (opY) {
           const cf yy = cy * mulc(yr[sb], yc[tb]);
           x = csel(opY == DANSE_OP_SET, yy, by * x + yy);
-          if (in && fvalid) a.Ryy[matOff + (long long)i * D + c] = x;
+          if (PK && i == c) x.im = 0.0f;
+          if (in && fvalid && (!PK || i >= c)) a.Ryy[ent(i, c)] = x;
         }
         A.v[sb][tb] = x;
       });

@@ -51,6 +51,7 @@ __global__ void __launch_bounds__(64) update_kernel_lane(const UpdateArgs a) {
   const uint8_t fl = a.flags[(((long long)r * a.S + s) * kMaxFam + d.fam) * a.K + d.k];
   const int opY = fl & 3, opN = (fl >> 2) & 3;
   const bool solve = (fl & DANSE_FLAG_SOLVE) != 0 && (fl & DANSE_FLAG_PREGIVEN) == 0;
+  if (a.splitSolve && solve) return;   // this item's round runs on update_kernel_2d<.., PK = true>
   // GEVD: reuse the cached float32 Li / g when Rnn has not changed since the
   // last factorisation (skips the float64 load, Cholesky and inverse)
   const bool reuse = GEVD && solve && li_reusable(a, d, s, opN);

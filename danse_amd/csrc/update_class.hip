@@ -52,6 +52,23 @@ void DANSE_CAT(launch_update_d, DANSE_DMAX)(const UpdateArgs& a, hipStream_t st)
   }
 }
 
+// Split solves of a lane class (UpdateArgs.splitSolve): the GEVD rounds of the
+// nItems solving items on 4 x 4 lane grids (four bins per wave, NB = 3:
+// D 9..12) over the lane class's packed SCMs.  Returns false if the class
+// has no split kernel.
+bool DANSE_CAT(launch_split_solve_d, DANSE_DMAX)(const UpdateArgs& a, int nItems, hipStream_t st) {
+  if constexpr (kG == 1 && kD >= 9) {
+    const unsigned g2 = (unsigned)(nItems * ((a.F + 3) / 4));
+    if (!a.gevd) return false;
+    if (a.rank == 1) hipLaunchKernelGGL((update_kernel_2d<3, 1, 4, true>), dim3(g2), dim3(64), 0, st, a);
+    else hipLaunchKernelGGL((update_kernel_2d<3, kRMax, 4, true>), dim3(g2), dim3(64), 0, st, a);
+    return true;
+  } else {
+    (void)a; (void)nItems; (void)st;
+    return false;
+  }
+}
+
 void DANSE_CAT(launch_filter_update_d, DANSE_DMAX)(const cd* Ryy, const cd* Rnn, int B, int D, int gevd, int rank,
                                                    int ref, cf* w, int* diag, hipStream_t st) {
   const bool r1 = !gevd || rank == 1;
