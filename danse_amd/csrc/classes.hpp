@@ -60,8 +60,9 @@ inline bool launch_split_solve_class(int DMAX, const UpdateArgs& a, int nItems, 
     default: return false;
   }
 }
-// the lane classes with a split-solve kernel (update_class.hip)
-constexpr bool class_split(int DMAX) { return DMAX >= 9 && DMAX <= kLaneMaxD; }
+// the classes with split solves (update_class.hip): the GEVD of the lane
+// classes D 9..12 and of the lane-grid classes
+constexpr bool class_split(int DMAX) { return (DMAX >= 9 && DMAX <= kLaneMaxD) || class_grid(DMAX) > 0; }
 constexpr long long class_split_li_record() { return 12LL * 13 / 2 + 16; }   // li_record<3, 4>
 
 inline bool launch_filter_update_class(int DMAX, const cd* Ryy, const cd* Rnn, int B, int D, int gevd, int rank,

@@ -582,7 +582,7 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
     // (DANSE_LANE_SPLIT=0 turns them off)
     const char* sp = std::getenv("DANSE_LANE_SPLIT");
     const bool on = c->gevd && !(sp && std::atoi(sp) == 0);
-    for (auto& cl : eng->classes) cl.split = on && cl.G == 1 && class_split(cl.DMAX);
+    for (auto& cl : eng->classes) cl.split = on && class_split(cl.DMAX) && (cl.G == 1 || cl.DMAX > kLaneMaxD);
     if (int rc = build_split_lists(eng, c->flags)) return rc;
   }
   const size_t MT = (size_t)eng->MT;

@@ -23,25 +23,34 @@ namespace danse {
 // G = 8: one bin per wave on the 8 x 8 lane grid; G = 4: four bins per wave
 // (bins f0 .. f0 + 3 of one scene / family-node), each on a 16-lane DPP row,
 // lane-layout vectors with vpl entries per lane (solver2d.hpp).
-// PK: the SCMs of a lane class (packed lower triangles, bin-minor,
-// kernels_lane.hpp) for the split solves (UpdateArgs.splitSolve): launch item
-// b / FG is solveItems[b / FG]; the upper entries of a lane's blocks are the
+// Split solves (UpdateArgs.splitSolve; in asy updating one node of K solves
+// per round, the others only run the recursion):
+//   SM = 1  recursion-only launch over every item: the items that solve this
+//           round return at once, the solver is compiled out, so the launch
+//           is not held to the solver's register budget;
+//   SM = 2  the solving items only, launch item b / FG = solveItems[b / FG].
+// PK (with SM = 2): the SCMs of a lane class (packed lower triangles,
+// bin-minor, kernels_lane.hpp): the upper entries of a lane's blocks are the
 // conjugates of the stored lower ones, only the lower ones are written back,
 // and the diagonals are kept real as the lane kernel keeps them.
-template <int NB, int RMAX, int G = 8, bool PK = false>
+template <int NB, int RMAX, int G = 8, bool PK = false, int SM = 0>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NB <= 5 ? DANSE_2D_WPE : 1)))
 update_kernel_2d(const UpdateArgs a) {
   using namespace t2d;
   constexpr int L = bin_lanes<G>(), W = 64 / L, V = vpl<NB, G>();
-  __shared__ LDS2<NB, G> Sall[W];
+  // (the recursion-only launch needs only the y staging vector: its LDS
+  // stays small so that the launch is not held to the solver's LDS budget)
+  constexpr int kLds = (SM == 1) ? (int)sizeof(cf) * W * L * V : (int)sizeof(LDS2<NB, G>) * W;
+  __shared__ __attribute__((aligned(16))) char ldsRaw[kLds];
   const int bw = threadIdx.x / L;
   const int li = threadIdx.x % L;
-  LDS2<NB, G>& S = Sall[bw];
+  LDS2<NB, G>& S = reinterpret_cast<LDS2<NB, G>*>(ldsRaw)[bw];   // (not touched when SM == 1)
+  cf* const vb = (SM == 1) ? reinterpret_cast<cf*>(ldsRaw) + bw * L * V : S.vb;
   const int p = li / G, q = li % G;
   const int F = a.F;
   const int FG = (F + W - 1) / W;
   const int fg = blockIdx.x % FG;
-  const int tt = PK ? a.solveItems[blockIdx.x / FG] : blockIdx.x / FG;
+  const int tt = (SM == 2) ? a.solveItems[blockIdx.x / FG] : blockIdx.x / FG;
   const int f0 = fg * W + bw;
   const bool fvalid = (W == 1) || f0 < F;   // the last group's tail bins compute on bin F-1, store nothing
   const int f = (W == 1 || f0 < F) ? f0 : F - 1;
@@ -53,7 +62,11 @@ update_kernel_2d(const UpdateArgs a) {
   const uint8_t fl = a.flags[(((long long)r * a.S + s) * kMaxFam + d.fam) * a.K + d.k];
   const int opY = fl & 3, opN = (fl >> 2) & 3;
   const bool pregiven = (fl & DANSE_FLAG_PREGIVEN) != 0;
-  const bool solve = (fl & DANSE_FLAG_SOLVE) != 0 && !pregiven;
+  bool solve = (fl & DANSE_FLAG_SOLVE) != 0 && !pregiven;
+  if constexpr (SM == 1) {
+    if (solve) return;   // wave-uniform: the SM = 2 launch runs this item
+    solve = false;
+  }
   const bool initslot = (fl & DANSE_FLAG_INITSLOT) != 0;
   // factor cache (kernels.hpp li_reusable): per bin S.Ls (packed Li, float32)
   // and g (solver2d.hpp li_record / li_store2d)
@@ -65,14 +78,14 @@ update_kernel_2d(const UpdateArgs a) {
     constexpr int v = decltype(vc)::value;
     const int i = li + L * v;
     y[v] = load_y(a, d, s, f, i, i < D);
-    S.vb[i] = y[v];
+    vb[i] = y[v];
   });
   t2d::wsync();
   cf yr[NB], yc[NB];
   sfor<0, NB>([&](auto sc) {
     constexpr int sb = decltype(sc)::value;
-    yr[sb] = S.vb[p + G * sb];
-    yc[sb] = S.vb[q + G * sb];
+    yr[sb] = vb[p + G * sb];
+    yc[sb] = vb[q + G * sb];
   });
   t2d::wsync();
   const double beta = a.beta[s * a.K + d.k];

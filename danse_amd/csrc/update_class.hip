@@ -43,8 +43,14 @@ void DANSE_CAT(launch_update_d, DANSE_DMAX)(const UpdateArgs& a, hipStream_t st)
       hipLaunchKernelGGL((update_kernel_big<kDBig, 1, false>), dim3(grid), dim3(64), 0, st, a);
     } else if constexpr (k2D) {
       const unsigned g2 = (unsigned)(a.S * a.nFN * ((a.F + kBinsPerWave - 1) / kBinsPerWave));
-      if (r1) hipLaunchKernelGGL((update_kernel_2d<kNB, 1, kGrid>), dim3(g2), dim3(64), 0, st, a);
-      else hipLaunchKernelGGL((update_kernel_2d<kNB, kRMax, kGrid>), dim3(g2), dim3(64), 0, st, a);
+      if (a.splitSolve) {   // the recursion-only launch of the split solves
+        if (r1) hipLaunchKernelGGL((update_kernel_2d<kNB, 1, kGrid, false, 1>), dim3(g2), dim3(64), 0, st, a);
+        else hipLaunchKernelGGL((update_kernel_2d<kNB, kRMax, kGrid, false, 1>), dim3(g2), dim3(64), 0, st, a);
+      } else if (r1) {
+        hipLaunchKernelGGL((update_kernel_2d<kNB, 1, kGrid>), dim3(g2), dim3(64), 0, st, a);
+      } else {
+        hipLaunchKernelGGL((update_kernel_2d<kNB, kRMax, kGrid>), dim3(g2), dim3(64), 0, st, a);
+      }
     } else {
       if (r1) hipLaunchKernelGGL((update_kernel_big<kDBig, 1, true>), dim3(grid), dim3(64), 0, st, a);
       else hipLaunchKernelGGL((update_kernel_big<kDBig, kRMax, true>), dim3(grid), dim3(64), 0, st, a);
@@ -57,11 +63,17 @@ void DANSE_CAT(launch_update_d, DANSE_DMAX)(const UpdateArgs& a, hipStream_t st)
 // D 9..12) over the lane class's packed SCMs.  Returns false if the class
 // has no split kernel.
 bool DANSE_CAT(launch_split_solve_d, DANSE_DMAX)(const UpdateArgs& a, int nItems, hipStream_t st) {
+  if (!a.gevd) return false;
   if constexpr (kG == 1 && kD >= 9) {
     const unsigned g2 = (unsigned)(nItems * ((a.F + 3) / 4));
-    if (!a.gevd) return false;
-    if (a.rank == 1) hipLaunchKernelGGL((update_kernel_2d<3, 1, 4, true>), dim3(g2), dim3(64), 0, st, a);
-    else hipLaunchKernelGGL((update_kernel_2d<3, kRMax, 4, true>), dim3(g2), dim3(64), 0, st, a);
+    if (a.rank == 1) hipLaunchKernelGGL((update_kernel_2d<3, 1, 4, true, 2>), dim3(g2), dim3(64), 0, st, a);
+    else hipLaunchKernelGGL((update_kernel_2d<3, kRMax, 4, true, 2>), dim3(g2), dim3(64), 0, st, a);
+    return true;
+  } else if constexpr (k2D) {
+    // the solving items of a lane-grid class (full storage)
+    const unsigned g2 = (unsigned)(nItems * ((a.F + kBinsPerWave - 1) / kBinsPerWave));
+    if (a.rank == 1) hipLaunchKernelGGL((update_kernel_2d<kNB, 1, kGrid, false, 2>), dim3(g2), dim3(64), 0, st, a);
+    else hipLaunchKernelGGL((update_kernel_2d<kNB, kRMax, kGrid, false, 2>), dim3(g2), dim3(64), 0, st, a);
     return true;
   } else {
     (void)a; (void)nItems; (void)st;
