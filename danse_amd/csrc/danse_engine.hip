@@ -578,10 +578,10 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
     HIPCHK(hipMemcpy(cl.devIds, cl.ids.data(), cl.ids.size() * sizeof(int), hipMemcpyHostToDevice));
   }
   {
-    // split solves: on by default for the GEVD of the lane classes D 9..12
-    // (DANSE_LANE_SPLIT=0 turns them off)
+    // split solves for the GEVD of the lane classes D 9..12 and the lane-grid
+    // classes (DANSE_LANE_SPLIT=1 turns them on)
     const char* sp = std::getenv("DANSE_LANE_SPLIT");
-    const bool on = c->gevd && !(sp && std::atoi(sp) == 0);
+    const bool on = c->gevd && (sp && std::atoi(sp) != 0);
     for (auto& cl : eng->classes) cl.split = on && class_split(cl.DMAX) && (cl.G == 1 || cl.DMAX > kLaneMaxD);
     if (int rc = build_split_lists(eng, c->flags)) return rc;
   }
