@@ -828,6 +828,7 @@ static void launch_update(danse_engine* e, int r, hipStream_t st) {
     int dm = 1;
     for (const auto& fn : e->fns) dm = std::max(dm, fn.D);
     const size_t lds = (size_t)dm * (dm + 1) * sizeof(cd);
+    if (lds > 65536) (void)hipFuncSetAttribute((const void*)cond_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(cond_kernel, dim3(e->F, e->S * (int)e->fns.size()), dim3(64), lds, st, make_update(e, r),
                        e->dFnAll, (int)e->fns.size(), e->condHist);
   }
