@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 TAG=${TAG:-r3s}
 DANSE_LANE_SPLIT=1 timeout -k 10 400 python -u -m pytest tests/test_gpu_engine_modes.py tests/test_gpu_parity.py -m gpu -q -s -x -k "config_B_shape or condition or sandbox or keep_history or sharded or gate or headline or config_C or large_D or init_random" --timeout 250 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_split_$TAG.log 2>&1
 rc=$?
-grep -E "passed|failed|online_B_shape|cond log10|^FAILED" gpurun_out/pytest_split_$TAG.log | tail -8
+grep -E "passed|failed|online_B_shape|cond error|^FAILED" gpurun_out/pytest_split_$TAG.log | tail -8
 [ $rc -eq 0 ] || exit $rc
 DANSE_LANE_SPLIT=1 timeout -k 10 200 python bench.py --workload B --no-cpu-baseline --no-traffic --no-extra > gpurun_out/bench_split_$TAG.log 2>&1 || exit 1
 DANSE_LANE_SPLIT=0 timeout -k 10 200 python bench.py --workload B --no-cpu-baseline --no-traffic --no-extra > gpurun_out/bench_nosplit_$TAG.log 2>&1 || exit 1

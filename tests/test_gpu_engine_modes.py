@@ -335,10 +335,13 @@ def test_cohdrift_sro_estimates_vs_oracle():
 def test_condition_numbers_vs_oracle():
     """saveConditionNumber (ConditionNumbers, d_classes.py:19-130,2126-2186):
     np.linalg.cond of every bin's Ryy after every saveConditionNumberEvery-th
-    update, DANSE and local families, against the oracle's float64 SCMs.  The
-    device SCMs are float32 (Ryy), so the comparison is in
-    log10 and only where the oracle's matrix is not numerically singular
-    (cond < 1e6; the first-frame basis is rank one)."""
+    update, DANSE and local families, against the oracle's float64 SCMs, on
+    the same iterations.  The device's Ryy is float32, and a
+    perturbation of relative size e moves cond by about e * cond, so the
+    tolerance scales with cond: |cond_dev - cond_ref| / cond_ref <= 3e-6 cond
+    + 1e-5 (float32 rounding accumulated over the recursion), checked where
+    the oracle's matrix is not numerically singular (cond < 1e6; the
+    first-frame basis is rank one)."""
     from danse_amd.core import danse_multi
     from oracle import danse_ref_cpu as O
     case = dict(name='cond_k4m3', M=[3, 3, 3, 3], dur=2.0, seed=41,
@@ -348,7 +351,7 @@ def test_condition_numbers_vs_oracle():
     dv = danse_multi([sc], dp)[0]
     ov = O.danse(sc, dp, vadMinProp=wp.vadMinProportionActive)
     cn, co = dv.condNumbers, ov.condNumbers
-    errs = []
+    ratio = []
     for fam in ('DANSE', 'Local'):
         for k in range(4):
             it_d, it_o = getattr(cn, f'iter_cn_Ryy{fam}')[k], getattr(co, f'iter_cn_Ryy{fam}')[k]
@@ -357,8 +360,9 @@ def test_condition_numbers_vs_oracle():
             a = getattr(cn, f'cn_Ryy{fam}')[k][:, :n]
             b = getattr(co, f'cn_Ryy{fam}')[k][:, :n]
             ok = np.isfinite(b) & (b < 1e6)
-            assert np.array_equal(np.isfinite(a[ok]), np.ones(int(ok.sum()), dtype=bool))
-            errs.append(np.abs(np.log10(a[ok]) - np.log10(b[ok])))
-    e = np.concatenate(errs)
-    print('cond log10 error median', np.median(e), 'p99', np.percentile(e, 99), 'max', e.max(), 'n', e.size)
-    assert np.median(e) <= 1e-5 and np.percentile(e, 99) <= 1e-3, (np.median(e), np.percentile(e, 99))
+            assert np.all(np.isfinite(a[ok])), (fam, k)
+            rel = np.abs(a[ok] - b[ok]) / b[ok]
+            ratio.append(rel / (3e-6 * b[ok] + 1e-5))
+    r = np.concatenate(ratio)
+    print('cond error / tolerance: median', np.median(r), 'p99', np.percentile(r, 99), 'max', r.max(), 'n', r.size)
+    assert np.percentile(r, 99) <= 1.0 and np.median(r) <= 0.1, (np.median(r), np.percentile(r, 99))
