@@ -371,8 +371,7 @@ def run_online(args, wl, S, rank, world, local, dist, traffic=True, pmc_child=Fa
         if runner is not None:
             runner.run(reset=True)
         else:
-            L.check(eng.lib.danse_engine_reset(eng.eng, eng.stream_ptr()), eng.eng)
-            eng.run(graph=not args.no_graph)
+            eng.run(graph=not args.no_graph)     # (every run starts with the state reset)
 
     if pmc_child:
         # one un-graphed pass for the PMC collector (every kernel its own dispatch)

@@ -11,6 +11,7 @@
 
 #include "../../include/danse_mi355x.h"
 #include "bcast.hpp"
+#include "fill.hpp"
 #include "classes.hpp"
 #include "gate.hpp"
 #include "cohdrift.hpp"
@@ -111,6 +112,11 @@ struct danse_engine {
   danse_dxcp* dx = nullptr;
   float* dxFrames = nullptr;     // [P][2][2048]
   double *dxOut = nullptr, *dxEst = nullptr;   // [P][2], [S][K][K] current estimate (relative SRO)
+  // record of every feed's gathered frames and estimator outputs
+  // (danse_engine_dxcp_record): [nFeeds][P][2][2048] f32, [nFeeds][P][2] f64
+  float* dxRecFrames = nullptr;
+  double* dxRecOut = nullptr;
+  int dxRecFeeds = 0;
   // centralised / SSBC raw frames under asynchronous clocks (cfg.cEnd)
   int* dCEnd = nullptr;
   cf* Cspec = nullptr;
@@ -330,27 +336,27 @@ int danse_engine_reset(danse_engine* eng, void* stream) {
   HIPCHK(hipSetDevice(eng->dev));
   hipStream_t st = (hipStream_t)stream;
   const int S = eng->S, K = eng->K, F = eng->F, R = eng->R;
-  HIPCHK(hipMemsetAsync(eng->zPrev, 0, (size_t)S * K * eng->N * sizeof(float), st));
+  HIPCHK(fill_async(eng->zPrev, 0, (size_t)S * K * eng->N * sizeof(float), st));
   if (eng->dxcpOn) {
-    HIPCHK(hipMemsetAsync(eng->dxEst, 0, (size_t)S * K * K * sizeof(double), st));
+    HIPCHK(fill_async(eng->dxEst, 0, (size_t)S * K * K * sizeof(double), st));
     if (danse_dxcp_reset(eng->dx, st) != 0) return fail(eng, std::string("DXCP estimator: ") + danse_dxcp_last_error(eng->dx));
   }
   if (eng->cohDrift || eng->dxcpOn) {
-    HIPCHK(hipMemsetAsync(eng->cdPhase, 0, (size_t)S * K * K * sizeof(double), st));
-    HIPCHK(hipMemsetAsync(eng->cdEst, 0, (size_t)S * K * (K - 1) * R * sizeof(double), st));
-    HIPCHK(hipMemsetAsync(eng->cdRes, 0, (size_t)S * K * (K - 1) * R * sizeof(double), st));
+    HIPCHK(fill_async(eng->cdPhase, 0, (size_t)S * K * K * sizeof(double), st));
+    HIPCHK(fill_async(eng->cdEst, 0, (size_t)S * K * (K - 1) * R * sizeof(double), st));
+    HIPCHK(fill_async(eng->cdRes, 0, (size_t)S * K * (K - 1) * R * sizeof(double), st));
   }
-  HIPCHK(hipMemsetAsync(eng->Zspec, 0, (size_t)2 * K * S * F * sizeof(cf), st));
-  if (eng->Cspec) HIPCHK(hipMemsetAsync(eng->Cspec, 0, (size_t)2 * S * eng->MT * F * sizeof(cf), st));
-  HIPCHK(hipMemsetAsync(eng->zStream, 0, (size_t)S * K * eng->zLen * sizeof(float), st));
+  HIPCHK(fill_async(eng->Zspec, 0, (size_t)2 * K * S * F * sizeof(cf), st));
+  if (eng->Cspec) HIPCHK(fill_async(eng->Cspec, 0, (size_t)2 * S * eng->MT * F * sizeof(cf), st));
+  HIPCHK(fill_async(eng->zStream, 0, (size_t)S * K * eng->zLen * sizeof(float), st));
   if (eng->wIR) {
-    HIPCHK(hipMemsetAsync(eng->wIR, 0, (size_t)S * K * eng->Mmax * tzc::kA * sizeof(float), st));
+    HIPCHK(fill_async(eng->wIR, 0, (size_t)S * K * eng->Mmax * tzc::kA * sizeof(float), st));
     hipLaunchKernelGGL(fs_ir_init_kernel, dim3(S * K), dim3(64), 0, st, eng->wIR, K, eng->Mmax, eng->ref, eng->N);
     HIPCHK(hipGetLastError());
   }
-  HIPCHK(hipMemsetAsync(eng->dhat, 0, (size_t)kMaxFam * S * K * R * F * sizeof(cf), st));
-  HIPCHK(hipMemsetAsync(eng->d, 0, (size_t)kMaxFam * S * K * eng->T * sizeof(float), st));
-  HIPCHK(hipMemsetAsync(eng->diag, 0, (size_t)S * K * kMaxFam * sizeof(int), st));
+  HIPCHK(fill_async(eng->dhat, 0, (size_t)kMaxFam * S * K * R * F * sizeof(cf), st));
+  HIPCHK(fill_async(eng->d, 0, (size_t)kMaxFam * S * K * eng->T * sizeof(float), st));
+  HIPCHK(fill_async(eng->diag, 0, (size_t)S * K * kMaxFam * sizeof(int), st));
   const int nFN = (int)eng->fns.size();
   hipLaunchKernelGGL(reset_fam_kernel, dim3(64, S * nFN), dim3(256), 0, st, eng->dFnAll, nFN, eng->dInitW0Off,
                      eng->dInitScmOff, eng->dW0, eng->dScm0, eng->wHist, eng->wStride, eng->Ryy, eng->Rnn,
@@ -760,7 +766,8 @@ void danse_engine_destroy(danse_engine* eng) {
                   eng->cdRes, eng->dCEnd, eng->Cspec, eng->dChanNode, eng->dCPhase, eng->dxFrames, eng->dxOut,
                   eng->dxEst, eng->resYB, eng->resYU, eng->resZall, eng->resZhat, eng->resRyyG, eng->resRnnG,
                   eng->resUFlag, eng->resZFlag, eng->resGateRound, eng->resDanseFni, eng->resErr, eng->resFams,
-                  eng->resFrames, eng->resChanNode, eng->resTrace, eng->condHist};
+                  eng->resFrames, eng->resChanNode, eng->resTrace, eng->condHist, eng->dxRecFrames,
+                  eng->dxRecOut};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (eng->dx) danse_dxcp_destroy(eng->dx);
@@ -850,6 +857,13 @@ static void launch_update(danse_engine* e, int r, hipStream_t st) {
       hipLaunchKernelGGL(dxcp_gather_kernel, dim3(P), dim3(256), 0, st, make_update(e, r), e->dUpEnd, e->y, e->zStream,
                          e->zLen, e->T, e->Ns, e->dBase, e->ref, e->k0, nOwn, e->dxFrames);
       (void)danse_dxcp_process(e->dx, e->dxFrames, e->dxOut, st);
+      const int feed = (r + 1) / every - 1;
+      if (e->dxRecFrames && feed < e->dxRecFeeds) {
+        (void)hipMemcpyAsync(e->dxRecFrames + (size_t)feed * P * 2 * kDxFrame, e->dxFrames,
+                             (size_t)P * 2 * kDxFrame * sizeof(float), hipMemcpyDeviceToDevice, st);
+        (void)hipMemcpyAsync(e->dxRecOut + (size_t)feed * P * 2, e->dxOut, (size_t)P * 2 * sizeof(double),
+                             hipMemcpyDeviceToDevice, st);
+      }
     }
     hipLaunchKernelGGL(dxcp_round_kernel, dim3((P + 63) / 64), dim3(64), 0, st, e->S, e->K, e->k0, nOwn, r, e->R, fed,
                        e->cdComp, (double)e->Ns, e->dxOut, e->dxEst, e->cdPhase, e->cdEst, e->cdRes);
@@ -900,7 +914,7 @@ int danse_engine_gate_launch(danse_engine* eng, int32_t r, void* stream) {
   if (r < 0 || r >= eng->R) return fail(eng, "round out of range");
   HIPCHK(hipSetDevice(eng->dev));
   hipStream_t st = (hipStream_t)stream;
-  if (eng->nGate > 0 && r == 0) HIPCHK(hipMemsetAsync(eng->dGateVerdict, 0xff, eng->nGate * sizeof(int), st));
+  if (eng->nGate > 0 && r == 0) HIPCHK(fill_async(eng->dGateVerdict, 0xff, eng->nGate * sizeof(int), st));
   launch_gate_round(eng, r, st);
   HIPCHK(hipGetLastError());
   return 0;
@@ -938,7 +952,7 @@ int danse_engine_run(danse_engine* eng, int32_t r0, int32_t r1, void* stream, in
   HIPCHK(hipSetDevice(eng->dev));
   hipStream_t st = (hipStream_t)stream;
   auto seq = [&](hipStream_t s) {
-    if (eng->nGate > 0 && r0 == 0) (void)hipMemsetAsync(eng->dGateVerdict, 0xff, eng->nGate * sizeof(int), s);
+    if (eng->nGate > 0 && r0 == 0) (void)fill_async(eng->dGateVerdict, 0xff, eng->nGate * sizeof(int), s);
     for (int r = r0; r < r1; ++r) {
       launch_bcast(eng, r, r > 0, 1, s);
       launch_gate_round(eng, r, s);
@@ -1069,7 +1083,7 @@ int danse_engine_run_resident(danse_engine* eng, void* stream) {
       HIPCHK(hipMalloc((void**)&eng->resTrace, nb));
       eng->resTraceBytes = nb;
     }
-    HIPCHK(hipMemsetAsync(eng->resTrace, 0, nb, st));
+    HIPCHK(fill_async(eng->resTrace, 0, nb, st));
     ra.trace = eng->resTrace;
   }
   int fits = 0;
@@ -1082,10 +1096,11 @@ int danse_engine_run_resident(danse_engine* eng, void* stream) {
   std::vector<int> gr((size_t)S * nFN, -1);
   for (auto& x : eng->gateHost) gr[(size_t)x.second.s * nFN + x.second.fni] = x.first;
   HIPCHK(hipMemcpyAsync(eng->resGateRound, gr.data(), gr.size() * sizeof(int), hipMemcpyHostToDevice, st));
-  HIPCHK(hipMemsetAsync(eng->resUFlag, 0, (size_t)S * nFN * FG * sizeof(unsigned), st));
-  HIPCHK(hipMemsetAsync(eng->resZFlag, 0, (size_t)S * K * sizeof(unsigned), st));
-  HIPCHK(hipMemsetAsync(eng->resZall, 0, (size_t)K * S * F * sizeof(cf), st));   // slot 0: before round 0
-  if (eng->nGate > 0) HIPCHK(hipMemsetAsync(eng->dGateVerdict, 0xff, eng->nGate * sizeof(int), st));
+  HIPCHK(fill_async(eng->resUFlag, 0, (size_t)S * nFN * FG * sizeof(unsigned), st));
+  HIPCHK(fill_async(eng->resZFlag, 0, (size_t)S * K * sizeof(unsigned), st));
+  HIPCHK(fill_async(eng->resErr, 0, sizeof(int), st));   // per run: a previous run's give-up does not stick
+  HIPCHK(fill_async(eng->resZall, 0, (size_t)K * S * F * sizeof(cf), st));   // slot 0: before round 0
+  if (eng->nGate > 0) HIPCHK(fill_async(eng->dGateVerdict, 0xff, eng->nGate * sizeof(int), st));
   // WOLA analyses of every round (inputs only)
   {
     BcastArgs b = make_bcast(eng, 0, 0, 1);
@@ -1164,6 +1179,68 @@ int danse_engine_resident_error(danse_engine* eng, int32_t* err, void* stream) {
   HIPCHK(hipSetDevice(eng->dev));
   HIPCHK(hipMemcpyAsync(err, eng->resErr, sizeof(int), hipMemcpyDeviceToHost, (hipStream_t)stream));
   HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  return 0;
+}
+
+int danse_engine_resident_set_error(danse_engine* eng, int32_t value) {
+  if (!eng) return fail(eng, "null engine");
+  if (!eng->resErr) return fail(eng, "no resident run prepared");
+  HIPCHK(hipSetDevice(eng->dev));
+  HIPCHK(hipMemcpy(eng->resErr, &value, sizeof(int), hipMemcpyHostToDevice));
+  return 0;
+}
+
+int danse_engine_dxcp_record(danse_engine* eng, int32_t on) {
+  if (!eng) return fail(eng, "null engine");
+  if (!eng->dxcpOn) return fail(eng, "DXCP-PhaT estimation is not on");
+  HIPCHK(hipSetDevice(eng->dev));
+  if (eng->graphExec) {   // the captured run changes
+    (void)hipGraphExecDestroy(eng->graphExec);
+    eng->graphExec = nullptr;
+  }
+  if (eng->dxRecFrames) (void)hipFree(eng->dxRecFrames);
+  if (eng->dxRecOut) (void)hipFree(eng->dxRecOut);
+  eng->dxRecFrames = nullptr;
+  eng->dxRecOut = nullptr;
+  eng->dxRecFeeds = 0;
+  if (!on) return 0;
+  const size_t P = (size_t)eng->S * (eng->k1 - eng->k0) * (eng->K - 1);
+  const int feeds = eng->R / (kDxFrame / eng->Ns);
+  if (feeds < 1) return 0;
+  HIPCHK(dalloc(&eng->dxRecFrames, (size_t)feeds * P * 2 * kDxFrame));
+  HIPCHK(dalloc(&eng->dxRecOut, (size_t)feeds * P * 2));
+  HIPCHK(hipMemset(eng->dxRecFrames, 0, (size_t)feeds * P * 2 * kDxFrame * sizeof(float)));
+  HIPCHK(hipMemset(eng->dxRecOut, 0, (size_t)feeds * P * 2 * sizeof(double)));
+  eng->dxRecFeeds = feeds;
+  return 0;
+}
+
+int danse_engine_dxcp_recorded(danse_engine* eng, int32_t* nFeeds, int32_t* nPairs, float* frames, size_t frameBytes,
+                               double* out, size_t outBytes) {
+  if (!eng || !nFeeds || !nPairs) return fail(eng, "null argument");
+  const size_t P = (size_t)eng->S * (eng->k1 - eng->k0) * (eng->K - 1);
+  *nFeeds = eng->dxRecFeeds;
+  *nPairs = (int32_t)P;
+  if (!eng->dxRecFrames) return 0;
+  HIPCHK(hipSetDevice(eng->dev));
+  HIPCHK(hipDeviceSynchronize());
+  const size_t fb = (size_t)eng->dxRecFeeds * P * 2 * kDxFrame * sizeof(float);
+  const size_t ob = (size_t)eng->dxRecFeeds * P * 2 * sizeof(double);
+  if (frames) {
+    if (frameBytes < fb) return fail(eng, "frame buffer too small");
+    HIPCHK(hipMemcpy(frames, eng->dxRecFrames, fb, hipMemcpyDeviceToHost));
+  }
+  if (out) {
+    if (outBytes < ob) return fail(eng, "output buffer too small");
+    HIPCHK(hipMemcpy(out, eng->dxRecOut, ob, hipMemcpyDeviceToHost));
+  }
+  return 0;
+}
+
+int danse_mi355x_fill(void* ptr, int32_t value, size_t bytes, void* stream) {
+  danse_engine* eng = nullptr;   // (HIPCHK's error slot)
+  if (!ptr && bytes) return fail(eng, "null pointer");
+  HIPCHK(fill_async(ptr, value, bytes, (hipStream_t)stream));
   return 0;
 }
 

@@ -21,6 +21,7 @@
 
 #include "../../include/danse_mi355x.h"
 #include "wfft.hpp"
+#include "fill.hpp"
 
 using namespace danse;
 
@@ -571,18 +572,18 @@ int danse_dxcp_reset(danse_dxcp* eng, void* stream) {
   DCHK(hipSetDevice(eng->dev));
   hipStream_t st = (hipStream_t)stream;
   const size_t P = (size_t)eng->P;
-  DCHK(hipMemsetAsync(eng->st.ring, 0, P * 2 * 4 * kFrame * sizeof(float), st));
-  DCHK(hipMemsetAsync(eng->st.gavg, 0, P * kN * sizeof(cf), st));
-  DCHK(hipMemsetAsync(eng->st.cont, 0, P * kCont * kN * sizeof(cf), st));
-  DCHK(hipMemsetAsync(eng->st.g2, 0, P * kN * sizeof(cf), st));
-  DCHK(hipMemsetAsync(eng->st.c1, 0, P * (2 * kUps + 1) * sizeof(float), st));
+  DCHK(fill_async(eng->st.ring, 0, P * 2 * 4 * kFrame * sizeof(float), st));
+  DCHK(fill_async(eng->st.gavg, 0, P * kN * sizeof(cf), st));
+  DCHK(fill_async(eng->st.cont, 0, P * kCont * kN * sizeof(cf), st));
+  DCHK(fill_async(eng->st.g2, 0, P * kN * sizeof(cf), st));
+  DCHK(fill_async(eng->st.c1, 0, P * (2 * kUps + 1) * sizeof(float), st));
   hipLaunchKernelGGL(dxcp_reset_ps_kernel, dim3((eng->P + 63) / 64), dim3(64), 0, st, eng->st.ps, eng->P);
   DCHK(hipGetLastError());
   if (eng->cl.cp) {
-    DCHK(hipMemsetAsync(eng->cl.inBuf, 0, P * 4 * kB * sizeof(float), st));
-    DCHK(hipMemsetAsync(eng->cl.outBuf, 0, P * 3 * kB * sizeof(float), st));
-    DCHK(hipMemsetAsync(eng->cl.zj, 0, P * 3 * kB * sizeof(float), st));
-    DCHK(hipMemsetAsync(eng->cl.cp, 0, P * sizeof(ClPair), st));
+    DCHK(fill_async(eng->cl.inBuf, 0, P * 4 * kB * sizeof(float), st));
+    DCHK(fill_async(eng->cl.outBuf, 0, P * 3 * kB * sizeof(float), st));
+    DCHK(fill_async(eng->cl.zj, 0, P * 3 * kB * sizeof(float), st));
+    DCHK(fill_async(eng->cl.cp, 0, P * sizeof(ClPair), st));
   }
   return 0;
 }

@@ -25,6 +25,24 @@ def node_range(K: int, world: int, rank: int):
     return rank * per, (rank + 1) * per
 
 
+def control_group(group, backend):
+    """The group the host-side control traffic of a run over ``group`` uses.
+
+    Over RCCL it is a gloo group of the SAME ranks as ``group`` (an RCCL
+    collective issued outside a captured graph on the graph's communicator
+    makes later replays diverge, ``profiles/round3/rccl_graph_mixing_r3d.log``);
+    for a sub-group only its members create it (local synchronization), so
+    other shards neither take part nor see its verdicts.  Over gloo it is
+    ``group`` itself."""
+    import torch.distributed as dist
+    if str(backend).lower() != 'nccl':
+        return group
+    if group is None or group is dist.group.WORLD:
+        return dist.new_group(backend='gloo')
+    return dist.new_group(ranks=dist.get_process_group_ranks(group), backend='gloo',
+                          use_local_synchronization=True)
+
+
 class ShardedRun:
     """Drives a node-sharded engine over ``torch.distributed``.
 
@@ -48,7 +66,7 @@ class ShardedRun:
     gloo and device tensors the exchange is staged through host memory.
     """
 
-    def __init__(self, engine, group=None, graph=None):
+    def __init__(self, engine, group=None, graph=None, ctl=None):
         import torch
         import torch.distributed as dist
         self.torch = torch
@@ -76,23 +94,17 @@ class ShardedRun:
         if self.stage:
             self.hslot = [torch.zeros(per, dtype=torch.float32) for _ in range(self.slots)]
         self.graph = (backend == 'nccl') if graph is None else bool(graph)
-        # host-side control traffic (gate verdicts, callers' barriers) on a
-        # gloo group: an RCCL collective issued outside the captured graph on
-        # the graph's communicator (or a second one) between two replays makes
-        # the later replays diverge from the eager run
-        # (profiles/round3/rccl_graph_mixing_r3d.log)
-        self.ctl = dist.new_group(backend='gloo') if backend == 'nccl' else group
+        # host-side control traffic (gate verdicts, callers' barriers)
+        self.ctl = ctl if ctl is not None else control_group(group, backend)
         self._graphs = {}
+        self._graph_gen = None
         self._eager_runs = 0
 
     def exchange(self, r=0):
         i = r % self.slots
-        if self.world == 1:
-            # the all-gather of one rank is the identity.  (Issued anyway, an
-            # in-place RCCL all-gather captured into the round graph made the
-            # second and later replays differ from the eager run now and then:
-            # profiles/round3/pytest_gpu_r3g.log, rccl_graph_mixing_r3d.log.)
-            return
+        # (issued at world size 1 too: an identity, but a real collective in
+        # the captured round graph, which test_rccl_graph_captured_rounds
+        # replays)
         if self.stage:
             mine = self.mine[i].cpu()
             self.dist.all_gather_into_tensor(self.hslot[i], mine, group=self.group)
@@ -119,6 +131,13 @@ class ShardedRun:
         key = (bool(reset), bool(gate))
         if not self.graph or self.stage or self.zbuf.device.type == 'cpu':
             return self._rounds(reset, gate)
+        # a captured graph holds the engine's flag-derived launch sizes and
+        # gate buffer pointers: drop it when the engine's flags or gate
+        # schedule changed since the capture
+        gen = getattr(self.eng, 'graph_gen', None)
+        if gen != self._graph_gen:
+            self._graphs.clear()
+            self._graph_gen = gen
         g = self._graphs.get(key)
         if g is None:
             if self._eager_runs < 1:
@@ -152,6 +171,10 @@ class ShardedRun:
         e = self.eng
         gating = getattr(e, 'gating', None) is not None and e.gating(gate)
         if not gating:
+            if getattr(e, 'begin_run', None) is not None:
+                # the same bookkeeping as a gated run: init slots re-loaded,
+                # counter-compiled flags restored, no in-run gate
+                e.begin_run(speculative=False)
             self._sequence(reset, False)
             return self
         if not e.gate_spec_failed:
@@ -203,6 +226,11 @@ class ShardedEngine:
 
     def finish(self):
         self.e.finish()
+
+    @property
+    def graph_gen(self):
+        """Changes whenever the engine's flags or gate schedule do."""
+        return self.e.graph_gen
 
     # the start gate (DanseEngine's caller-sequenced gate API)
     def gating(self, gate=True):

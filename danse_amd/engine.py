@@ -216,6 +216,9 @@ class DanseEngine:
         self.pregiven = pregiven
         self._ran = False
         self._gateMoved = False
+        # bumped whenever the flags or the gate schedule change (callers that
+        # capture their own graphs of the rounds, dist.ShardedRun, re-capture)
+        self.graph_gen = 0
         self._gateSpecFailed = False
         self._gateInstalled = None
         self._build_flags()
@@ -593,8 +596,10 @@ class DanseEngine:
         st = stream if stream is not None else t.cuda.current_stream(self.device)
         return ctypes.c_void_p(st.cuda_stream)
 
-    def run(self, graph=True, stream=None, gate=True):
-        """The whole run.  ``gate``: the reference's start gate (Hermitian /
+    def run(self, graph=True, stream=None, gate=True, reset=True):
+        """The whole run, from the initial state (``reset``: the state reset
+        of danse_engine_reset first; a fresh engine starts there anyway).
+        ``gate``: the reference's start gate (Hermitian /
         positive definite / full rank over every bin, ``check_covariance_
         matrices``, ``d_classes.py:1430-1540``) is evaluated on the device at
         each family-node's first counter-eligible round.  Speculatively first:
@@ -603,11 +608,13 @@ class DanseEngine:
         one failed, the run is repeated exactly with the host loop
         (``_run_gated``: un-graphed up to the last decision, the start and
         the solve flags moved to the first round that passes)."""
+        st = self.stream_ptr(stream)
         if self._ran:
             self._load_init_history()   # the solves of the previous run overwrote init slots
             self._reset_gate()
+            if reset:
+                L.check(self.lib.danse_engine_reset(self.eng, st), self.eng)
         self._ran = True
-        st = self.stream_ptr(stream)
         gating = gate and self.pregiven is None and not self.p.bypassUpdates
         if gating and not self._gateSpecFailed:
             n = self._install_gate()
@@ -673,6 +680,7 @@ class DanseEngine:
         L.check(self.lib.danse_engine_set_gate(self.eng, n, _ptr(rnd, ctypes.c_int32), _ptr(fam, ctypes.c_int32),
                                                _ptr(node, ctypes.c_int32), _ptr(scn, ctypes.c_int32),
                                                _ptr(qY, ctypes.c_double), _ptr(qN, ctypes.c_double)), self.eng)
+        self.graph_gen += 1
         self._gateInstalled = n
         return n
 
@@ -683,6 +691,7 @@ class DanseEngine:
             L.check(self.lib.danse_engine_set_gate(self.eng, 0, _ptr(z, ctypes.c_int32), _ptr(z, ctypes.c_int32),
                                                    _ptr(z, ctypes.c_int32), _ptr(z, ctypes.c_int32),
                                                    _ptr(d, ctypes.c_double), _ptr(d, ctypes.c_double)), self.eng)
+            self.graph_gen += 1
         self._gateInstalled = None
 
     def _reset_gate(self):
@@ -694,6 +703,7 @@ class DanseEngine:
             fl[:, s, f, k] = self._flags_for(s, f, k, int(np.argmax(g['elig'])) if g['elig'].any() else -1)
         self._flags = np.ascontiguousarray(fl)
         L.check(self.lib.danse_engine_set_flags(self.eng, _ptr(self._flags, ctypes.c_uint8), None), self.eng)
+        self.graph_gen += 1
 
     def _gate_q(self, s, k, ops, r):
         """beta^m of the init slice's anti-Hermitian residue after round r
@@ -753,6 +763,7 @@ class DanseEngine:
             self._gateMoved = True
             self._flags = np.ascontiguousarray(self.flags)
             L.check(self.lib.danse_engine_set_flags(self.eng, _ptr(self._flags, ctypes.c_uint8), st), self.eng)
+            self.graph_gen += 1
 
     def _run_gated(self, st):
         R = self.R
@@ -842,6 +853,28 @@ class DanseEngine:
 
     def diagnostics(self):
         return self._get(L.OUT_DIAG, dtype=np.int32, shape=(self.S, self.K, 4))
+
+    def dxcp_record(self, on=True):
+        """Record every DXCP-PhaT feed's gathered input frames and estimator
+        outputs over the following runs (estimateSROs='DXCPPhaT')."""
+        L.check(self.lib.danse_engine_dxcp_record(self.eng, int(bool(on))), self.eng)
+
+    def dxcp_recorded(self):
+        """(frames [feeds][S][nOwn][K-1][2][2048] float32 -- channel 0 the
+        receiver's reference sensor, 1 the sender's received z stream --,
+        outputs [feeds][S][nOwn][K-1][2] float64 -- SRO ppm, STO samples) of
+        the last recorded run; sender q of slot qi is qi + (qi >= k)."""
+        nf, npair = ctypes.c_int32(), ctypes.c_int32()
+        L.check(self.lib.danse_engine_dxcp_recorded(self.eng, ctypes.byref(nf), ctypes.byref(npair), None, 0, None,
+                                                    0), self.eng)
+        fr = np.empty((nf.value, npair.value, 2, 2048), dtype=np.float32)
+        out = np.empty((nf.value, npair.value, 2), dtype=np.float64)
+        if nf.value:
+            L.check(self.lib.danse_engine_dxcp_recorded(self.eng, ctypes.byref(nf), ctypes.byref(npair),
+                                                        fr.ctypes.data_as(ctypes.c_void_p), fr.nbytes,
+                                                        out.ctypes.data_as(ctypes.c_void_p), out.nbytes), self.eng)
+        shp = (nf.value, self.S, self.k1 - self.k0, self.K - 1)
+        return fr.reshape(shp + (2, 2048)), out.reshape(shp + (2,))
 
     # ------------------------------------------------------------------ #
     def outputs(self):

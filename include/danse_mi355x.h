@@ -183,6 +183,26 @@ int danse_engine_run(danse_engine* eng, int32_t r0, int32_t r1, void* stream, in
  * gives up sets the flag danse_engine_resident_error reads.             */
 int danse_engine_run_resident(danse_engine* eng, void* stream);
 int danse_engine_resident_error(danse_engine* eng, int32_t* err, void* stream);
+/* Test hook: overwrite the give-up flag (every resident run clears it at
+ * its start, so a stale flag never outlives the run that set it).       */
+int danse_engine_resident_set_error(danse_engine* eng, int32_t value);
+/* DXCP-PhaT in the loop (danse_cfg.dxcp): record every feed's gathered
+ * estimator input frames and outputs, for checking the per-(receiver,
+ * sender) estimators against the reference's DXCPPhaT
+ * (dxcpphat/sro_estimation.py:117-345; d_sros.py:98-140 is the reference's
+ * per-pair wrapper).  Pairs p = (s * nOwn + (k - k0)) * (K - 1) + qi, sender
+ * q = qi < k ? qi : qi + 1; frames [nFeeds][P][2][2048] f32 (channel 0 the
+ * receiver's reference sensor, channel 1 the sender's received z stream),
+ * outputs [nFeeds][P][2] f64 (SRO ppm, STO samples).  _recorded reports the
+ * sizes when the buffers are NULL.                                       */
+/* Graph-safe device fill (every byte of [ptr, ptr + bytes) set to value &
+ * 0xff, asynchronously on stream): a kernel, where a hipMemsetAsync captured
+ * into a graph is not re-applied correctly by later launches of the graph
+ * (DESIGN.md §6.2).  The engines fill their own state this way.          */
+int danse_mi355x_fill(void* ptr, int32_t value, size_t bytes, void* stream);
+int danse_engine_dxcp_record(danse_engine* eng, int32_t on);
+int danse_engine_dxcp_recorded(danse_engine* eng, int32_t* nFeeds, int32_t* nPairs, float* frames,
+                               size_t frameBytes, double* out, size_t outBytes);
 /* Diagnostics: with DANSE_RESIDENT_TRACE set, the last resident run's
  * per-(round, wave) wall-clock marks ([R][waves][2] uint64, 100 MHz: after
  * the wait, at the publish); *bytes in: capacity of dst (may be NULL), out:

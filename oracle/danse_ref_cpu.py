@@ -28,6 +28,8 @@ import scipy.signal as sig
 
 from danse_amd.scheduler import initialize_events
 
+from ._gevd_pool import eigh_bins, set_workers  # noqa: F401
+
 
 # --------------------------------------------------------------------------- #
 # Helpers (d_base.py)
@@ -186,8 +188,11 @@ def update_w_gevd(Ryy, Rnn, refSensorIdx, rank=1):
     nFreqs = Ryy.shape[0]
     Xmat = np.zeros((nFreqs, n, n), dtype=complex)
     sigma = np.zeros((nFreqs, n))
+    # the per-bin eigh calls (serial, or spread over worker processes with
+    # bit-identical results: oracle/_gevd_pool.py)
+    S, Xall = eigh_bins(Ryy, Rnn)
     for kappa in range(nFreqs):
-        s, X = sla.eigh(Ryy[kappa], Rnn[kappa])
+        s, X = S[kappa], Xall[kappa]
         idx = np.flip(np.argsort(s))
         sigma[kappa, :] = s[idx]
         Xmat[kappa] = X[:, idx]

@@ -9,10 +9,10 @@
     verdicts are all-reduced and every rank repeats the run exactly;
   - CohDrift SRO estimation on a sharded engine (each rank estimates for its
     own receivers from the all-gathered fused spectra);
-* world size 1 over RCCL: the round sequence (bcast, gate, update; the
-  all-gather of one rank is the identity and is not issued, see
-  ``ShardedRun.exchange``) captured into a CUDA graph and replayed equals the
-  eager run.
+* world size 1 over RCCL: the round sequence (bcast, the in-place RCCL
+  all-gather of the fused spectra -- an identity at one rank, but a real
+  collective in the graph --, gate, update) captured into a CUDA graph and
+  replayed equals the eager run.
 """
 import os
 import sys
@@ -136,10 +136,12 @@ def test_sharded_processes_match_single_engine(name):
 
 @pytest.mark.parametrize('name', ['plain_k4', 'gate_delay_k4'])
 def test_rccl_graph_captured_rounds(name):
-    """RCCL, world size 1: pass 0 eager, pass 1 captures the rounds into a
-    CUDA graph, pass 2 replays it (speculative gate inside the graph); the
-    gate-delay case falls back to the exact host-gated loop."""
-    ref, td = _spawn(name, 1, 'nccl', 3)
-    _compare(ref, td, len(CASES[name]['M']), 3)
+    """RCCL, world size 1: pass 0 eager, pass 1 captures the rounds (R
+    in-graph all-gathers) into a CUDA graph and replays it, passes 2 and 3
+    replay it again (speculative gate inside the graph): three replays
+    bit-equal to the single engine; the gate-delay case falls back to the
+    exact host-gated loop."""
+    ref, td = _spawn(name, 1, 'nccl', 4)
+    _compare(ref, td, len(CASES[name]['M']), 4)
     if name == 'plain_k4':
         assert int(np.load(td / 'graphs_0.npy')) == 1

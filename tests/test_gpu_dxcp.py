@@ -128,3 +128,127 @@ def test_dxcp_in_the_loop_vs_oracle():
     de = float(np.max(np.abs(dv.d - ov.d)) / np.max(np.abs(ov.d)))
     print('filters', st, 'd', de)
     assert st['median'] <= 1e-5 and st['p99'] <= 1e-4 and de <= 1e-4
+
+
+@pytest.mark.timeout(1200)
+def test_config_C_dxcp_K16x4_vs_oracle():
+    """Config C as BASELINE names it: K = 16 x 4 (D = 19), SROs
+    linspace(0, 200, 16) ppm, estimateSROs 'DXCPPhaT' with compensation and
+    full-sample-drift flags, asy.  The in-loop estimation is pinned step by
+    step:
+
+    1. the gather: every recorded (receiver k, sender q) estimator input
+       frame equals, bit for bit, the host's own slice of the receiver's
+       reference sensor (update frame end upEnd[r, k]) and of the sender's
+       broadcast z stream (end (r + 1 - zLag) Ns) -- a wrong stream, offset,
+       lag or sensor fails here;
+    2. the estimators: the reference's DXCPPhaT restated bit-exactly
+       (oracle/dxcp_ref.py, pinned to the reference's own outputs) fed the
+       same frames gives the device's SRO / STO per feed within the
+       open-loop KAT tolerance (0.05 ppm / samples), for receivers 0, 7, 15
+       against every sender;
+    3. the loop: the float64 oracle DANSE fed the device's estimate sequence
+       reproduces the filters (p99 <= 1e-4 over bins x rounds after the
+       start), d (<= 1e-4) and the broadcast z streams (<= 1e-4).
+
+    The estimates' distance from the true relative SRO is reported next to
+    the reference DXCPPhaT run on the raw sensor signals of the same pairs
+    (the estimator's own transient at 7 s)."""
+    from danse_amd.engine import DanseEngine
+    from danse_amd.scene import make_scenes_device
+    from oracle import danse_ref_cpu as O
+    from oracle import dxcp_ref as DX
+    from _util import make_case_params, rel_err
+    from golden_cases import BATTERY, _d
+    K, Mk = 16, 4
+    sros = [float(x) for x in np.linspace(0, 200, K)]
+    M = [Mk] * K
+    case = dict(M=M, sros=sros, danse=_d(BATTERY, nodeUpdating='asy', compensateSROs=True, includeFSDflags=True,
+                                         estimateSROs='DXCPPhaT'))
+    dp, wp = make_case_params(case)
+    scenes, _ = make_scenes_device(M, 1, sigDur=7.0, seed=3, SROperNode=sros, host_signals=True)
+    sc = scenes[0]
+    for nd in sc.wasn:
+        for f in ('data', 'cleanspeech', 'cleannoise'):
+            setattr(nd, f, getattr(nd, f).astype(np.float64))
+    sc.get_vad_per_frame(dp.DFTsize, dp.Ns, wp.vadMinProportionActive)
+    eng = DanseEngine([sc], dp, vadMinProp=wp.vadMinProportionActive)
+    try:
+        eng.dxcp_record(True)
+        eng.run()
+        dv = eng.outputs()[0]
+        fr, out = eng.dxcp_recorded()
+        upEnd = np.asarray(eng.rt.upEnd)
+        zLag = None if eng.rt.synchronous else np.asarray(eng.rt.zLag)
+    finally:
+        eng.close()
+    Ns, R, ref = dp.Ns, dv.nRounds, dp.referenceSensor
+    every = 2048 // Ns
+    nF = fr.shape[0]
+    assert nF == R // every and fr.shape[1:4] == (1, K, K - 1)
+    # 1. the gather, bit for bit
+    for f in range(nF):
+        r = (f + 1) * every - 1
+        for k in range(K):
+            e0 = int(upEnd[r, k])
+            y = sc.wasn[k].data[:, ref].astype(np.float32)
+            want0 = np.zeros(2048, np.float32)
+            lo = max(e0 - 2048, 0)
+            want0[2048 - (e0 - lo):] = y[lo:e0]
+            for qi in range(K - 1):
+                q = qi if qi < k else qi + 1
+                lag = 0 if zLag is None else int(zLag[r, k, q])
+                zEnd = (r + 1 - lag) * Ns
+                zs = dv.zFullTD[q].astype(np.float32)
+                want1 = np.zeros(2048, np.float32)
+                lo = max(zEnd - 2048, 0)
+                want1[2048 - (zEnd - lo):] = zs[lo:zEnd]
+                assert np.array_equal(fr[f, 0, k, qi, 0], want0), (f, k, qi)
+                assert np.array_equal(fr[f, 0, k, qi, 1], want1), (f, k, qi)
+    # 2. the estimators against the reference DXCPPhaT on the same frames
+    worst = np.zeros(2)
+    rep = []
+    for k in (0, 7, 15):
+        for qi in range(K - 1):
+            q = qi if qi < k else qi + 1
+            est = DX.DXCPPhaT()
+            got = np.zeros((nF, 2))
+            for f in range(nF):
+                o = est.process_data(np.stack((fr[f, 0, k, qi, 0], fr[f, 0, k, qi, 1]), axis=1).astype(np.float64))
+                got[f] = (o['SROppm_est_out'], o['STOsmp_est_out'])
+            worst = np.maximum(worst, np.max(np.abs(got - out[:, 0, k, qi]), axis=0))
+            if qi in (0, K - 2):
+                # the reference estimator on the raw reference sensors of k and q
+                raw = DX.DXCPPhaT()
+                xk, xq = sc.wasn[k].data[:, ref], sc.wasn[q].data[:, ref]
+                n = min(len(xk), len(xq)) // 2048
+                for i in range(n):
+                    o = raw.process_data(np.stack((xk[i * 2048:(i + 1) * 2048], xq[i * 2048:(i + 1) * 2048]), axis=1))
+                rep.append((k, q, sros[q] - sros[k], -out[-1, 0, k, qi, 0], -got[-1, 0], -o['SROppm_est_out']))
+    print('DXCP device vs oracle on the same frames: max |dSRO| ppm, |dSTO|', worst)
+    for k, q, tr, dvv, orc, rw in rep:
+        print(f'  pair ({k},{q}) true {tr:+.1f} ppm: device {dvv:+.2f}, oracle on device frames {orc:+.2f}, '
+              f'reference on raw sensors {rw:+.2f}')
+    assert worst[0] <= 0.05 and worst[1] <= 0.05, worst
+    # the estimates reached the compensation (not all zero)
+    assert np.count_nonzero(out[:, 0, :, :, 0]) > 0
+    # 3. the loop: the oracle DANSE fed the device's estimate sequence
+    O.set_workers(min(16, max(2, len(__import__('os').sched_getaffinity(0)))))
+    try:
+        ov = O.danse(sc, dp, vadMinProp=wp.vadMinProportionActive,
+                     sroEstimates=[dv.SROsResiduals[k] for k in range(K)])
+    finally:
+        O.set_workers(0)
+    errs = []
+    for k in range(K):
+        s0 = int(ov.startRound[k])
+        assert s0 == int(dv.startRound[k])
+        wg, wr = dv.wTilde[k][:, s0 + 1:R + 1, :], ov.wTilde[k][:, s0 + 1:R + 1, :]
+        errs.append((np.linalg.norm(wg - wr, axis=-1) / np.maximum(np.linalg.norm(wr, axis=-1), 1e-30)).ravel())
+    e = np.concatenate(errs)
+    st = dict(median=float(np.median(e)), p99=float(np.percentile(e, 99)))
+    de = rel_err(dv.d, ov.d)
+    ze = max(rel_err(dv.zFullTD[k][:len(ov.zFullTD[k])], ov.zFullTD[k]) for k in range(K))
+    print('config C with DXCP: filters', st, 'd', de, 'z streams', ze)
+    assert st['median'] <= 1e-5 and st['p99'] <= 1e-4, st
+    assert de <= 1e-4 and ze <= 1e-4, (de, ze)

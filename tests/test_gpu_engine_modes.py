@@ -99,6 +99,25 @@ def test_resident_B_shape_vs_oracle(case):
     assert dg <= 1e-5
 
 
+def test_resident_error_flag_cleared_per_run():
+    """The resident run's give-up flag is cleared at the start of every run:
+    a flag poisoned by hand (as a timed-out wave would leave it) does not
+    make the next, successful run raise, and that run's outputs are the
+    first run's."""
+    from danse_amd import _lib as L
+    from danse_amd.engine import DanseEngine
+    sc, dp, wp = _scene_params(B_SHAPE[0])
+    eng = DanseEngine([sc], dp, smallDGrid=True, resident=True)
+    try:
+        eng.run()
+        d0 = eng.outputs()[0].d.copy()
+        L.check(eng.lib.danse_engine_resident_set_error(eng.eng, 1), eng.eng)
+        eng.run()
+        assert np.array_equal(eng.outputs()[0].d, d0)
+    finally:
+        eng.close()
+
+
 def test_resident_gate_delay_falls_back():
     """A start the reference gate delays (online_gate_delay_asy): the
     resident run's speculative gate checks (on the SCM snapshots of the
@@ -351,18 +370,31 @@ def test_condition_numbers_vs_oracle():
     dv = danse_multi([sc], dp)[0]
     ov = O.danse(sc, dp, vadMinProp=wp.vadMinProportionActive)
     cn, co = dv.condNumbers, ov.condNumbers
-    ratio = []
+    ratio, nsing = [], []
     for fam in ('DANSE', 'Local'):
         for k in range(4):
             it_d, it_o = getattr(cn, f'iter_cn_Ryy{fam}')[k], getattr(co, f'iter_cn_Ryy{fam}')[k]
-            n = min(len(it_d), len(it_o))
-            assert n > 10 and list(it_d[:n]) == list(it_o[:n]), (fam, k)
+            # the same saved iterations, all of them
+            assert len(it_d) > 10 and list(it_d) == list(it_o), (fam, k, it_d, it_o)
+            n = len(it_d)
             a = getattr(cn, f'cn_Ryy{fam}')[k][:, :n]
             b = getattr(co, f'cn_Ryy{fam}')[k][:, :n]
+            assert a.shape == b.shape, (fam, k)
             ok = np.isfinite(b) & (b < 1e6)
             assert np.all(np.isfinite(a[ok])), (fam, k)
             rel = np.abs(a[ok] - b[ok]) / b[ok]
             ratio.append(rel / (3e-6 * b[ok] + 1e-5))
+            # numerically singular in float64 (cond >= 1e6, e.g. the rank-one
+            # first-frame basis): the float32 device matrix is at least as
+            # ill-conditioned as float32 resolution can tell
+            sing = ~ok
+            if np.any(sing):
+                assert np.all(~np.isfinite(a[sing]) | (a[sing] >= 1e4)), (fam, k, np.nanmin(a[sing]))
+            nsing.append(int(np.count_nonzero(sing)))
     r = np.concatenate(ratio)
-    print('cond error / tolerance: median', np.median(r), 'p99', np.percentile(r, 99), 'max', r.max(), 'n', r.size)
+    out = int(np.count_nonzero(r > 1.0))
+    print('cond error / tolerance: median', np.median(r), 'p99', np.percentile(r, 99), 'max', r.max(), 'n', r.size,
+          'outliers', out, 'singular (skipped) values', sum(nsing))
     assert np.percentile(r, 99) <= 1.0 and np.median(r) <= 0.1, (np.median(r), np.percentile(r, 99))
+    # at most 0.1 % of the values above the tolerance, none by more than 10x
+    assert out <= 1e-3 * r.size and r.max() <= 10.0, (out, r.max())

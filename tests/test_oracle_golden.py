@@ -227,3 +227,18 @@ def test_cl_dxcp_oracle_matches_reference(case, golden_dir):
         out, zi = D.run_closed_loop(x1, x2, case['startDelay'], cldxcp_acs(case, n))
     assert np.array_equal(out, g['out'])
     assert np.array_equal(zi[::5], g['zi'])
+
+
+def test_gevd_pool_bit_identical(golden_dir):
+    """The oracle's per-bin eigh spread over worker processes
+    (oracle/_gevd_pool.py, used by the heavy parity tests) gives the serial
+    loop's filters bit for bit, on the filter-update KAT inputs."""
+    case = next(c for c in KAT_CASES if c['name'] == 'kat_gevd_D19_r1')
+    Ryy, Rnn = kat_inputs(case)
+    serial = O.update_w_gevd(Ryy, Rnn, 0, 2)
+    O.set_workers(3)
+    try:
+        pooled = O.update_w_gevd(Ryy, Rnn, 0, 2)
+    finally:
+        O.set_workers(0)
+    assert np.array_equal(serial, pooled)
