@@ -100,7 +100,7 @@ WORKLOADS = {
     # the battery itself (tests/battery20230919_perf_asfctofL.py:60-104): SROs [0, 200] ppm, Oracle
     # estimates, sandbox_config.yaml families on (local, centralised, SSBC: SSBC with compensation
     # raises in the reference, d_classes.py:2042-2044, so the comp variants run local + centralised);
-    # --L sets broadcastLength (the device fewSamples schedule covers L = 32..256 under these SROs)
+    # --L sets broadcastLength (every L in divisors(512): scheduler.compile_rounds_fs step lists)
     'E_noComp': dict(M=[2, 3], dur=10.0, nodeUpdating='asy', sros=[0.0, 200.0],
                      extra=dict(broadcastType='fewSamples', broadcastLength=64, compensateSROs=False,
                                 computeLocal=True, computeCentralised=True, computeSingleSensorBroadcast=True),

@@ -55,6 +55,7 @@ class DanseCfg(ctypes.Structure):
         ('cohDrift', _c_i32), ('cdSegLength', _c_i32), ('cdStart', _c_i32), ('cdEvery', _c_i32),
         ('cdCompensate', _c_i32), ('cdNIter', _c_i32), ('cdAlpha', ctypes.c_double), ('cdAlphaEps', ctypes.c_double),
         ('cEnd', _p_i32), ('cPhase', ctypes.POINTER(ctypes.c_double)), ('dxcp', _c_i32), ('smallDGrid', _c_i32),
+        ('fsEv', _p_i32), ('nFsEv', _c_i32), ('fsSteps', _p_i32), ('nFsSteps', _c_i32), ('rawStreams', _c_i32),
     ]
 
 
@@ -93,6 +94,7 @@ SIGNATURES = {
     'danse_engine_resident_set_error': (_c_i32, [ctypes.c_void_p, _c_i32]),
     'danse_engine_dxcp_record': (_c_i32, [ctypes.c_void_p, _c_i32]),
     'danse_mi355x_fill': (_c_i32, [ctypes.c_void_p, _c_i32, ctypes.c_size_t, ctypes.c_void_p]),
+    'danse_engine_run_steps': (_c_i32, [ctypes.c_void_p, _c_i32, _c_i32, ctypes.c_void_p]),
     'danse_engine_dxcp_recorded': (_c_i32, [ctypes.c_void_p, ctypes.POINTER(_c_i32), ctypes.POINTER(_c_i32),
                                             ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t]),
     'danse_engine_resident_trace': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_size_t)]),
@@ -160,6 +162,9 @@ SIGNATURES = {
     'danse_scene_last_error': (ctypes.c_char_p, []),
     'danse_scene_generate': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                       ctypes.c_void_p, ctypes.c_void_p]),
+    'danse_scene_convolve_vad': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p, _c_i32, _c_i32, _c_i32, ctypes.c_void_p,
+                                          ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_void_p,
+                                          ctypes.c_void_p]),
     'danse_stoi_last_error': (ctypes.c_char_p, []),
     'danse_stoi': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, _c_i32, ctypes.c_double, _c_i32,
                             ctypes.c_void_p, ctypes.c_void_p]),

@@ -56,6 +56,13 @@ struct BcastArgs {
   int dbg;                 // diagnostic ablation mask (DANSE_BCAST_ABLATE; 0 in production)
   const int* cEnd;         // [R*K] raw stream end of the centralised frame (danse_cfg.cEnd) or null
   cf* Cspec;               // [2][S][MT][F] (slot r & 1)
+  const float* rawStream;  // fewSamples raw streams [S][MT][zLen] (danse_cfg.rawStreams): the
+                           // centralised frame is rawStream[cEnd - N, cEnd) instead of y
+  // fewSamples step lists: the senders whose z frame this launch analyses
+  // (bit k), and zOnly = that analysis alone (a late z frame: no local-frame
+  // analyses, no estimate synthesis)
+  unsigned zMask;
+  int zOnly;
 };
 
 // y[(frame end - N) .. frame end) * win, zero before sample 0 -> buf (complex, imag 0)
@@ -118,18 +125,24 @@ __global__ void __launch_bounds__(256) bcast_kernel(const BcastArgs a) {
 #pragma unroll
     for (int c = 0; c < 16; ++c) zp[c] = cf{0.0f, 0.0f};
     // jobs: [0, Mk) broadcast frames, then the update frames (needUp), then
-    // the raw frames y[cEnd - N, cEnd) of the centralised buffers (cEnd)
-    const int nUp = needUp ? Mk : 0;
-    const int nJobs = Mk + nUp + (a.cEnd ? Mk : 0);
+    // the raw frames y[cEnd - N, cEnd) of the centralised buffers (cEnd; of
+    // the senders in zMask, whose received streams are complete); a zOnly
+    // launch (a late fewSamples z frame) runs only the last kind
+    const bool zk = ((a.zMask >> k) & 1u) != 0u;
+    const int nBc = a.zOnly ? 0 : Mk;
+    const int nUp = (needUp && !a.zOnly) ? Mk : 0;
+    const int nJobs = nBc + nUp + ((a.cEnd && zk) ? Mk : 0);
     for (int j = wv; j < nJobs; j += kBcWaves) {
-      const int kind = (j < Mk) ? 0 : (j < Mk + nUp ? 1 : 2);
+      const int kind = (j < nBc) ? 0 : (j < nBc + nUp ? 1 : 2);
       const bool up = kind == 1;
-      const int m = j - (kind == 0 ? 0 : (kind == 1 ? Mk : Mk + nUp));
+      const int m = j - (kind == 0 ? 0 : (kind == 1 ? nBc : nBc + nUp));
       const int ch = a.base[k] + m;
       const int fend = kind == 0 ? bEnd : (kind == 1 ? uEnd : a.cEnd[r * a.K + k]);
       cf v[16];
       if (a.dbg & 8) {
         for (int jj = 0; jj < 16; ++jj) v[jj] = cf{(float)(jj + threadIdx.x), 0.0f};
+      } else if (kind == 2 && a.rawStream) {
+        load_frame_wave(v, a.rawStream + ((long long)s * a.MT + ch) * a.zLen, fend, a.zLen, a.hA);
       } else {
         load_frame_wave(v, a.y + ((long long)s * a.MT + ch) * a.T, fend, a.T, a.hA);
       }
@@ -156,6 +169,8 @@ __global__ void __launch_bounds__(256) bcast_kernel(const BcastArgs a) {
   __syncthreads();
 
   if (a.doBcast && wv == 0 && a.fsTab) {
+    // (a sender outside zMask: its z frame is analysed by a later step)
+    if (((a.zMask >> k) & 1u) != 0u) {
     // ---- fewSamples: the chunks are already in the stream (fs_chunk_kernel);
     // the receivers' z frame is stream[ZEND - N, ZEND) (process_incoming_
     // signals_buffers, d_classes.py:1701-1807: the last N received samples)
@@ -175,6 +190,7 @@ __global__ void __launch_bounds__(256) bcast_kernel(const BcastArgs a) {
     for (int c = 0; c < 16; ++c) {
       const int f = wfft::out_index(c);
       if (f < F) Zs[f] = invSqNs * v[c];
+    }
     }
   } else if (a.doBcast && wv == 0 && !(a.dbg & 2)) {
     // ---- z synthesis: sqrt(Ns) * real(ifft(herm-ext(zhat))) * f, OLA with the previous frame
@@ -237,7 +253,7 @@ __global__ void __launch_bounds__(256) bcast_kernel(const BcastArgs a) {
   }
 
   // ---- synthesis of the estimates of round r-1, one family per wave
-  if (a.doSynth && !(a.dbg & 4)) {
+  if (a.doSynth && !a.zOnly && !(a.dbg & 4)) {
     const int rp = r - 1;
     const int end = a.upEnd[rp * a.K + k];
     const int w0 = a.doBcast ? 1 : 0;

@@ -102,8 +102,13 @@ struct danse_engine {
   long long *dInitW0Off = nullptr, *dInitScmOff = nullptr, *dExtSrcOff = nullptr, *dTgtOff = nullptr;
   // fewSamples broadcasts (cfg.fsTab): T(z) IRs [S][K][Mmax][2N-1], schedule
   int zLen = 0, Mmax = 0;
-  std::vector<int> fsTab;          // host copy [R][K][DANSE_FS_FIELDS]
+  std::vector<int> fsTab;          // host copy [R][K][DANSE_FS_FIELDS] (ZEND per consuming round)
   int* dFsTab = nullptr;
+  // the fewSamples device steps (danse_cfg.fsSteps): chunk rows [nEv][K][FIELDS],
+  // steps [n][DANSE_FS_STEP_FIELDS], first step of each round [R + 1]
+  std::vector<int> fsEv, fsSteps, fsRoundStep;
+  int* dFsEv = nullptr;
+  float* rawStream = nullptr;      // [S][MT][zLen] (cfg.rawStreams)
   float *wIR = nullptr, *dSn = nullptr;
   // DXCP-PhaT SRO estimation in the loop (cfg.dxcp, an extension: the
   // reference's integration raises, quirk Q12): one estimator per (scene,
@@ -221,6 +226,7 @@ struct FsArgs {
   const float* sn;           // window correlation / (N Ns), [2N-1]
   float* wIR;                // [S][K][Mmax][2N-1]
   float* zStream;            // [S][K][zLen]
+  float* rawStream;          // [S][MT][zLen] raw-sample streams of the centralised buffers, or null
 };
 
 DANSE_DEV const int* fs_entry(const FsArgs& a, int k) { return a.fsTab + ((long long)a.r * a.K + k) * DANSE_FS_FIELDS; }
@@ -270,6 +276,19 @@ __global__ void __launch_bounds__(tzc::kThr) fs_chunk_kernel(const FsArgs a) {
         return (idx >= 0 && idx < T) ? y[(long long)m * T + idx] : 0.0f;
       },
       [&](int i, int m) { return ir[(long long)m * tzc::kA + i]; }, [&](int i, float v) { z[i] = v; });
+  if (a.rawStream) {
+    // the raw samples the centralised buffers receive with the chunk
+    // (pre_fill_buffers_centralised + fill_buffers_centr, d_classes.py:
+    // 1162-1250: the last currL samples of the broadcast frame, zero before 0)
+    const int pos = e[DANSE_FS_POS];
+    for (int m = 0; m < Mk; ++m) {
+      float* o = a.rawStream + ((long long)s * a.MT + a.base[k] + m) * a.zLen + pos;
+      for (int i = threadIdx.x; i < L; i += blockDim.x) {
+        const int idx = end - L + i;
+        o[i] = (idx >= 0 && idx < T) ? y[(long long)m * T + idx] : 0.0f;
+      }
+    }
+  }
 }
 
 // Initial IR: a Dirac at tap N on the reference sensor (d_classes.py:660-663).
@@ -349,6 +368,7 @@ int danse_engine_reset(danse_engine* eng, void* stream) {
   HIPCHK(fill_async(eng->Zspec, 0, (size_t)2 * K * S * F * sizeof(cf), st));
   if (eng->Cspec) HIPCHK(fill_async(eng->Cspec, 0, (size_t)2 * S * eng->MT * F * sizeof(cf), st));
   HIPCHK(fill_async(eng->zStream, 0, (size_t)S * K * eng->zLen * sizeof(float), st));
+  if (eng->rawStream) HIPCHK(fill_async(eng->rawStream, 0, (size_t)S * eng->MT * eng->zLen * sizeof(float), st));
   if (eng->wIR) {
     HIPCHK(fill_async(eng->wIR, 0, (size_t)S * K * eng->Mmax * tzc::kA * sizeof(float), st));
     hipLaunchKernelGGL(fs_ir_init_kernel, dim3(S * K), dim3(64), 0, st, eng->wIR, K, eng->Mmax, eng->ref, eng->N);
@@ -419,14 +439,67 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
     for (int r = 0; r < R; ++r)
       for (int k = 0; k < K; ++k) {
         const int* e = &eng->fsTab[((size_t)r * K + k) * DANSE_FS_FIELDS];
-        if (e[DANSE_FS_LEN] < 0 || e[DANSE_FS_LEN] > c->N) return fail(eng, "fewSamples chunk length outside [0, N]");
-        if (e[DANSE_FS_POS] < 0 || e[DANSE_FS_POS] + e[DANSE_FS_LEN] > eng->zLen)
-          return fail(eng, "fewSamples chunk outside the stream");
         if (e[DANSE_FS_ZEND] < 0 || e[DANSE_FS_ZEND] > eng->zLen) return fail(eng, "fewSamples z frame end outside the stream");
-        if (e[DANSE_FS_IRSRC] > r || e[DANSE_FS_IRSRC] < -1) return fail(eng, "IR refresh from a future wExt iteration");
-        if (!c->keepHistory && e[DANSE_FS_IRSRC] >= 0 && e[DANSE_FS_IRSRC] != r)
-          return fail(eng, "IR refresh from an old wExt iteration needs keepHistory");
       }
+    if (K > 31) return fail(eng, "fewSamples steps: at most 31 nodes (node masks)");
+    const int all = (1 << K) - 1;
+    if (c->fsSteps) {
+      if (!c->fsEv || c->nFsSteps < 3 * R || c->nFsEv < 0) return fail(eng, "fewSamples steps without chunk rows");
+      eng->fsEv.assign(c->fsEv, c->fsEv + (size_t)c->nFsEv * K * DANSE_FS_FIELDS);
+      eng->fsSteps.assign(c->fsSteps, c->fsSteps + (size_t)c->nFsSteps * DANSE_FS_STEP_FIELDS);
+    } else {   // one CHUNK (fsTab row r), BCAST, UPDATE per round
+      eng->fsEv = eng->fsTab;
+      for (int r = 0; r < R; ++r) {
+        const int st[3][4] = {{DANSE_FS_STEP_CHUNK, r, all, r}, {DANSE_FS_STEP_BCAST, r, all, -1},
+                              {DANSE_FS_STEP_UPDATE, r, all, -1}};
+        for (auto& x : st) eng->fsSteps.insert(eng->fsSteps.end(), x, x + 4);
+      }
+    }
+    // validate: rounds contiguous and in order, one BCAST per round and before
+    // its updates, every node updated once per round, a chunk's IR source
+    // written before it (and still in the two-slot ring without history)
+    const int nSt = (int)(eng->fsSteps.size() / DANSE_FS_STEP_FIELDS);
+    const int nEv = (int)(eng->fsEv.size() / ((size_t)K * DANSE_FS_FIELDS));
+    std::vector<int> done(K, 0);
+    eng->fsRoundStep.assign(R + 1, nSt);
+    int cur = -1, upd = 0, bc = 0;
+    for (int i = 0; i < nSt; ++i) {
+      const int* x = &eng->fsSteps[(size_t)i * DANSE_FS_STEP_FIELDS];
+      const int ty = x[0], r = x[1], mask = x[2], row = x[3];
+      if (r != cur) {
+        if (r != cur + 1 || r >= R || (cur >= 0 && (upd != all || !bc))) return fail(eng, "fewSamples steps out of round order");
+        cur = r; upd = 0; bc = 0;
+        eng->fsRoundStep[r] = i;
+      }
+      if (mask & ~all) return fail(eng, "fewSamples step mask names a missing node");
+      if (ty == DANSE_FS_STEP_CHUNK) {
+        if (row < 0 || row >= nEv) return fail(eng, "fewSamples chunk row out of range");
+        for (int k = 0; k < K; ++k) {
+          const int* e = &eng->fsEv[((size_t)row * K + k) * DANSE_FS_FIELDS];
+          if (e[DANSE_FS_LEN] < 0 || e[DANSE_FS_LEN] > c->N) return fail(eng, "fewSamples chunk length outside [0, N]");
+          if (e[DANSE_FS_POS] < 0 || e[DANSE_FS_POS] + e[DANSE_FS_LEN] > eng->zLen)
+            return fail(eng, "fewSamples chunk outside the stream");
+          if (e[DANSE_FS_IRSRC] > done[k] || e[DANSE_FS_IRSRC] < -1)
+            return fail(eng, "IR refresh from a wExt iteration not yet written");
+          if (!c->keepHistory && e[DANSE_FS_IRSRC] >= 0 && e[DANSE_FS_IRSRC] < done[k] - 1)
+            return fail(eng, "IR refresh from an old wExt iteration needs keepHistory");
+        }
+      } else if (ty == DANSE_FS_STEP_BCAST) {
+        if (bc || upd) return fail(eng, "fewSamples BCAST step after an update of its round");
+        bc = 1;
+      } else if (ty == DANSE_FS_STEP_ZAN) {
+        if (!bc) return fail(eng, "fewSamples z analysis before its round's BCAST");
+      } else if (ty == DANSE_FS_STEP_UPDATE) {
+        if (!bc || (upd & mask)) return fail(eng, "fewSamples update step out of order");
+        upd |= mask;
+        for (int k = 0; k < K; ++k)
+          if ((mask >> k) & 1) done[k] = r + 1;
+      } else {
+        return fail(eng, "unknown fewSamples step type");
+      }
+    }
+    if (cur != R - 1 || upd != all || !bc) return fail(eng, "fewSamples steps do not cover every round");
+    eng->fsRoundStep[R] = nSt;
   }
   eng->extMode.assign(c->extMode, c->extMode + K);
   eng->base.resize(K);
@@ -615,6 +688,13 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
   if (c->fsTab) {
     HIPCHK(dalloc(&eng->dFsTab, eng->fsTab.size()));
     HIPCHK(hipMemcpy(eng->dFsTab, eng->fsTab.data(), eng->fsTab.size() * sizeof(int), hipMemcpyHostToDevice));
+    if (c->rawStreams) {
+      if (!c->cEnd) return fail(eng, "rawStreams needs cEnd (the consumed raw stream ends)");
+      HIPCHK(dalloc(&eng->rawStream, (size_t)S * eng->MT * eng->zLen));
+    }
+    HIPCHK(dalloc(&eng->dFsEv, std::max<size_t>(eng->fsEv.size(), 1)));
+    if (!eng->fsEv.empty())
+      HIPCHK(hipMemcpy(eng->dFsEv, eng->fsEv.data(), eng->fsEv.size() * sizeof(int), hipMemcpyHostToDevice));
     HIPCHK(dalloc(&eng->wIR, (size_t)S * K * eng->Mmax * tzc::kA));
     // sn[i] = sum_n f[n] h[n + i - N + 1] / (N Ns)  (dist_fct_approx with R = Ns)
     std::vector<float> sn(tzc::kA);
@@ -767,7 +847,7 @@ void danse_engine_destroy(danse_engine* eng) {
                   eng->dxEst, eng->resYB, eng->resYU, eng->resZall, eng->resZhat, eng->resRyyG, eng->resRnnG,
                   eng->resUFlag, eng->resZFlag, eng->resGateRound, eng->resDanseFni, eng->resErr, eng->resFams,
                   eng->resFrames, eng->resChanNode, eng->resTrace, eng->condHist, eng->dxRecFrames,
-                  eng->dxRecOut};
+                  eng->dxRecOut, eng->dFsEv, eng->rawStream};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (eng->dx) danse_dxcp_destroy(eng->dx);
@@ -797,7 +877,9 @@ static BcastArgs make_bcast(danse_engine* e, int r, int synth, int bc) {
   a.dbg = e->bcastAblate;
   a.zLen = e->zLen;
   a.fsTab = e->dFsTab;
-  a.cEnd = e->dCEnd; a.Cspec = e->Cspec;
+  a.cEnd = e->dCEnd; a.Cspec = e->Cspec; a.rawStream = e->rawStream;
+  a.zMask = ~0u;
+  a.zOnly = 0;
   return a;
 }
 
@@ -814,12 +896,16 @@ static UpdateArgs make_update(danse_engine* e, int r) {
   a.liCache = e->liCache; a.liStride = e->liStride;
   a.cdPhase = e->cdPhase;
   a.Cspec = e->Cspec; a.chanNode = e->dChanNode; a.cPhase = e->dCPhase;
+  a.nodeMask = ~0u;
   return a;
 }
 
-static void launch_update(danse_engine* e, int r, hipStream_t st) {
+// mask: the nodes updated by this launch; full: the round's last update
+// launch (its per-round extras run)
+static void launch_update(danse_engine* e, int r, hipStream_t st, unsigned mask = ~0u, bool full = true) {
   for (auto& cl : e->classes) {
     UpdateArgs a = make_update(e, r);
+    a.nodeMask = mask;
     a.nFN = (int)cl.host.size();
     a.fn = cl.dev;
     a.famNodeId = cl.devIds;
@@ -830,6 +916,7 @@ static void launch_update(danse_engine* e, int r, hipStream_t st) {
       launch_split_solve_class(cl.DMAX, a, cl.solveCount[r], st);
     }
   }
+  if (!full) return;
   if (e->condEvery > 0 && (r + 1) % e->condEvery == 0) {
     // (saved when i - last >= every, last starting at -1: d_classes.py:2128-2130)
     int dm = 1;
@@ -870,17 +957,18 @@ static void launch_update(danse_engine* e, int r, hipStream_t st) {
   }
 }
 
-static void launch_fs(danse_engine* e, int r, hipStream_t st) {
+// one CHUNK step: the T(z) IR refreshes and chunk appends of fsEv row `row`
+static void launch_fs(danse_engine* e, int row, hipStream_t st) {
   FsArgs a{};
-  a.S = e->S; a.K = e->K; a.MT = e->MT; a.T = e->T; a.N = e->N; a.F = e->F; a.r = r; a.k0 = e->k0; a.k1 = e->k1;
+  a.S = e->S; a.K = e->K; a.MT = e->MT; a.T = e->T; a.N = e->N; a.F = e->F; a.r = row; a.k0 = e->k0; a.k1 = e->k1;
   a.Mmax = e->Mmax; a.ref = e->ref; a.keepHistory = e->keepHistory; a.zLen = e->zLen;
-  a.M = e->dM; a.base = e->dBase; a.fsTab = e->dFsTab; a.y = e->y;
+  a.M = e->dM; a.base = e->dBase; a.fsTab = e->dFsEv; a.y = e->y;
   a.wExtHist = e->wExtHist; a.wExtNodeOff = e->dWExtNodeOff; a.wExtStride = e->wExtStride;
-  a.tw = e->dTw + e->N; a.sn = e->dSn; a.wIR = e->wIR; a.zStream = e->zStream;
+  a.tw = e->dTw + e->N; a.sn = e->dSn; a.wIR = e->wIR; a.zStream = e->zStream; a.rawStream = e->rawStream;
   const int nOwn = e->k1 - e->k0;
   bool refresh = false, chunk = false;
   for (int k = e->k0; k < e->k1; ++k) {
-    const int* t = &e->fsTab[((size_t)r * e->K + k) * DANSE_FS_FIELDS];
+    const int* t = &e->fsEv[((size_t)row * e->K + k) * DANSE_FS_FIELDS];
     refresh = refresh || t[DANSE_FS_IRSRC] >= 0;
     chunk = chunk || t[DANSE_FS_LEN] > 0;
   }
@@ -891,22 +979,63 @@ static void launch_fs(danse_engine* e, int r, hipStream_t st) {
   if (chunk) hipLaunchKernelGGL(fs_chunk_kernel, dim3(e->S * nOwn), dim3(tzc::kThr), 0, st, a);
 }
 
-static void launch_bcast(danse_engine* e, int r, int synth, int bc, hipStream_t st) {
-  if (bc && e->dFsTab) launch_fs(e, r, st);
+// zMask: fewSamples senders whose z frame this launch analyses; zOnly: that
+// analysis alone (no local-frame analyses, no estimate synthesis)
+static void launch_bcast(danse_engine* e, int r, int synth, int bc, hipStream_t st, unsigned zMask = ~0u,
+                         int zOnly = 0) {
   BcastArgs a = make_bcast(e, r, synth, bc);
+  a.zMask = zMask;
+  a.zOnly = zOnly;
   const unsigned grid = (unsigned)(e->S * (e->k1 - e->k0));
   hipLaunchKernelGGL(bcast_kernel, dim3(grid), dim3(256), 0, st, a);
 }
 
 // the installed speculative gate candidates of round r (danse_engine_set_gate)
-static void launch_gate_round(danse_engine* eng, int r, hipStream_t s) {
+// whose node is in `mask`
+static void launch_gate_round(danse_engine* eng, int r, hipStream_t s, unsigned mask = ~0u) {
   if (eng->nGate > 0 && eng->gateOff[r + 1] > eng->gateOff[r]) {
     const int n = eng->gateOff[r + 1] - eng->gateOff[r];
     const size_t lds = (size_t)eng->gateDmax[r] * (eng->gateDmax[r] + 1) * sizeof(cd);
-    hipLaunchKernelGGL(gate_kernel, dim3(eng->F, n), dim3(64), lds, s, make_update(eng, r), eng->dFnAll,
+    UpdateArgs a = make_update(eng, r);
+    a.nodeMask = mask;
+    hipLaunchKernelGGL(gate_kernel, dim3(eng->F, n), dim3(64), lds, s, a, eng->dFnAll,
                        eng->dGateCand + eng->gateOff[r], eng->dInitScmOff, eng->dScm0, eng->scmPerBin,
                        eng->dGateVerdict + eng->gateOff[r]);
   }
+}
+
+// fewSamples: steps [i0, i1) of the step list (compile_rounds_fs)
+static void run_fs_steps(danse_engine* e, int i0, int i1, hipStream_t st) {
+  const unsigned all = (1u << e->K) - 1u;
+  for (int i = i0; i < i1; ++i) {
+    const int* x = &e->fsSteps[(size_t)i * DANSE_FS_STEP_FIELDS];
+    const int ty = x[0], r = x[1];
+    const unsigned mask = (unsigned)x[2];
+    if (ty == DANSE_FS_STEP_CHUNK) {
+      launch_fs(e, x[3], st);
+    } else if (ty == DANSE_FS_STEP_BCAST) {
+      launch_bcast(e, r, r > 0, 1, st, mask, 0);
+    } else if (ty == DANSE_FS_STEP_ZAN) {
+      launch_bcast(e, r, 0, 1, st, mask, 1);
+    } else {
+      // the round's per-round extras (condition numbers, SRO estimators) run
+      // with its last update step
+      unsigned upd = 0;
+      for (int j = e->fsRoundStep[r]; j <= i; ++j) {
+        const int* y = &e->fsSteps[(size_t)j * DANSE_FS_STEP_FIELDS];
+        if (y[0] == DANSE_FS_STEP_UPDATE) upd |= (unsigned)y[2];
+      }
+      launch_gate_round(e, r, st, mask);
+      launch_update(e, r, st, mask, upd == all);
+    }
+  }
+}
+
+// the first UPDATE step of round r (fewSamples)
+static int fs_first_update(const danse_engine* e, int r) {
+  for (int i = e->fsRoundStep[r]; i < e->fsRoundStep[r + 1]; ++i)
+    if (e->fsSteps[(size_t)i * DANSE_FS_STEP_FIELDS] == DANSE_FS_STEP_UPDATE) return i;
+  return e->fsRoundStep[r + 1];
 }
 
 int danse_engine_gate_launch(danse_engine* eng, int32_t r, void* stream) {
@@ -915,7 +1044,9 @@ int danse_engine_gate_launch(danse_engine* eng, int32_t r, void* stream) {
   HIPCHK(hipSetDevice(eng->dev));
   hipStream_t st = (hipStream_t)stream;
   if (eng->nGate > 0 && r == 0) HIPCHK(fill_async(eng->dGateVerdict, 0xff, eng->nGate * sizeof(int), st));
-  launch_gate_round(eng, r, st);
+  // (fewSamples: the checks run inside danse_engine_update, before each
+  // update step of their node)
+  if (!eng->dFsTab) launch_gate_round(eng, r, st);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -924,7 +1055,10 @@ int danse_engine_bcast(danse_engine* eng, int32_t r, void* stream) {
   if (!eng || !eng->y) return fail(eng, "inputs not set");
   if (r < 0 || r >= eng->R) return fail(eng, "round out of range");
   HIPCHK(hipSetDevice(eng->dev));
-  launch_bcast(eng, r, r > 0, 1, (hipStream_t)stream);
+  if (eng->dFsTab)
+    run_fs_steps(eng, eng->fsRoundStep[r], fs_first_update(eng, r), (hipStream_t)stream);
+  else
+    launch_bcast(eng, r, r > 0, 1, (hipStream_t)stream);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -933,7 +1067,21 @@ int danse_engine_update(danse_engine* eng, int32_t r, void* stream) {
   if (!eng) return fail(eng, "null engine");
   if (r < 0 || r >= eng->R) return fail(eng, "round out of range");
   HIPCHK(hipSetDevice(eng->dev));
-  launch_update(eng, r, (hipStream_t)stream);
+  if (eng->dFsTab)
+    run_fs_steps(eng, fs_first_update(eng, r), eng->fsRoundStep[r + 1], (hipStream_t)stream);
+  else
+    launch_update(eng, r, (hipStream_t)stream);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int danse_engine_run_steps(danse_engine* eng, int32_t s0, int32_t s1, void* stream) {
+  if (!eng || !eng->y) return fail(eng, "inputs not set");
+  if (!eng->dFsTab) return fail(eng, "step lists are for fewSamples engines");
+  const int n = (int)(eng->fsSteps.size() / DANSE_FS_STEP_FIELDS);
+  if (s0 < 0 || s1 > n || s0 > s1) return fail(eng, "bad step range");
+  HIPCHK(hipSetDevice(eng->dev));
+  run_fs_steps(eng, s0, s1, (hipStream_t)stream);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -953,10 +1101,14 @@ int danse_engine_run(danse_engine* eng, int32_t r0, int32_t r1, void* stream, in
   hipStream_t st = (hipStream_t)stream;
   auto seq = [&](hipStream_t s) {
     if (eng->nGate > 0 && r0 == 0) (void)fill_async(eng->dGateVerdict, 0xff, eng->nGate * sizeof(int), s);
-    for (int r = r0; r < r1; ++r) {
-      launch_bcast(eng, r, r > 0, 1, s);
-      launch_gate_round(eng, r, s);
-      launch_update(eng, r, s);
+    if (eng->dFsTab) {
+      run_fs_steps(eng, eng->fsRoundStep[r0], eng->fsRoundStep[r1], s);
+    } else {
+      for (int r = r0; r < r1; ++r) {
+        launch_bcast(eng, r, r > 0, 1, s);
+        launch_gate_round(eng, r, s);
+        launch_update(eng, r, s);
+      }
     }
     if (r1 == eng->R) launch_bcast(eng, eng->R, 1, 0, s);
   };

@@ -39,6 +39,7 @@ __global__ void __launch_bounds__(64) gate_kernel(const UpdateArgs a, const FamN
   const int f = blockIdx.x;
   const GateCand c = cand[blockIdx.y];
   const FamNode d = fns[c.fni];
+  if (!node_in(a.nodeMask, d.k)) return;   // (fewSamples: checked before its node's update step)
   const int D = d.D, s = c.s, F = a.F;
   const int P = D + 1;
   const bool act = li < D;

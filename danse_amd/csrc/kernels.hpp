@@ -88,7 +88,12 @@ struct UpdateArgs {
   // lane-grid kernel runs them, one launch item per entry of solveItems
   int splitSolve;
   const int* solveItems;   // this round's solving items (s * nFN + fni)
+  // fewSamples step lists (compile_rounds_fs): the nodes this launch updates
+  // (bit k: node k); the others are left untouched
+  unsigned nodeMask;
 };
+
+DANSE_DEV bool node_in(unsigned mask, int k) { return ((mask >> k) & 1u) != 0u; }
 
 // Agent-coherent (sc1) 8-byte load / store of a complex value: the resident
 // engine's hand-offs between waves of one launch (payload stored sc1 and

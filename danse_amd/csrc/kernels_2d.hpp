@@ -57,6 +57,7 @@ update_kernel_2d(const UpdateArgs a) {
   const int fni = tt % a.nFN;
   const int s = tt / a.nFN;
   const FamNode d = a.fn[fni];
+  if (!node_in(a.nodeMask, d.k)) return;   // wave-uniform: one item per wave
   const int D = d.D;
   const int r = a.r;
   const uint8_t fl = a.flags[(((long long)r * a.S + s) * kMaxFam + d.fam) * a.K + d.k];

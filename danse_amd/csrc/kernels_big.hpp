@@ -22,6 +22,7 @@ __global__ void __launch_bounds__(64) update_kernel_big(const UpdateArgs a) {
   const int fni = t % a.nFN;
   const int s = t / a.nFN;
   const FamNode d = a.fn[fni];
+  if (!node_in(a.nodeMask, d.k)) return;   // one bin per wave
   const int D = d.D;
   const bool act = li < D;
   const int r = a.r;

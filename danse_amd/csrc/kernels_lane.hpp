@@ -46,8 +46,9 @@ __global__ void __launch_bounds__(64) update_kernel_lane(const UpdateArgs a) {
   constexpr int NT = tri_n(D);
   const LaneIdx ix = lane_index(a);
   const int F = a.F, f = ix.f, s = ix.s, r = a.r;
-  const bool valid = ix.valid;
   const FamNode d = a.fn[ix.fni];
+  // (lanes of nodes outside the launch's node mask compute and store nothing)
+  const bool valid = ix.valid && node_in(a.nodeMask, d.k);
   const uint8_t fl = a.flags[(((long long)r * a.S + s) * kMaxFam + d.fam) * a.K + d.k];
   const int opY = fl & 3, opN = (fl >> 2) & 3;
   const bool solve = (fl & DANSE_FLAG_SOLVE) != 0 && (fl & DANSE_FLAG_PREGIVEN) == 0;

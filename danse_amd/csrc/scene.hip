@@ -258,8 +258,10 @@ __global__ void mix_kernel(SceneArgs a, const float* __restrict__ wS, const floa
   }
 }
 
-// energy VAD of node k's mic-0 wet speech: window of nw samples centred on
-// each sample, [i - nw/2, i + nw/2) clipped, energy > max(x^2) / 10^(dB/10)
+// energy VAD of node k's mic-0 wet speech (oracleVAD + compute_VAD,
+// siggen/utils.py:1079-1151): window [i - nw/2, i + nw/2) clipped to the
+// signal, its MEAN energy > max(x^2) / 10^(dB/10) (get_or_load_vad,
+// siggen/utils.py:921)
 __global__ void vad_kernel(const float* __restrict__ wS, int S, int K, int MT, int T, const int* __restrict__ base,
                            int nw, double dB, const double* __restrict__ maxSq, uint8_t* __restrict__ vad) {
   const long long n = (long long)S * K * T;
@@ -271,7 +273,7 @@ __global__ void vad_kernel(const float* __restrict__ wS, int S, int K, int MT, i
     const long long b = max(i - nw / 2, 0LL), en = min(i + nw / 2, (long long)T);
     double acc = 0.0;
     for (long long j = b; j < en; ++j) acc += (double)x[j] * (double)x[j];
-    vad[e] = acc > maxSq[(long long)s * K + k] / pow(10.0, dB / 10.0) ? 1 : 0;
+    vad[e] = acc / (double)(en - b) > maxSq[(long long)s * K + k] / pow(10.0, dB / 10.0) ? 1 : 0;
   }
 }
 
@@ -411,6 +413,63 @@ int danse_scene_generate(const danse_scene_cfg* c, float* data, float* cleanspee
   cleanup();
   if (le != hipSuccess) return fail(std::string("scene launch: ") + hipGetErrorString(le));
   if (se != hipSuccess) return fail(std::string("scene: ") + hipGetErrorString(se));
+  return 0;
+}
+
+int danse_scene_convolve_vad(const float* x, const float* h, int32_t rows, int32_t T, int32_t nIR, float* out,
+                             double vadWinLength, double fs, double vadEnergyDecrease_dB, uint8_t* vad,
+                             void* stream) {
+  if (!x || !h || !out || rows < 1 || T < 1 || nIR < 1) return fail("bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  std::vector<void*> owned;
+  auto cleanup = [&]() {
+    for (void* p : owned) (void)hipFree(p);
+  };
+  auto alloc = [&](void** p, size_t bytes) -> bool {
+    if (hipMalloc(p, bytes < 8 ? 8 : bytes) != hipSuccess) return false;
+    owned.push_back(*p);
+    return true;
+  };
+  // the generator's kernels on rows (s = row, one channel, two sources w):
+  // both sources carry the injected row, the second output is discarded
+  float *ir2 = nullptr, *wN = nullptr;
+  int* dBase = nullptr;
+  double* mx = nullptr;
+  if (!alloc((void**)&ir2, (size_t)rows * 2 * nIR * sizeof(float)) ||
+      !alloc((void**)&wN, (size_t)rows * T * sizeof(float)) || !alloc((void**)&dBase, sizeof(int)) ||
+      !alloc((void**)&mx, (size_t)rows * sizeof(double))) {
+    cleanup();
+    return fail("convolve: device allocation failed");
+  }
+  for (int r = 0; r < rows; ++r)
+    for (int w = 0; w < 2; ++w)
+      if (hipMemcpyAsync(ir2 + ((size_t)r * 2 + w) * nIR, h + (size_t)r * nIR, nIR * sizeof(float),
+                         hipMemcpyDeviceToDevice, st) != hipSuccess) {
+        cleanup();
+        return fail("convolve: IR copy failed");
+      }
+  const int zero = 0;
+  if (hipMemcpyAsync(dBase, &zero, sizeof(int), hipMemcpyHostToDevice, st) != hipSuccess) {
+    cleanup();
+    return fail("convolve: upload failed");
+  }
+  SceneArgs a{};
+  a.S = rows; a.K = 1; a.MT = 1; a.T = T; a.nIR = nIR;
+  const int nBlk = (T + kConvOut - 1) / kConvOut;
+  hipLaunchKernelGGL(conv_kernel, dim3((unsigned)((long long)rows * 2 * nBlk)), dim3(kThr), 0, st, a, x, x, ir2, out,
+                     wN);
+  if (vad) {
+    auto grid = [](long long n) { return dim3((unsigned)std::min<long long>((n + kThr - 1) / kThr, 1 << 20)); };
+    hipLaunchKernelGGL(max_sq_kernel, dim3(rows), dim3(kThr), 0, st, out, T, 1, 1, dBase, mx);
+    const int nw = std::max((int)(vadWinLength * fs), 1);
+    hipLaunchKernelGGL(vad_kernel, grid((long long)rows * T), dim3(kThr), 0, st, out, rows, 1, 1, T, dBase, nw,
+                       vadEnergyDecrease_dB, mx, vad);
+  }
+  const hipError_t le = hipGetLastError();
+  const hipError_t se = hipStreamSynchronize(st);
+  cleanup();
+  if (le != hipSuccess) return fail(std::string("convolve launch: ") + hipGetErrorString(le));
+  if (se != hipSuccess) return fail(std::string("convolve: ") + hipGetErrorString(se));
   return 0;
 }
 

@@ -27,7 +27,8 @@ from dataclasses import dataclass
 import numpy as np
 
 from . import _lib as L
-from .scheduler import initialize_events, compile_rounds, compile_rounds_fs, FS_BCEND, FS_LEN, FS_POS, FS_ZEND
+from .scheduler import (initialize_events, compile_rounds, compile_rounds_fs, FS_BCEND, FS_LEN, FS_POS, FS_ZEND,
+                        FS_IRSRC, FS_FIELDS, FS_STEP_UPDATE)
 from .outputs import host_fields, stft_frames
 
 
@@ -172,6 +173,11 @@ class DanseEngine:
         else:
             self.rt = compile_rounds(events, fs, p, K)
         self.R = R = self.rt.nRounds
+        if self.fewSamples and (self.k0, self.k1) != (0, K) and any(self._split_round(r) for r in range(R)):
+            # a node-subset update step inside a round would need its own
+            # exchange of the late chunk's z frame between the ranks
+            raise NotImplementedError('node-sharded fewSamples engines: rounds whose updates run in several steps '
+                                      '(SRO clocks with L < Ns drift)')
         if (self.k0, self.k1) != (0, K) and (p.computeCentralised or p.computeSingleSensorBroadcast):
             # the centralised / SSBC observation vectors read every node's raw
             # local spectra and the centralised VAD averages every node's VAD;
@@ -326,8 +332,11 @@ class DanseEngine:
         buffers as to the z buffers (Ns first samples of the broadcast frame
         for wholeChunk, the last currL for fewSamples), so the buffer flags are
         the z flags and receiver k's frame of q is the last N samples of q's
-        raw stream: y_q[E - N, E) with E = ``cEnd[r][q]`` (the stream is
-        contiguous from sample 0, checked here), read with the z lag.  The
+        raw stream: y_q[E - N, E) with E = ``cEnd[r][q]`` (wholeChunk: the
+        stream is contiguous from sample 0, checked here; fewSamples: the
+        chunks' frame ends floor(t fs) can overlap or skip a sample, so the
+        device keeps the raw streams themselves, danse_cfg.rawStreams), read
+        with the z lag.  The
         compensation phase of the centralised vector (``compensate_sros``,
         ``d_classes.py:1996-2038``) keeps the reference's flag index
         arithmetic (quirk Q14: the flag of sender q lands on
@@ -338,27 +347,15 @@ class DanseEngine:
         p, K, R, N, Ns = self.p, self.K, self.R, self.N, self.Ns
         self._cEnd = None
         self._cPhase = None
+        self._rawStreams = 0
         if self.rt.synchronous or not (p.computeCentralised or p.computeSingleSensorBroadcast):
             return
         if self.fewSamples:
-            tab = self.rt.fsTab
-            cEnd = np.zeros((R, K), dtype=np.int64)
-            for q in range(K):
-                off = None
-                for r in range(R):
-                    ln = int(tab[r, q, FS_LEN])
-                    if ln > 0:
-                        o = int(tab[r, q, FS_BCEND]) - int(tab[r, q, FS_POS]) - ln
-                        if off is None:
-                            off = o
-                        elif o != off:
-                            raise NotImplementedError(f'node {q} raw broadcast stream is not contiguous')
-                # off < 0: the first chunk starts with the zero padding of a
-                # frame that ends before sample N (raw index < 0 reads zero,
-                # as in the stream); off > 0 would leave unsent samples
-                if off is not None and off > 0:
-                    raise NotImplementedError(f'node {q} raw broadcast stream does not start at sample 0')
-                cEnd[:, q] = np.maximum(tab[:R, q, FS_ZEND] + (off or 0), 0)
+            # the centralised buffers receive each chunk's raw samples into
+            # per-channel streams at the z streams' positions (danse_cfg.
+            # rawStreams): receiver k's frame of q ends where its z frame does
+            self._rawStreams = 1
+            cEnd = self.rt.fsTab[:R, :, FS_ZEND].astype(np.int64)
         else:
             bc = self.rt.bcEnd[:R]
             if R > 1 and not np.all(np.diff(bc, axis=0) == Ns):
@@ -544,6 +541,18 @@ class DanseEngine:
         c.zPhase = _ptr(self._zPhase, ctypes.c_double)
         self._fsTab = np.ascontiguousarray(self.rt.fsTab, dtype=np.int32) if self.fewSamples else None
         c.fsTab = _ptr(self._fsTab, ctypes.c_int32)
+        if self.fewSamples:
+            # the step list (chunk appends, analyses, node-subset updates in
+            # the reference's dependency order) and its chunk rows, padded to
+            # the fsTab field layout
+            ev = self.rt.fsEv
+            rows = np.zeros((max(len(ev), 1), K, FS_FIELDS), dtype=np.int32)
+            rows[:, :, FS_IRSRC] = -1
+            rows[:len(ev), :, :4] = ev
+            self._fsEv = np.ascontiguousarray(rows)
+            self._fsSteps = np.ascontiguousarray(self.rt.fsSteps, dtype=np.int32)
+            c.fsEv, c.nFsEv = _ptr(self._fsEv, ctypes.c_int32), int(len(ev))
+            c.fsSteps, c.nFsSteps = _ptr(self._fsSteps, ctypes.c_int32), int(len(self._fsSteps))
         c.scmInitPerBin = 0 if p.covMatSameInitForAllFreqs else 1
         if self.cohDrift:
             cd = p.cohDrift
@@ -556,6 +565,7 @@ class DanseEngine:
             c.dxcp = 1
             c.cdCompensate = int(bool(p.compensateSROs))
         c.cEnd = _ptr(self._cEnd, ctypes.c_int32)
+        c.rawStreams = int(self._rawStreams)
         c.cPhase = _ptr(self._cPhase, ctypes.c_double)
         c.zStreamLen = int(self.rt.zStreamLen) if self.fewSamples else 0
         self.zLen = c.zStreamLen if self.fewSamples else self.R * self.Ns
@@ -724,12 +734,12 @@ class DanseEngine:
                 pending[key] = int(e[0])
         return pending
 
-    def _gate_decide(self, rc, pending, st):
+    def _gate_decide(self, rc, pending, st, nodes=None):
         """The exact gate of round rc (after its broadcast, before its update):
-        check every candidate pending at rc on the device, move the start
-        (and the solve flags) of those that fail to their next eligible
-        round, and upload the flags if they changed."""
-        cands = sorted(key for key, r in pending.items() if r == rc)
+        check every candidate pending at rc (of ``nodes``, default all) on the
+        device, move the start (and the solve flags) of those that fail to
+        their next eligible round, and upload the flags if they changed."""
+        cands = sorted(key for key, r in pending.items() if r == rc and (nodes is None or key[2] in nodes))
         if not cands:
             return
         fam = np.array([c[1] for c in cands], dtype=np.int32)
@@ -765,6 +775,13 @@ class DanseEngine:
             L.check(self.lib.danse_engine_set_flags(self.eng, _ptr(self._flags, ctypes.c_uint8), st), self.eng)
             self.graph_gen += 1
 
+    def _split_round(self, r):
+        """fewSamples: round r's updates run as several node-subset steps."""
+        if not self.fewSamples:
+            return False
+        rs = self.rt.fsRoundStep
+        return int(np.count_nonzero(self.rt.fsSteps[rs[r]:rs[r + 1], 0] == FS_STEP_UPDATE)) > 1
+
     def _run_gated(self, st):
         R = self.R
         pending = self._gate_pending()
@@ -773,9 +790,22 @@ class DanseEngine:
             rc = min(pending.values())
             if rc > r0:
                 L.check(self.lib.danse_engine_run(self.eng, r0, rc, st, 0), self.eng)
-            L.check(self.lib.danse_engine_bcast(self.eng, rc, st), self.eng)
-            self._gate_decide(rc, pending, st)
-            L.check(self.lib.danse_engine_update(self.eng, rc, st), self.eng)
+            if self._split_round(rc):
+                # each node's gate right before its own update step (its z
+                # frames may be analysed only after another node's update)
+                rs = self.rt.fsRoundStep
+                i0 = int(rs[rc])
+                for i in range(int(rs[rc]), int(rs[rc + 1])):
+                    ty, _, mask, _ = (int(x) for x in self.rt.fsSteps[i])
+                    if ty == FS_STEP_UPDATE:
+                        L.check(self.lib.danse_engine_run_steps(self.eng, i0, i, st), self.eng)
+                        self._gate_decide(rc, pending, st, nodes={k for k in range(self.K) if (mask >> k) & 1})
+                        i0 = i
+                L.check(self.lib.danse_engine_run_steps(self.eng, i0, int(rs[rc + 1]), st), self.eng)
+            else:
+                L.check(self.lib.danse_engine_bcast(self.eng, rc, st), self.eng)
+                self._gate_decide(rc, pending, st)
+                L.check(self.lib.danse_engine_update(self.eng, rc, st), self.eng)
             r0 = rc + 1
             if r0 >= R:
                 break

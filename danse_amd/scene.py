@@ -254,3 +254,29 @@ def make_scenes_device(nSensorPerNode, S, sigDur=10.0, fs=16000.0, seed=0, snr=5
                                   vad=vad[s, k][:, None].astype(np.float64), **sig))
         scenes.append(Scene(wasn=wasn, fs=fs, seed=seed + s))
     return scenes, out
+
+
+def convolve_vad(x, h, fs=16000.0, vadWinLength=0.04, vadEnergyDecrease_dB=40.0, vad=True, device=0):
+    """The device generator's convolution and VAD kernels on given rows
+    (``danse_scene_convolve_vad``): ``x`` [rows][T] and ``h`` [rows][nIR]
+    (host arrays, rounded to float32) -> (out [rows][T] float32 = (x * h)
+    [:T], vad [rows][T] uint8 = oracleVAD(out), or None).  The checks of the
+    generator against the reference's get_vad on injected inputs use it."""
+    import ctypes
+    import torch
+    from . import _lib as L
+    lib = L.load_library()
+    dev = f'cuda:{device}'
+    xt = torch.as_tensor(np.ascontiguousarray(x, dtype=np.float32), device=dev)
+    ht = torch.as_tensor(np.ascontiguousarray(h, dtype=np.float32), device=dev)
+    rows, T = xt.shape
+    out = torch.empty((rows, T), dtype=torch.float32, device=dev)
+    v = torch.empty((rows, T), dtype=torch.uint8, device=dev) if vad else None
+    st = torch.cuda.current_stream(device).cuda_stream
+    rc = lib.danse_scene_convolve_vad(ctypes.c_void_p(xt.data_ptr()), ctypes.c_void_p(ht.data_ptr()), int(rows),
+                                      int(T), int(ht.shape[1]), ctypes.c_void_p(out.data_ptr()), float(vadWinLength),
+                                      float(fs), float(vadEnergyDecrease_dB),
+                                      ctypes.c_void_p(v.data_ptr() if v is not None else 0), ctypes.c_void_p(st))
+    if rc != 0:
+        raise L.DanseError((lib.danse_scene_last_error() or b'').decode() or f'error {rc}')
+    return out.cpu().numpy(), (v.cpu().numpy() if v is not None else None)

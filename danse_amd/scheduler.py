@@ -298,6 +298,9 @@ def compile_rounds(events, fs, p, nNodes: int) -> RoundTables:
 
 FS_FIELDS = 5   # enum danse_fs_field (include/danse_mi355x.h)
 FS_BCEND, FS_LEN, FS_POS, FS_IRSRC, FS_ZEND = range(FS_FIELDS)
+# fewSamples device steps (enum danse_fs_step): one row (type, round, node
+# mask, chunk-table row) per launch group
+FS_STEP_CHUNK, FS_STEP_BCAST, FS_STEP_ZAN, FS_STEP_UPDATE = range(4)
 
 
 def compile_rounds_fs(events, fs, p, nNodes: int, timeStamps, M) -> RoundTables:
@@ -315,27 +318,44 @@ def compile_rounds_fs(events, fs, p, nNodes: int, timeStamps, M) -> RoundTables:
     the samples received so far (zero before 0, the reference's front
     padding).
 
-    Device round r runs the broadcasts of every node at its own iteration r
-    (wExt index r), then the updates r.  A schedule is accepted when
-    (i) each node broadcasts at most once per own iteration, (ii) every
-    update consumes only chunks broadcast in its round or earlier, and
-    (iii) in round r all receivers of a sender consume the same stream length
-    (always true at K = 2 and on synchronous clocks).  Returns RoundTables with
-    ``fsTab [R][K][FS_FIELDS]`` and ``zStreamLen``."""
+    The broadcast instants of a node are its neighbours' update instants
+    snapped to its own L-sample grid (``d_base.py:837-863``), so under SRO
+    clocks a broadcast can fall anywhere between the updates: before the
+    node's own update of the same iteration, after it (a faster node's chunk
+    that its slower neighbour consumes in the same round, computed with the
+    node's NEXT iteration's IR when the refresh timer fires there: L < 32 at
+    200 ppm over 10 s), or twice in one iteration (L = Ns, the first
+    snapped instants).  The device therefore runs a round as a list of steps
+    (``fsSteps``): chunk appends (``fsEv`` rows: T(z) IR refresh + the currL
+    convolution outputs per node), the round's analyses (``BCAST``: local
+    frames, estimate synthesis and the z frames of the senders whose
+    consumed chunks are in), late z-frame analyses (``ZAN``) and updates
+    (``UPDATE``) of node subsets, in an order that respects every dependency
+    of the reference's event order: a chunk after the update that wrote its
+    IR source wExt[IRSRC], a z frame after the chunks it covers, an update
+    after the z frames it consumes.  A plain round is CHUNK, BCAST, UPDATE.
+
+    Accepted when in every round all receivers of a sender consume the same
+    stream length (always true at K = 2 and on synchronous clocks).  Returns
+    RoundTables with ``fsTab [R][K][FS_FIELDS]`` (ZEND per consuming round;
+    the chunk fields of the round's first chunk of each node),
+    ``fsEv [nEv][K][4]``, ``fsSteps [nSteps][4]``, ``fsRoundStep [R + 1]``
+    and ``zStreamLen``."""
     if p.broadcastType != 'fewSamples':
         raise ValueError('compile_rounds_fs is for fewSamples broadcasts')
     if not p.efficientSpSBC:
         raise NotImplementedError('fewSamples without efficientSpSBC (one broadcast per L samples) on the device path')
     K, N, Ns = nNodes, p.DFTsize, p.Ns
+    if K > 31:
+        raise NotImplementedError('fewSamples device steps: node masks hold at most 31 nodes')
     Lb = int(p.broadcastLength)
     ts = [np.asarray(t, dtype=np.float64) for t in timeStamps]
     it = np.zeros(K, dtype=np.int64)              # iterations done per node
     lastBc = np.zeros(K)
     lastTD = np.zeros(K)
     streamLen = np.zeros(K, dtype=np.int64)
-    lastBcRound = np.full(K, -1, dtype=np.int64)  # device round of each node's last broadcast
     buf = np.zeros((K, K), dtype=np.int64)
-    bcRec = {}                                    # (r, k) -> [bcEnd, len, pos, irSrc]
+    chunks = [[] for _ in range(K)]               # per node, in order: [bcEnd, len, pos, irSrc]
     zEnd = {}                                     # (r, q) -> stream length consumed
     up = [[] for _ in range(K)]
     solve = [[] for _ in range(K)]
@@ -350,8 +370,6 @@ def compile_rounds_fs(events, fs, p, nNodes: int, timeStamps, M) -> RoundTables:
             k = int(k)
             if typ == 'bc':
                 r = int(it[k])
-                if (r, k) in bcRec:
-                    raise NotImplementedError(f'node {k} broadcasts twice in iteration {r}')
                 irSrc = -1
                 if np.abs(ev.t - lastTD[k]) >= p.upTDfilterEvery:
                     if not (p.noFusionAtSingleSensorNodes and M[k] == 1):
@@ -363,9 +381,8 @@ def compile_rounds_fs(events, fs, p, nNodes: int, timeStamps, M) -> RoundTables:
                 lastBc[k] = ev.t
                 if currL > N:
                     raise NotImplementedError(f'broadcast chunk of {currL} > N samples')
-                bcRec[(r, k)] = [int(np.floor(ev.t * fs[k])), currL, int(streamLen[k]), irSrc]
+                chunks[k].append([int(np.floor(ev.t * fs[k])), currL, int(streamLen[k]), irSrc])
                 streamLen[k] += currL
-                lastBcRound[k] = r
                 for q in range(K):
                     if q != k:
                         buf[q, k] += currL
@@ -385,8 +402,6 @@ def compile_rounds_fs(events, fs, p, nNodes: int, timeStamps, M) -> RoundTables:
                         if Bq > N:
                             raise NotImplementedError('more than N samples received between two updates')
                         fr[q] = 0 if Bq == Ns else (-(Ns - Bq) if Bq < Ns else (Bq - Ns))
-                    if lastBcRound[q] > r:
-                        raise NotImplementedError(f'node {k} update {r} consumes a broadcast of a later round')
                     if (r, q) in zEnd and zEnd[(r, q)] != streamLen[q]:
                         raise NotImplementedError('receivers of one sender consume different stream lengths')
                     zEnd[(r, q)] = int(streamLen[q])
@@ -396,19 +411,17 @@ def compile_rounds_fs(events, fs, p, nNodes: int, timeStamps, M) -> RoundTables:
     R = min(len(u) for u in up)
     if R < 1:
         raise ValueError('signal too short for one DANSE round')
-    tab = np.zeros((R, K, FS_FIELDS), dtype=np.int32)
-    tab[:, :, FS_IRSRC] = -1
-    for (r, k), (e, ln, pos, src) in bcRec.items():
-        if r < R:
-            tab[r, k, FS_BCEND], tab[r, k, FS_LEN], tab[r, k, FS_POS], tab[r, k, FS_IRSRC] = e, ln, pos, src
-    for (r, q), z in zEnd.items():
-        if r < R:
-            tab[r, q, FS_ZEND] = z
-    # senders nobody consumed in a round keep the previous frame end
+    zTab = np.zeros((R, K), dtype=np.int64)
     for r in range(R):
         for q in range(K):
-            if (r, q) not in zEnd:
-                tab[r, q, FS_ZEND] = tab[r - 1, q, FS_ZEND] if r > 0 else 0
+            # senders nobody consumed in a round keep the previous frame end
+            zTab[r, q] = zEnd.get((r, q), zTab[r - 1, q] if r > 0 else 0)
+    steps, evRows, roundStep, first = _fs_steps(chunks, zTab, K, R)
+    tab = np.zeros((R, K, FS_FIELDS), dtype=np.int32)
+    tab[:, :, FS_IRSRC] = -1
+    for (r, k), (e, ln, pos, src) in first.items():
+        tab[r, k, FS_BCEND], tab[r, k, FS_LEN], tab[r, k, FS_POS], tab[r, k, FS_IRSRC] = e, ln, pos, src
+    tab[:, :, FS_ZEND] = zTab
     upEnd = np.array([u[:R] for u in up], dtype=np.int64).T
     # the broadcast kernel's phase 1 analyses "bcEnd" into the spectrum slot of
     # the next round's local frame: point it at upEnd[r + 1]
@@ -420,5 +433,84 @@ def compile_rounds_fs(events, fs, p, nNodes: int, timeStamps, M) -> RoundTables:
     t = np.array([x[:R] for x in tUp], dtype=np.float64).T
     rt = RoundTables(bcEnd, upEnd, doSolve, R, t, np.zeros((R, K, K), np.uint8), flags, sync)
     rt.fsTab = tab
+    rt.fsEv = evRows
+    rt.fsSteps = steps
+    rt.fsRoundStep = roundStep
+    rt.fsChunks = [np.array(c, dtype=np.int64).reshape(-1, 4) for c in chunks]
     rt.zStreamLen = int(max(1, streamLen.max()))
     return rt
+
+
+def _fs_steps(chunks, zTab, K, R):
+    """List-schedules one round at a time (see ``compile_rounds_fs``).
+
+    chunks[q]: node q's chunk events in stream order; zTab[r, q]: the stream
+    length the round-r receivers of q consume.  Returns (steps [n][4] int32,
+    chunk rows [nEv][K][4] int32, first step of each round [R + 1], {(r, k):
+    the first chunk row of node k appended in round r})."""
+    done = np.zeros(K, dtype=np.int64)     # updates done per node (wExt[done] is the newest)
+    nxt = np.zeros(K, dtype=np.int64)      # next chunk event per node
+    steps, rows, roundStep, first = [], [], [], {}
+    full = (1 << K) - 1
+    for r in range(R):
+        roundStep.append(len(steps))
+        pend = set(range(K))
+        zdone = set()
+        bcast = False
+        while pend:
+            progress = False
+            # chunk steps: each node's next needed chunk (stream position below
+            # what round r consumes) whose IR source wExt[IRSRC] is written
+            while True:
+                row = np.zeros((K, 4), dtype=np.int64)
+                row[:, 3] = -1
+                mask = 0
+                for q in range(K):
+                    c = chunks[q]
+                    if nxt[q] < len(c) and c[nxt[q]][2] < zTab[r, q] and c[nxt[q]][3] <= done[q]:
+                        row[q] = c[nxt[q]]
+                        first.setdefault((r, q), tuple(c[nxt[q]]))
+                        nxt[q] += 1
+                        mask |= 1 << q
+                if not mask:
+                    break
+                steps.append((FS_STEP_CHUNK, r, mask, len(rows)))
+                rows.append(row)
+                progress = True
+            # z frames whose chunks are all in
+            ready = 0
+            for q in range(K):
+                if q in zdone:
+                    continue
+                c = chunks[q]
+                if nxt[q] >= len(c) or c[nxt[q]][2] >= zTab[r, q]:
+                    ready |= 1 << q
+                    zdone.add(q)
+            if not bcast:
+                steps.append((FS_STEP_BCAST, r, ready, -1))
+                bcast = True
+                progress = True
+            elif ready:
+                steps.append((FS_STEP_ZAN, r, ready, -1))
+                progress = True
+            # updates whose senders' z frames are analysed
+            umask = 0
+            for k in sorted(pend):
+                if all(q in zdone for q in range(K) if q != k):
+                    umask |= 1 << k
+            if umask:
+                steps.append((FS_STEP_UPDATE, r, umask, -1))
+                for k in range(K):
+                    if (umask >> k) & 1:
+                        pend.discard(k)
+                        done[k] = r + 1
+                progress = True
+            if not progress:
+                raise NotImplementedError(f'fewSamples round {r}: no order of chunks, z frames and updates '
+                                          'satisfies the event dependencies')
+    roundStep.append(len(steps))
+    st = np.array(steps, dtype=np.int32).reshape(-1, 4)
+    ev = np.array(rows, dtype=np.int32).reshape(-1, K, 4)
+    # (every update step of a plain round covers all nodes)
+    assert full > 0
+    return st, ev, np.array(roundStep, dtype=np.int32), first

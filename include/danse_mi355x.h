@@ -132,6 +132,23 @@ typedef struct danse_cfg {
    * [F][D][D] SCM storage) instead of one bin per lane: 16x the wavefronts,
    * for one or a few WASNs per GPU.  0 = one bin per lane (throughput).   */
   int32_t smallDGrid;
+  /* fewSamples device steps (with fsTab): fsEv [nFsEv][K][DANSE_FS_FIELDS]
+   * chunk rows (BCEND, LEN, POS, IRSRC; ZEND unused; LEN 0 and IRSRC -1 for
+   * nodes without a chunk in that step), fsSteps [nFsSteps][DANSE_FS_STEP_
+   * FIELDS] in execution order, round r's steps contiguous and in round
+   * order.  NULL = one CHUNK (fsTab row r), BCAST, UPDATE per round.       */
+  const int32_t* fsEv;
+  int32_t nFsEv;
+  const int32_t* fsSteps;
+  int32_t nFsSteps;
+  /* fewSamples with centralised / SSBC estimates under SRO clocks: 1 = the
+   * centralised buffers receive each chunk's raw samples (the last currL of
+   * the broadcast frame, pre_fill_buffers_centralised, d_classes.py:
+   * 1162-1250) into per-channel streams with the z streams' positions, and
+   * the receivers' raw frame of sender q is stream[cEnd - N, cEnd) -- the
+   * frame ends floor(t fs) of consecutive chunks may overlap or skip a
+   * sample, so the stream is not a slice of y.                           */
+  int32_t rawStreams;
 } danse_cfg;
 
 typedef struct danse_engine danse_engine;
@@ -223,7 +240,15 @@ int danse_engine_cond(danse_engine* eng, double* dst, size_t bytes);
  * spectra between them).  bcast(r) also synthesises the estimates of r-1. */
 int danse_engine_bcast(danse_engine* eng, int32_t r, void* stream);
 int danse_engine_update(danse_engine* eng, int32_t r, void* stream);
-int danse_engine_finish(danse_engine* eng, void* stream);   /* synthesis of the last round */
+int danse_engine_finish(danse_engine* eng, void* stream);
+/* fewSamples engines: steps [s0, s1) of the compiled step list (danse_cfg.
+ * fsSteps; round r's steps are contiguous), un-graphed and without the
+ * speculative gate checks: the exact start gate of a round whose updates run
+ * as several steps decides each node right before its own update step
+ * (check_covariance_matrices, d_classes.py:1430-1540).  danse_engine_bcast /
+ * _update of such an engine run round r's steps before / from its first
+ * update step.                                                            */
+int danse_engine_run_steps(danse_engine* eng, int32_t s0, int32_t s1, void* stream);   /* synthesis of the last round */
 
 /* Device pointer + byte size of the fused-signal spectra buffer [2][K][S][F]
  * complex: round r writes slot r & 1 (node-major within a slot, so that a
@@ -445,6 +470,15 @@ typedef struct danse_scene_cfg {
 const char* danse_scene_last_error(void);
 int danse_scene_generate(const danse_scene_cfg* cfg, float* data, float* cleanspeech, float* cleannoise, uint8_t* vad,
                          void* stream);
+/* The generator's convolution and VAD kernels on injected rows (device
+ * pointers): out[r] = (x[r] * h[r])[:T] (the wet signals of build_wasn,
+ * sig.fftconvolve(xdry, rir)[:T], siggen/utils.py:867-872) and, if vad is
+ * not NULL, vad[r] = oracleVAD(out[r], vadWinLength, max(out[r]^2) /
+ * 10^(dB/10), fs) (siggen/utils.py:896-939,1079-1151).  x, out [rows][T]
+ * float, h [rows][nIR] float, vad [rows][T] uint8.  Synchronises stream. */
+int danse_scene_convolve_vad(const float* x, const float* h, int32_t rows, int32_t T, int32_t nIR, float* out,
+                             double vadWinLength, double fs, double vadEnergyDecrease_dB, uint8_t* vad,
+                             void* stream);
 
 /* ---- T(z) few-samples compression (broadcastType 'fewSamples').
  * danse_tz_create: analysis window h, synthesis window f (N floats, host), the

@@ -58,4 +58,17 @@ enum danse_fs_field {
   DANSE_FS_FIELDS = 5
 };
 
+/* One fewSamples device step (danse_cfg.fsSteps, DANSE_FS_STEP_FIELDS int32):
+ * type, round r, node mask (bit k: node k), chunk row (fsEv row of a CHUNK
+ * step, else -1).  A round is a list of steps that keeps every dependency of
+ * the reference's event order (danse_amd/scheduler.py compile_rounds_fs).   */
+enum danse_fs_step {
+  DANSE_FS_STEP_CHUNK = 0,   /* T(z) IR refresh + currL chunk append of the row's nodes */
+  DANSE_FS_STEP_BCAST = 1,   /* round r's analyses, estimate synthesis of round r-1 and
+                                the z frames of the masked senders                     */
+  DANSE_FS_STEP_ZAN = 2,     /* z frames of the masked senders only                   */
+  DANSE_FS_STEP_UPDATE = 3,  /* update r of the masked nodes                          */
+  DANSE_FS_STEP_FIELDS = 4
+};
+
 #endif /* DANSE_MI355X_DEFS_H */

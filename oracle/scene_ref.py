@@ -11,7 +11,9 @@ the reference's siggen (trueRoom false, signalType random):
   device (the reference's resample_for_sro, siggen/utils.py:1579-1622, uses
   resampy, absent offline -- this resampler is parity unpinned against it);
 * white self-noise per sensor (siggen/utils.py:1414-1431);
-* energy VAD of each node's mic-0 wet speech (siggen/utils.py:1079-1133).
+* energy VAD of each node's mic-0 wet speech (oracleVAD, siggen/utils.py:
+  1079-1151), pinned with the wet-signal convolution to the reference's own
+  get_vad on injected inputs (tests/golden/scene_vad_conv.npz).
 
 The device accumulates the convolution in float32 and rounds every output
 to float32; tests compare at a relative tolerance.
@@ -77,13 +79,22 @@ def resample_sro(x, eps, half=32, roll=0.95, beta=8.0):
 
 
 def energy_vad(x, fs, tw, dB):
+    """oracleVAD + compute_VAD (siggen/utils.py:1079-1151) with the
+    threshold of get_or_load_vad (utils.py:921): sample i is active when the
+    MEAN energy of x[max(i - nw//2, 0) : min(i + nw//2, n)] exceeds
+    max(x^2) / 10^(dB/10), nw = int(tw fs)."""
     thr = np.max(x ** 2) / 10 ** (dB / 10)
     nw = max(int(tw * fs), 1)
     c = np.concatenate(([0.0], np.cumsum(x ** 2)))
     idx = np.arange(len(x))
     b = np.maximum(idx - nw // 2, 0)
     e = np.minimum(idx + nw // 2, len(x))
-    return (c[e] - c[b] > thr).astype(np.uint8)
+    return ((c[e] - c[b]) / (e - b) > thr).astype(np.uint8)
+
+
+def wet_signal(x, h):
+    """sig.fftconvolve(xdry, rir)[:N] (get_vad, siggen/utils.py:867-872)."""
+    return fftconvolve(x, h)[:len(x)]
 
 
 def generate(M, S, T, nIR, seed, fs=16000.0, snr=5.0, selfnoiseSNR=15.0, pauseDuration=0.5, pauseSpacing=0.5,
@@ -109,8 +120,8 @@ def generate(M, S, T, nIR, seed, fs=16000.0, snr=5.0, selfnoiseSNR=15.0, pauseDu
         for c, (k, m) in enumerate(chan):
             hS = (0.5 * urand(stream_key(sd, ST_IRS, k, m), nIR)).astype(np.float32).astype(np.float64)
             hN = (0.5 * urand(stream_key(sd, ST_IRN, k, m), nIR)).astype(np.float32).astype(np.float64)
-            wS[c] = fftconvolve(d, hS)[:T]
-            wN[c] = fftconvolve(n, hN)[:T]
+            wS[c] = wet_signal(d, hS)
+            wN[c] = wet_signal(n, hN)
         gN = 10 ** (-(snr - 10 * np.log10(np.mean(wS[0] ** 2) / np.mean(wN[0] ** 2))) / 20)
         for k in range(K):
             vad[s, k] = energy_vad(wS[base[k]], fs, vadWinLength, vadEnergyDecrease_dB)

@@ -107,6 +107,17 @@ ONLINE_CASES = [
                   computeCentralised=True)),
     dict(name='online_E_fs_L1_seq', M=[2, 3, 1], dur=2.5, seed=12,
          danse=_d(BATTERY, nodeUpdating='seq', broadcastType='fewSamples', broadcastLength=1)),
+    # the E battery's remaining broadcast lengths under SROs [0, 200] ppm
+    # (tests/battery20230919_perf_asfctofL.py:21-24,60-104): L < 32 puts the
+    # faster node's chunk after its own update (with the next iteration's IR
+    # at the refresh timer), L = Ns broadcasts twice in iteration 0
+    # (scheduler.compile_rounds_fs step lists)
+    *[dict(name=f'online_E_fs_L{L}_sro_{tag}', M=[2, 3], dur=dur, seed=seed, sros=[0, 200],
+           danse=_d(BATTERY, nodeUpdating='asy', broadcastType='fewSamples', broadcastLength=L,
+                    compensateSROs=comp, includeFSDflags=comp, estimateSROs='Oracle', computeLocal=True,
+                    computeCentralised=True, computeSingleSensorBroadcast=not comp))
+      for L, dur, seed in ((1, 2.5, 20), (16, 6.0, 21), (512, 2.5, 22))
+      for tag, comp in (('nocomp', False), ('comp', True))],
 ]
 
 BATCH_CASES = [
@@ -337,3 +348,23 @@ def stoi_inputs(case):
 # per node, from sample startIdx to the end
 E2E_METRICS_CASE = dict(name='metrics_e2e_k3', M=[2, 2, 2], dur=4.0, seed=31, startIdx=16000,
                         danse=_d(BATTERY, nodeUpdating='asy', computeLocal=True, computeCentralised=True))
+
+
+# The device scene generator's convolution and VAD (csrc/scene.hip) against
+# the reference's own get_vad (siggen/utils.py:834-893: wet signals by
+# sig.fftconvolve(xdry, rir)[:N], oracleVAD on each node's reference sensor,
+# utils.py:896-939,1079-1151) on injected inputs: a paused uniform dry source
+# and uniform random IRs (float32 values), stored in the fixture.
+SCENE_CASES = [dict(name='scene_vad_conv', M=[2, 1, 2], T=32000, nIR=3200, seed=5, fs=16000.0,
+                    vadWinLength=0.04, vadEnergyDecrease_dB=40.0)]
+
+
+def scene_inputs(case):
+    """(xdry [T], IRs [sum M][nIR]) as float32-valued float64 arrays."""
+    rng = np.random.default_rng(case['seed'])
+    T, fs = case['T'], case['fs']
+    x = rng.uniform(-1, 1, T).astype(np.float32).astype(np.float64)
+    t = np.arange(T) / fs
+    x[np.fmod(t, 1.0) >= 0.5] = 0.0
+    h = (0.5 * rng.uniform(-1, 1, (sum(case['M']), case['nIR']))).astype(np.float32).astype(np.float64)
+    return x, h

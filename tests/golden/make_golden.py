@@ -26,6 +26,7 @@ from golden_cases import ONLINE_CASES, BATCH_CASES, SRO_EVENT_CASES, KAT_CASES, 
 from golden_cases import DXCP_CASES, dxcp_inputs, TZ_CASES, tz_inputs, CLDXCP_CASES, cldxcp_acs  # noqa: E402
 from golden_cases import METRIC_CASES, metric_inputs, GETMETRICS_CASE, get_metrics_inputs  # noqa: E402
 from golden_cases import FIELD_CASES, FIELD_STFT_BIN_STEP, STOI_CASES, stoi_inputs, E2E_METRICS_CASE  # noqa: E402
+from golden_cases import SCENE_CASES, scene_inputs  # noqa: E402
 
 
 def _run_online(ns, case):
@@ -269,6 +270,34 @@ def _run_e2e_metrics(ns, case):
     return out
 
 
+def _run_scene(ns, case):
+    """The reference's get_vad (siggen/utils.py:834-893) on injected inputs,
+    and oracleVAD on the float32-rounded wet reference-sensor signals."""
+    import tempfile
+    import siggen.utils as sgu
+    x, h = scene_inputs(case)
+    M = case['M']
+    p = ns.sgc.WASNparameters(trueRoom=False, signalType='random', fs=case['fs'], nSensorPerNode=list(M),
+                              SROperNode=np.zeros(len(M)),
+                              topologyParams=ns.sgc.TopologyParameters(topologyType='fully-connected', seed=12348))
+    p.VADwinLength = case['vadWinLength']
+    p.VADenergyDecrease_dB = case['vadEnergyDecrease_dB']
+    p.VADenergyFactor = 10 ** (p.VADenergyDecrease_dB / 10)
+    p.enableVADloadFromFile = False
+    p.vadFilesFolder = tempfile.mkdtemp(prefix='danse_vad_')
+    rirs, c = [], 0
+    for m in M:
+        rirs.append([[h[c + i]] for i in range(m)])
+        c += m
+    vad, wet = sgu.get_vad(rirs, x[:, None], p)
+    wetAll = np.concatenate(wet, axis=0)                  # [sum M][T]
+    ref = np.cumsum([0] + list(M))[:-1]
+    vad32 = np.stack([sgu.oracleVAD(wetAll[b].astype(np.float32).astype(np.float64), tw=p.VADwinLength,
+                                    thrs=np.amax(wetAll[b].astype(np.float32).astype(np.float64) ** 2) /
+                                    p.VADenergyFactor, Fs=p.fs)[0] for b in ref])
+    return {'x': x, 'h': h, 'wet': wetAll, 'vad': vad[:, :, 0].T.astype(np.uint8), 'vad32': vad32.astype(np.uint8)}
+
+
 def main():
     ns = H.load()
     only = sys.argv[1:]
@@ -284,6 +313,7 @@ def main():
            [('metrics', GETMETRICS_CASE, _run_get_metrics)] + \
            [('stoi', c, _run_stoi) for c in STOI_CASES] + \
            [('metrics', E2E_METRICS_CASE, _run_e2e_metrics)] + \
+           [('scene', c, _run_scene) for c in SCENE_CASES] + \
            [('fields', dict(name=f'fields_{c}', src=c), lambda ns, c: _run_fields(ns, c['src'])) for c in FIELD_CASES]
     for kind, case, fn in jobs:
         name = case['name']

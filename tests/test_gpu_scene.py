@@ -62,3 +62,30 @@ def test_scene_generator_snr_and_engine_input():
     b.close()
     for s in range(2):
         assert np.array_equal(oa[s].d, ob[s].d)
+
+
+def test_scene_conv_vad_vs_reference(golden_dir):
+    """The device generator's convolution and VAD kernels on the injected
+    inputs of the reference fixture (get_vad, siggen/utils.py:834-893,
+    1079-1151): wet signals within float32 accumulation error of the
+    reference's float64 fftconvolve; the VAD kernel on the float32-rounded
+    reference wet signals equals the reference's oracleVAD of those signals
+    exactly; the VAD of the device's own wet signals differs at most at a
+    handful of threshold-borderline samples."""
+    from danse_amd.scene import convolve_vad
+    from golden_cases import SCENE_CASES
+    case = SCENE_CASES[0]
+    g = dict(np.load(golden_dir / f"{case['name']}.npz", allow_pickle=False))
+    x, h, wet = g['x'], g['h'], g['wet']
+    rows = h.shape[0]
+    kw = dict(fs=case['fs'], vadWinLength=case['vadWinLength'], vadEnergyDecrease_dB=case['vadEnergyDecrease_dB'])
+    out, vad = convolve_vad(np.repeat(x[None], rows, axis=0), h, **kw)
+    err = np.max(np.abs(out - wet)) / np.max(np.abs(wet))
+    ref = np.cumsum([0] + list(case['M']))[:-1]
+    mism = float(np.mean(vad[ref] != g['vad']))
+    # the VAD kernel alone: identity IR on the float32-rounded reference signals
+    _, v32 = convolve_vad(wet[ref].astype(np.float32), np.ones((len(ref), 1), np.float32), **kw)
+    print('wet rel err', err, 'VAD mismatch (device wet)', mism, 'active', float(g['vad'].mean()))
+    assert err <= 2e-6, err
+    assert np.array_equal(v32, g['vad32'])
+    assert mism <= 1e-3, mism

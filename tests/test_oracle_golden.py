@@ -4,7 +4,7 @@ import numpy as np
 import pytest
 
 from golden_cases import ONLINE_CASES, BATCH_CASES, SRO_EVENT_CASES, KAT_CASES, DXCP_CASES, TZ_CASES, kat_inputs
-from golden_cases import BESTPERF_CASES
+from golden_cases import BESTPERF_CASES, SCENE_CASES, scene_inputs
 from danse_amd.scene import scene_digest
 from danse_amd.scheduler import initialize_events
 from oracle import danse_ref_cpu as O
@@ -242,3 +242,25 @@ def test_gevd_pool_bit_identical(golden_dir):
     finally:
         O.set_workers(0)
     assert np.array_equal(serial, pooled)
+
+
+@pytest.mark.parametrize('case', SCENE_CASES, ids=[c['name'] for c in SCENE_CASES])
+def test_scene_vad_conv_vs_reference(case, golden_dir):
+    """oracle/scene_ref.py (the device scene generator's checker) against the
+    reference's get_vad on injected inputs: wet signals (fftconvolve) to
+    1e-12, the per-sample VAD of each node's reference sensor exactly, on the
+    float64 wet signals and on their float32 rounding."""
+    from oracle import scene_ref as SR
+    g = _load(golden_dir, case['name'])
+    x, h = scene_inputs(case)
+    assert np.array_equal(x, g['x']) and np.array_equal(h, g['h'])
+    wet = np.stack([SR.wet_signal(x, hc) for hc in h])
+    assert rel_err(wet, g['wet']) < 1e-12
+    ref = np.cumsum([0] + list(case['M']))[:-1]
+    for j, b in enumerate(ref):
+        v = SR.energy_vad(g['wet'][b], case['fs'], case['vadWinLength'], case['vadEnergyDecrease_dB'])
+        assert np.array_equal(v, g['vad'][j]), j
+        w32 = g['wet'][b].astype(np.float32).astype(np.float64)
+        v32 = SR.energy_vad(w32, case['fs'], case['vadWinLength'], case['vadEnergyDecrease_dB'])
+        assert np.array_equal(v32, g['vad32'][j]), j
+        assert 0.05 < v.mean() < 0.95
