@@ -95,6 +95,8 @@ SIGNATURES = {
     'danse_engine_dxcp_record': (_c_i32, [ctypes.c_void_p, _c_i32]),
     'danse_mi355x_fill': (_c_i32, [ctypes.c_void_p, _c_i32, ctypes.c_size_t, ctypes.c_void_p]),
     'danse_engine_run_steps': (_c_i32, [ctypes.c_void_p, _c_i32, _c_i32, ctypes.c_void_p]),
+    'danse_engine_set_zchunk': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p]),
+    'danse_engine_unpack_zchunk': (_c_i32, [ctypes.c_void_p, _c_i32, ctypes.c_void_p]),
     'danse_engine_dxcp_recorded': (_c_i32, [ctypes.c_void_p, ctypes.POINTER(_c_i32), ctypes.POINTER(_c_i32),
                                             ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t]),
     'danse_engine_resident_trace': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_size_t)]),

@@ -63,6 +63,10 @@ struct BcastArgs {
   // analyses, no estimate synthesis)
   unsigned zMask;
   int zOnly;
+  // node-sharded DXCP (danse_engine_set_zchunk): the round's new z samples of
+  // every owned node also go to zChunk [K][S][Ns] (node-major: a rank's block
+  // is one all-gather chunk), for the other ranks' estimators
+  float* zChunk;
 };
 
 // y[(frame end - N) .. frame end) * win, zero before sample 0 -> buf (complex, imag 0)
@@ -231,6 +235,7 @@ __global__ void __launch_bounds__(256) bcast_kernel(const BcastArgs a) {
       const int n = l + 64 * j;
       zpv[n] = zq[n];
       if (n < Ns) zs[(long long)r * Ns + n] = zq[n];
+      if (n < Ns && a.zChunk) a.zChunk[((long long)k * a.S + s) * Ns + n] = zq[n];
     }
     // ---- z frame the receivers consume at round r: stream samples [(r+1)Ns - N, (r+1)Ns)
 #pragma unroll

@@ -97,6 +97,8 @@ struct danse_engine {
   cd *cdRing = nullptr, *cdAvg = nullptr;
   double *cdPhase = nullptr, *cdEst = nullptr, *cdRes = nullptr;
   long long liStride = 0;
+  cf* vCache = nullptr;      // lane-grid GEVD classes: eigenvector of C per bin (warm start)
+  long long vStride = 0;
   int scmPerBin = 0;   // dScm0 holds [F][D][D] per family-node (else [D][D])
   FamNode* dFnAll = nullptr;
   long long *dInitW0Off = nullptr, *dInitScmOff = nullptr, *dExtSrcOff = nullptr, *dTgtOff = nullptr;
@@ -109,6 +111,7 @@ struct danse_engine {
   std::vector<int> fsEv, fsSteps, fsRoundStep;
   int* dFsEv = nullptr;
   float* rawStream = nullptr;      // [S][MT][zLen] (cfg.rawStreams)
+  float* zChunk = nullptr;         // node-sharded DXCP: [K][S][Ns] exchange buffer (borrowed)
   float *wIR = nullptr, *dSn = nullptr;
   // DXCP-PhaT SRO estimation in the loop (cfg.dxcp, an extension: the
   // reference's integration raises, quirk Q12): one estimator per (scene,
@@ -377,6 +380,7 @@ int danse_engine_reset(danse_engine* eng, void* stream) {
   HIPCHK(fill_async(eng->dhat, 0, (size_t)kMaxFam * S * K * R * F * sizeof(cf), st));
   HIPCHK(fill_async(eng->d, 0, (size_t)kMaxFam * S * K * eng->T * sizeof(float), st));
   HIPCHK(fill_async(eng->diag, 0, (size_t)S * K * kMaxFam * sizeof(int), st));
+  if (eng->vCache) HIPCHK(fill_async(eng->vCache, 0, (size_t)S * eng->vStride * sizeof(cf), st));
   const int nFN = (int)eng->fns.size();
   hipLaunchKernelGGL(reset_fam_kernel, dim3(64, S * nFN), dim3(256), 0, st, eng->dFnAll, nFN, eng->dInitW0Off,
                      eng->dInitScmOff, eng->dW0, eng->dScm0, eng->wHist, eng->wStride, eng->Ryy, eng->Rnn,
@@ -513,7 +517,9 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
   // ---- family-node table (owned nodes), channel lists; with cEnd the other
   // nodes' channels of the centralised / SSBC vectors are raw-frame codes
   // (MT + K + channel, kernels.hpp load_y)
-  long long scmOff = 0, wOff = 0, liOff = 0;
+  long long scmOff = 0, wOff = 0, liOff = 0, vOff = 0;
+  // warm-started rank-1 Lanczos on the lane-grid classes (DANSE_NO_WARM=1: off)
+  const bool warm = c->gevd && c->rank == 1 && !std::getenv("DANSE_NO_WARM");
   const int rawBase = mt + K;
   const long long histW = c->keepHistory ? (long long)R + 1 : 2;
   for (int fam = 0; fam < kMaxFam; ++fam) {
@@ -556,12 +562,18 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
                                                     class_split(class_dmax(fn.D)) ? class_split_li_record() : 0);
       else if (c->gevd && gridSmall) liOff += (long long)F * class_li_record(16);
       else if (c->gevd && class_grid(class_dmax(fn.D)) > 0) liOff += (long long)F * class_li_record(class_dmax(fn.D));
+      fn.vOff = -1;
+      if (warm && !fn.packed && (gridSmall || class_grid(class_dmax(fn.D)) > 0)) {
+        fn.vOff = vOff;
+        vOff += (long long)F * (gridSmall ? 16 : class_dmax(fn.D));
+      }
       eng->fns.push_back(fn);
     }
   }
   eng->scmStride = scmOff;
   eng->wStride = wOff;
   eng->liStride = liOff;
+  eng->vStride = vOff;
   eng->wExtNodeOff.assign(K, 0);
   long long eo = 0, to = 0;
   for (int k = 0; k < K; ++k) {
@@ -717,6 +729,7 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
   HIPCHK(dalloc(&eng->d, (size_t)kMaxFam * S * K * c->T));
   HIPCHK(dalloc(&eng->diag, (size_t)S * K * kMaxFam));
   if (eng->liStride > 0) HIPCHK(dalloc(&eng->liCache, (size_t)S * eng->liStride));
+  if (eng->vStride > 0) HIPCHK(dalloc(&eng->vCache, (size_t)S * eng->vStride));
   if (c->dxcp) {
     if (c->cohDrift) return fail(eng, "DXCP-PhaT and CohDrift estimation are exclusive");
     if (c->fsTab) return fail(eng, "DXCP-PhaT estimation runs on wholeChunk broadcasts");
@@ -847,7 +860,7 @@ void danse_engine_destroy(danse_engine* eng) {
                   eng->dxEst, eng->resYB, eng->resYU, eng->resZall, eng->resZhat, eng->resRyyG, eng->resRnnG,
                   eng->resUFlag, eng->resZFlag, eng->resGateRound, eng->resDanseFni, eng->resErr, eng->resFams,
                   eng->resFrames, eng->resChanNode, eng->resTrace, eng->condHist, eng->dxRecFrames,
-                  eng->dxRecOut, eng->dFsEv, eng->rawStream};
+                  eng->dxRecOut, eng->dFsEv, eng->rawStream, eng->vCache};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (eng->dx) danse_dxcp_destroy(eng->dx);
@@ -877,7 +890,7 @@ static BcastArgs make_bcast(danse_engine* e, int r, int synth, int bc) {
   a.dbg = e->bcastAblate;
   a.zLen = e->zLen;
   a.fsTab = e->dFsTab;
-  a.cEnd = e->dCEnd; a.Cspec = e->Cspec; a.rawStream = e->rawStream;
+  a.cEnd = e->dCEnd; a.Cspec = e->Cspec; a.rawStream = e->rawStream; a.zChunk = e->zChunk;
   a.zMask = ~0u;
   a.zOnly = 0;
   return a;
@@ -894,6 +907,7 @@ static UpdateArgs make_update(danse_engine* e, int r) {
   a.wExtTarget = e->wExtTarget; a.tgtStride = e->tgtStride; a.dhat = e->dhat; a.beta = e->dBeta;
   a.betaExt = e->dBetaExt; a.alphaExt = e->alphaExt; a.gevd = e->gevd; a.rank = e->rank; a.diag = e->diag;
   a.liCache = e->liCache; a.liStride = e->liStride;
+  a.vCache = e->vCache; a.vStride = e->vStride;
   a.cdPhase = e->cdPhase;
   a.Cspec = e->Cspec; a.chanNode = e->dChanNode; a.cPhase = e->dCPhase;
   a.nodeMask = ~0u;
@@ -1393,6 +1407,45 @@ int danse_mi355x_fill(void* ptr, int32_t value, size_t bytes, void* stream) {
   danse_engine* eng = nullptr;   // (HIPCHK's error slot)
   if (!ptr && bytes) return fail(eng, "null pointer");
   HIPCHK(fill_async(ptr, value, bytes, (hipStream_t)stream));
+  return 0;
+}
+
+// node-sharded DXCP: the gathered z chunks of round r into the streams of
+// the nodes this engine does not own (the received stream of every sender)
+__global__ void zchunk_unpack_kernel(const float* __restrict__ zc, float* __restrict__ zStream, int S, int K, int k0,
+                                     int k1, int Ns, int zLen, int r) {
+  const long long n = (long long)S * K * Ns;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+    const int i = (int)(e % Ns);
+    const int s = (int)((e / Ns) % S);
+    const int k = (int)(e / ((long long)Ns * S));
+    if (k >= k0 && k < k1) continue;
+    zStream[((long long)s * K + k) * zLen + (long long)r * Ns + i] = zc[e];
+  }
+}
+
+int danse_engine_set_zchunk(danse_engine* eng, void* ptr) {
+  if (!eng) return fail(eng, "null engine");
+  if (eng->dFsTab) return fail(eng, "z-chunk exchange is for wholeChunk broadcasts");
+  HIPCHK(hipSetDevice(eng->dev));
+  eng->zChunk = (float*)ptr;
+  if (eng->graphExec) {
+    (void)hipGraphExecDestroy(eng->graphExec);
+    eng->graphExec = nullptr;
+    eng->graphR0 = eng->graphR1 = -1;
+  }
+  return 0;
+}
+
+int danse_engine_unpack_zchunk(danse_engine* eng, int32_t r, void* stream) {
+  if (!eng || !eng->zChunk) return fail(eng, "no z-chunk buffer (danse_engine_set_zchunk)");
+  if (r < 0 || r >= eng->R) return fail(eng, "round out of range");
+  HIPCHK(hipSetDevice(eng->dev));
+  const long long n = (long long)eng->S * eng->K * eng->Ns;
+  hipLaunchKernelGGL(zchunk_unpack_kernel, dim3((unsigned)std::min<long long>((n + 255) / 256, 4096)), dim3(256), 0,
+                     (hipStream_t)stream, eng->zChunk, eng->zStream, eng->S, eng->K, eng->k0, eng->k1, eng->Ns,
+                     eng->zLen, r);
+  HIPCHK(hipGetLastError());
   return 0;
 }
 

@@ -37,6 +37,7 @@ struct FamNode {
   long long wExtOff;  // DANSE only: offset within one scene's wExt-history block
   long long tgtOff;   // DANSE only: offset within one scene's target block
   long long liOff;    // lane classes, GEVD: offset of the factor cache (Li, g) within one scene's block
+  long long vOff;     // lane-grid classes, GEVD: offset of the eigenvector cache (solver2d.hpp lanczos2d), -1 none
 };
 
 struct UpdateArgs {
@@ -91,6 +92,11 @@ struct UpdateArgs {
   // fewSamples step lists (compile_rounds_fs): the nodes this launch updates
   // (bit k: node k); the others are left untouched
   unsigned nodeMask;
+  // lane-grid GEVD classes: per bin the eigenvector of C of the previous
+  // solve ([F][DMAX] per family-node at FamNode.vOff, per scene stride
+  // vStride), the warm start of the rank-1 Lanczos path; null = off
+  cf* vCache;
+  long long vStride;
 };
 
 DANSE_DEV bool node_in(unsigned mask, int k) { return ((mask >> k) & 1u) != 0u; }

@@ -73,6 +73,10 @@ update_kernel_2d(const UpdateArgs a) {
   // and g (solver2d.hpp li_record / li_store2d)
   const bool reuse = solve && li_reusable(a, d, s, opN);
   cf* liC = a.liCache ? a.liCache + (long long)s * a.liStride + d.liOff + (long long)f * li_record<NB, G>() : nullptr;
+  // eigenvector cache of the warm-started rank-1 path (solver2d.hpp lanczos2d)
+  cf* vC = (!PK && SM == 0 && a.vCache && d.vOff >= 0)
+               ? a.vCache + (long long)s * a.vStride + d.vOff + (long long)f * (G * NB)
+               : nullptr;
 
   cf y[V];
   sfor<0, V>([&](auto vc) {
@@ -163,7 +167,7 @@ update_kernel_2d(const UpdateArgs a) {
         A.v[sb][tb] = x;
       });
     });
-    if (solve) gevd2d_filter<NB, RMAX, G>(A, S, li, D, a.rank, w);
+    if (solve) gevd2d_filter<NB, RMAX, G>(A, S, li, D, a.rank, w, vC, fvalid);
   }
 
   const long long wBase = (long long)s * a.wStride + d.wOff;

@@ -721,7 +721,8 @@ DANSE_DEV void tri_eigvec2d(const float* a, const float* ev, float4* fac, float*
 // ---- eigen part, back-transform, x = Li^H v,
 // w = sum_r (1 - 1/lambda_r) x_r (x_r^H Rnn e_ref); w[v] = entry li + L v
 template <int NB, int RMAX, int G = 8>
-DANSE_DEV void eigen2d(LDS2<NB, G>& S, int li, int D, int R, cf (&w)[vpl<NB, G>()]) {
+DANSE_DEV void eigen2d(LDS2<NB, G>& S, int li, int D, int R, cf (&w)[vpl<NB, G>()], cf* vOut = nullptr,
+                       bool store = false) {
   constexpr int DM = G * NB, L = bin_lanes<G>(), V = vpl<NB, G>();
   const int p = li / G, q = li % G;
   float lam[kRMax];
@@ -767,6 +768,13 @@ DANSE_DEV void eigen2d(LDS2<NB, G>& S, int li, int D, int R, cf (&w)[vpl<NB, G>(
       const cf sdot = gsum<L>(sd);
       sfor<0, V>([&](auto vc) { fms_c(vv[decltype(vc)::value], 2.0f * u[decltype(vc)::value], sdot); });
     }
+    if (r == 0 && vOut && store) {
+      // the eigenvector of C: the next frame's Lanczos start (lanczos2d)
+      sfor<0, V>([&](auto vc) {
+        const int i = li + L * decltype(vc)::value;
+        if (i < DM) vOut[i] = (i < D) ? vv[decltype(vc)::value] : cf{0.0f, 0.0f};
+      });
+    }
     cf sg;
     sfor<0, V>([&](auto vc) {
       const cf t = cmul(vv[decltype(vc)::value], gl[decltype(vc)::value]);
@@ -810,12 +818,224 @@ DANSE_DEV void eigen2d(LDS2<NB, G>& S, int li, int D, int R, cf (&w)[vpl<NB, G>(
   });
 }
 
+// ---- warm-started Lanczos for the top eigenpair (rank-1 GEVD) ------------
+// The SCMs move by a factor (1 - beta) ~ 2 % per frame, so the previous
+// frame's eigenvector of C (kept per bin, eigen2d / this function) is a close
+// start: kLz<DM>() Lanczos steps on C (one block matvec each, the vector moved
+// between the row and column layouts through LDS, one reorthogonalisation
+// pass against the stored basis), the top Ritz pair of the small tridiagonal
+// by the multisection / inverse iteration of the full path, and the Lanczos
+// residual |beta_m s_m| as the acceptance test.  Replaces the D-step
+// Householder tridiagonalisation and the D-point eigen part (the bulk of the
+// per-bin instruction count) when it converges; the caller
+// falls back to them otherwise.  Accuracy: the residual bound kLzTol theta is
+// a few float32 roundings of ||C||, the floor the Householder path reaches.
+template <int DM>
+constexpr int kLz() { return (DM - 1) / 2 < 8 ? (DM - 1) / 2 : 8; }
+constexpr float kLzTol = 3.0e-6f;
+
+// true (wave-uniform) if every bin of the wave converged: then vv (lane
+// layout) is the unit eigenvector of C and lam1 its eigenvalue
+template <int NB, int G = 8>
+DANSE_DEV bool lanczos2d(const Blk<NB>& A, LDS2<NB, G>& S, int li, int D, const cf* vIn, cf (&vv)[vpl<NB, G>()],
+                         float& lam1) {
+  constexpr int DM = G * NB, L = bin_lanes<G>(), V = vpl<NB, G>(), M = kLz<DM>();
+  static_assert(M * DM <= DM * (DM - 1) / 2, "the Lanczos basis lives in the reflector space");
+  const int p = li / G, q = li % G;
+  cf* Q = S.U;   // [M][DM] basis vectors (the Householder vectors' space: unused on this path)
+  wsync();       // the congruence's staging reads (S.cz aliases S.qb / S.a) before the writes below
+  // start vector, column layout (entries q + G t), unit norm
+  cf vc[NB];
+  float n0 = 0.0f;
+  sfor<0, NB>([&](auto tc) {
+    constexpr int t = decltype(tc)::value;
+    const int i = q + G * t;
+    vc[t] = (i < D) ? vIn[i] : cf{0.0f, 0.0f};
+    n0 += abs2(vc[t]);
+  });
+  n0 = sumq<G>(n0);
+  bool ok = n0 > 1e-30f && n0 < 1e30f;
+  const float s0 = ok ? frsq(n0) : 0.0f;
+  sfor<0, NB>([&](auto tc) { vc[decltype(tc)::value] = s0 * vc[decltype(tc)::value]; });
+  if (p == 0) sfor<0, NB>([&](auto tc) { Q[q + G * decltype(tc)::value] = vc[decltype(tc)::value]; });
+  cf pv[NB];
+  sfor<0, NB>([&](auto tc) { pv[decltype(tc)::value] = cf{0.0f, 0.0f}; });
+  float bprev = 0.0f, blast = 0.0f;
+  for (int k = 0; k < M; ++k) {
+    // w = C v: row-layout partial sums over the row group, then the column
+    // layout through LDS
+    sfor<0, NB>([&](auto sc) {
+      constexpr int sb = decltype(sc)::value;
+      cf acc = cf{0.0f, 0.0f};
+      sfor<0, NB>([&](auto tc) { pk_fma_c(acc, A.v[sb][decltype(tc)::value], vc[decltype(tc)::value]); });
+      acc = sumq<G>(acc);
+      if (q == 0) S.qb[k & 1][p + G * sb] = acc;
+    });
+    wsync();
+    cf wc[NB];
+    float al = 0.0f;
+    sfor<0, NB>([&](auto tc) {
+      constexpr int t = decltype(tc)::value;
+      wc[t] = S.qb[k & 1][q + G * t];
+      al += vc[t].re * wc[t].re + vc[t].im * wc[t].im;
+    });
+    al = sumq<G>(al);
+    sfor<0, NB>([&](auto tc) {
+      constexpr int t = decltype(tc)::value;
+      wc[t] = wc[t] - al * vc[t] - bprev * pv[t];
+    });
+    // one reorthogonalisation pass against the basis so far
+    for (int j = 0; j <= k; ++j) {
+      cf qj[NB], h = cf{0.0f, 0.0f};
+      sfor<0, NB>([&](auto tc) {
+        constexpr int t = decltype(tc)::value;
+        qj[t] = Q[j * DM + q + G * t];
+        h = h + cmul(qj[t], wc[t]);
+      });
+      h = sumq<G>(h);
+      sfor<0, NB>([&](auto tc) { fms_c(wc[decltype(tc)::value], h, qj[decltype(tc)::value]); });
+    }
+    float nb = 0.0f;
+    sfor<0, NB>([&](auto tc) { nb += abs2(wc[decltype(tc)::value]); });
+    nb = sumq<G>(nb);
+    const float b = fsqrt(nb);
+    if (li == 0) {
+      S.a[k] = al;
+      if (k + 1 < M) {
+        S.e2[k] = nb;
+        S.ev[k] = b;
+      }
+    }
+    // (a breakdown -- an invariant subspace, b ~ 0 -- leaves the remaining
+    // basis vectors zero: the small tridiagonal splits and its top Ritz pair
+    // is exact)
+    const float ib = (b > 1e-20f) ? frcp(b) : 0.0f;
+    sfor<0, NB>([&](auto tc) {
+      constexpr int t = decltype(tc)::value;
+      pv[t] = vc[t];
+      vc[t] = ib * wc[t];
+    });
+    if (k + 1 < M && p == 0) sfor<0, NB>([&](auto tc) { Q[(k + 1) * DM + q + G * decltype(tc)::value] = vc[decltype(tc)::value]; });
+    bprev = b;
+    blast = b;
+    wsync();
+  }
+  // top Ritz pair of the M x M tridiagonal (the full path's eigen routines)
+  float lam[kRMax], tnorm;
+  top_eigvals2d<M, 1, G>(S.a, S.e2, li, M, 1, lam, tnorm);
+  float x[(M + L - 1) / L];
+  tri_eigvec2d<M, G>(S.a, S.ev, S.fac, S.xs, li, M, lam[0], 1.2e-7f * fmaxf(tnorm, 1e-30f), 0,
+                     reinterpret_cast<const float(*)[M]>(S.x), x);
+  if (li < M) S.x[0][li] = x[0];
+  wsync();
+  const float sm = S.x[0][M - 1];
+  // Ritz vector y = sum_k s_k Q_k (column layout), unit norm
+  cf yc[NB];
+  sfor<0, NB>([&](auto tc) { yc[decltype(tc)::value] = cf{0.0f, 0.0f}; });
+  for (int k = 0; k < M; ++k) {
+    const float sk = S.x[0][k];
+    sfor<0, NB>([&](auto tc) {
+      constexpr int t = decltype(tc)::value;
+      yc[t] = yc[t] + sk * Q[k * DM + q + G * t];
+    });
+  }
+  float ny = 0.0f;
+  sfor<0, NB>([&](auto tc) { ny += abs2(yc[decltype(tc)::value]); });
+  ny = sumq<G>(ny);
+  const float theta = lam[0];
+  const float res = blast * fabsf(sm);
+  ok = ok && ny > 0.5f && theta > 0.0f && theta < 3.0e38f && res <= kLzTol * theta;
+  const float sy = frsq(fmaxf(ny, 1e-30f));
+  // lane layout through LDS
+  if (p == 0) sfor<0, NB>([&](auto tc) { S.vb[q + G * decltype(tc)::value] = sy * yc[decltype(tc)::value]; });
+  wsync();
+  sfor<0, V>([&](auto vc2) {
+    constexpr int v = decltype(vc2)::value;
+    const int i = li + L * v;
+    vv[v] = (i < D) ? S.vb[i < DM ? i : 0] : cf{0.0f, 0.0f};
+  });
+  wsync();   // vb reads before the caller's next write
+  lam1 = theta;
+  // wave-uniform verdict (G = 4: four bins per wave fall back together)
+  return __ballot(!ok) == 0ull;
+}
+
+// w from the rank-1 eigenpair (lam1, vv) of C: w = (1 - 1/lam1) x (v^H g),
+// x = Li^H v (the tail of eigen2d for one rank)
+template <int NB, int G = 8>
+DANSE_DEV void rank1_w2d(LDS2<NB, G>& S, int li, int D, const cf (&vv)[vpl<NB, G>()], float lam1,
+                         cf (&w)[vpl<NB, G>()]) {
+  constexpr int DM = G * NB, L = bin_lanes<G>(), V = vpl<NB, G>();
+  const int p = li / G, q = li % G;
+  cf sg;
+  sfor<0, V>([&](auto vc) {
+    constexpr int v = decltype(vc)::value;
+    const int i = li + L * v;
+    const cf t = cmul(vv[v], S.g[i]);
+    sg = (v == 0) ? t : sg + t;
+  });
+  const cf sr = gsum<L>(sg);
+  sfor<0, V>([&](auto vc) {
+    const int i = li + L * decltype(vc)::value;
+    if (i < DM) S.vb[i] = vv[decltype(vc)::value];
+  });
+  wsync();
+  cf vr[NB];
+  sfor<0, NB>([&](auto sc) {
+    constexpr int sb = decltype(sc)::value;
+    vr[sb] = S.vb[p + G * sb];
+  });
+  const float coef = 1.0f - frcp(lam1);
+  cf wc[NB];
+  sfor<0, NB>([&](auto tc) {
+    constexpr int t = decltype(tc)::value;
+    cf acc = cf{0.0f, 0.0f};
+    sfor<t, NB>([&](auto sc) {   // Li[i][c] = 0 for i < c
+      constexpr int sb = decltype(sc)::value;
+      acc = acc + cmul(ls_get<DM>(S.Ls, p + G * sb, q + G * t), vr[sb]);
+    });
+    acc = sump<G>(acc);
+    wc[t] = coef * (acc * sr);
+  });
+  wsync();   // vb reads before the wb writes (they share the union)
+  if (p == 0) {
+    sfor<0, NB>([&](auto tc) {
+      constexpr int t = decltype(tc)::value;
+      S.wb[q + G * t] = wc[t];
+    });
+  }
+  wsync();
+  sfor<0, V>([&](auto vc) {
+    const int i = li + L * decltype(vc)::value;
+    w[decltype(vc)::value] = (i < D) ? S.wb[i < D ? i : 0] : cf{0.0f, 0.0f};
+  });
+}
+
 // ---- phase 2: A = Ryy block (float32, destroyed), Li in S.Ls -> w[v] = entry li + L v
+// vCache (rank 1, or null): this bin's eigenvector of C from its previous
+// solve (the Lanczos start; zero = none), rewritten with this solve's (store:
+// the bin is real, not a padding copy)
 template <int NB, int RMAX, int G = 8>
-DANSE_DEV void gevd2d_filter(Blk<NB>& A, LDS2<NB, G>& S, int li, int D, int R, cf (&w)[vpl<NB, G>()]) {
+DANSE_DEV void gevd2d_filter(Blk<NB>& A, LDS2<NB, G>& S, int li, int D, int R, cf (&w)[vpl<NB, G>()],
+                             cf* vCache = nullptr, bool store = false) {
+  constexpr int V = vpl<NB, G>(), L = bin_lanes<G>(), DM = G * NB;
   congruence2d<NB, G>(A, S, li, D);
+  if (vCache && R == 1) {
+    cf vv[V];
+    float lam1;
+    if (lanczos2d<NB, G>(A, S, li, D, vCache, vv, lam1)) {
+      rank1_w2d<NB, G>(S, li, D, vv, lam1, w);
+      if (store) {
+        sfor<0, V>([&](auto vc) {
+          const int i = li + L * decltype(vc)::value;
+          if (i < DM) vCache[i] = vv[decltype(vc)::value];
+        });
+      }
+      return;
+    }
+  }
   tridiag2d<NB, G>(A, S, li, D);
-  eigen2d<NB, RMAX, G>(S, li, D, R, w);
+  eigen2d<NB, RMAX, G>(S, li, D, R, w, R == 1 ? vCache : nullptr, store);
 }
 
 }  // namespace t2d

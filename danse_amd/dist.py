@@ -93,6 +93,17 @@ class ShardedRun:
         self.stage = backend == 'gloo' and self.zbuf.device.type != 'cpu'
         if self.stage:
             self.hslot = [torch.zeros(per, dtype=torch.float32) for _ in range(self.slots)]
+        # node-sharded DXCP-PhaT: the Ns new z samples of every node per round
+        # ([K][S][Ns], this rank's nodes one chunk) for the receivers' estimators
+        nz = engine.zchunk_numel() if getattr(engine, 'zchunk_numel', None) is not None else 0
+        self.zc = None
+        if nz > 0:
+            self.zc = torch.zeros(nz, dtype=torch.float32, device=engine.torch_device)
+            engine.set_zchunk(self.zc)
+            zper = nz // self.world
+            self.zc_mine = self.zc[self.rank * zper:(self.rank + 1) * zper]
+            if self.stage:
+                self.zc_host = torch.zeros(nz, dtype=torch.float32)
         self.graph = (backend == 'nccl') if graph is None else bool(graph)
         # host-side control traffic (gate verdicts, callers' barriers)
         self.ctl = ctl if ctl is not None else control_group(group, backend)
@@ -109,8 +120,15 @@ class ShardedRun:
             mine = self.mine[i].cpu()
             self.dist.all_gather_into_tensor(self.hslot[i], mine, group=self.group)
             self.slot[i].copy_(self.hslot[i])
+            if self.zc is not None:
+                self.dist.all_gather_into_tensor(self.zc_host, self.zc_mine.cpu(), group=self.group)
+                self.zc.copy_(self.zc_host)
         else:
             self.dist.all_gather_into_tensor(self.slot[i], self.mine[i], group=self.group)
+            if self.zc is not None:
+                self.dist.all_gather_into_tensor(self.zc, self.zc_mine, group=self.group)
+        if self.zc is not None:
+            self.eng.unpack_zchunk(r)
 
     def _rounds(self, reset, gate):
         e = self.eng
@@ -213,6 +231,22 @@ class ShardedEngine:
     def set_zspec(self, t):
         from . import _lib as L
         L.check(self.e.lib.danse_engine_set_zspec(self.e.eng, ctypes.c_void_p(t.data_ptr())), self.e.eng)
+
+    def zchunk_numel(self):
+        """DXCP-PhaT on a node-sharded engine: [K][S][Ns] floats of z chunks
+        to exchange per round (0 otherwise)."""
+        e = self.e
+        if not getattr(e, 'dxcp', False) or (e.k0, e.k1) == (0, e.K):
+            return 0
+        return e.K * e.S * e.Ns
+
+    def set_zchunk(self, t):
+        from . import _lib as L
+        L.check(self.e.lib.danse_engine_set_zchunk(self.e.eng, ctypes.c_void_p(t.data_ptr())), self.e.eng)
+
+    def unpack_zchunk(self, r):
+        from . import _lib as L
+        L.check(self.e.lib.danse_engine_unpack_zchunk(self.e.eng, int(r), self.e.stream_ptr()), self.e.eng)
 
     def reset(self):
         from . import _lib as L

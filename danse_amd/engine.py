@@ -290,9 +290,9 @@ class DanseEngine:
             if any(n.fs and abs(n.fs / (1 + n.sro * 1e-6) - 16000.0) > 1e-6 for n in sc0.wasn) or self.N != 1024 \
                     or 2048 % self.Ns:
                 raise NotImplementedError('DXCP-PhaT (default parameters) needs 16 kHz, N = 1024 and Ns dividing 2048')
-            if (self.k0, self.k1) != (0, K):
-                raise NotImplementedError('DXCP-PhaT estimation on a node-sharded engine (the z streams are not '
-                                          'exchanged)')
+            # (node-sharded engines: the receivers' estimators read the other
+            # ranks' senders' z streams, exchanged per round by
+            # dist.ShardedRun through danse_engine_set_zchunk / _unpack_zchunk)
             if p.computeCentralised and p.compensateSROs:
                 raise NotImplementedError('centralised estimates with DXCP-PhaT SRO estimation')
         elif self.cohDrift:

@@ -248,7 +248,17 @@ int danse_engine_finish(danse_engine* eng, void* stream);
  * (check_covariance_matrices, d_classes.py:1430-1540).  danse_engine_bcast /
  * _update of such an engine run round r's steps before / from its first
  * update step.                                                            */
-int danse_engine_run_steps(danse_engine* eng, int32_t s0, int32_t s1, void* stream);   /* synthesis of the last round */
+int danse_engine_run_steps(danse_engine* eng, int32_t s0, int32_t s1, void* stream);
+/* Node-sharded DXCP-PhaT (danse_cfg.dxcp on an engine owning [k0, k1) of
+ * K nodes): the estimators of a receiver read every sender's received z
+ * stream, i.e. the Ns new samples each node broadcasts per round
+ * (fill_buffers, d_classes.py:1185-1224).  set_zchunk installs a [K][S][Ns]
+ * float device buffer (node-major: this engine's nodes [k0, k1) are one
+ * contiguous all-gather chunk) that every broadcast also writes; after the
+ * all-gather of round r, unpack_zchunk copies the other nodes' chunks into
+ * their streams.                                                          */
+int danse_engine_set_zchunk(danse_engine* eng, void* ptr);
+int danse_engine_unpack_zchunk(danse_engine* eng, int32_t r, void* stream);   /* synthesis of the last round */
 
 /* Device pointer + byte size of the fused-signal spectra buffer [2][K][S][F]
  * complex: round r writes slot r & 1 (node-major within a slot, so that a

@@ -28,14 +28,10 @@ _W = None     # worker-side shared block
 
 def _attach(name):
     global _W
-    from multiprocessing import resource_tracker
     from threadpoolctl import threadpool_limits
+    # (spawned workers share the parent's resource tracker: the block stays
+    # registered once, and the parent's unlink releases it)
     _W = shared_memory.SharedMemory(name=name)
-    # the parent owns the block; a worker attaching must not unlink it at exit
-    try:
-        resource_tracker.unregister(_W._name, 'shared_memory')
-    except Exception:
-        pass
     threadpool_limits(1)
 
 

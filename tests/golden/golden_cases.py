@@ -368,3 +368,11 @@ def scene_inputs(case):
     x[np.fmod(t, 1.0) >= 0.5] = 0.0
     h = (0.5 * rng.uniform(-1, 1, (sum(case['M']), case['nIR']))).astype(np.float32).astype(np.float64)
     return x, h
+
+
+# Condition numbers (saveConditionNumber: ConditionNumbers.get_new_cond_number,
+# d_classes.py:19-130,2126-2186) from the reference's own online run: the
+# shape of tests/test_gpu_engine_modes.py::test_condition_numbers_vs_oracle.
+COND_CASES = [dict(name='cond_k4m3', M=[3, 3, 3, 3], dur=2.0, seed=41,
+                   danse=_d(BATTERY, nodeUpdating='asy', computeLocal=True, saveConditionNumber=True,
+                            saveConditionNumberEvery=3))]

@@ -26,7 +26,7 @@ from golden_cases import ONLINE_CASES, BATCH_CASES, SRO_EVENT_CASES, KAT_CASES, 
 from golden_cases import DXCP_CASES, dxcp_inputs, TZ_CASES, tz_inputs, CLDXCP_CASES, cldxcp_acs  # noqa: E402
 from golden_cases import METRIC_CASES, metric_inputs, GETMETRICS_CASE, get_metrics_inputs  # noqa: E402
 from golden_cases import FIELD_CASES, FIELD_STFT_BIN_STEP, STOI_CASES, stoi_inputs, E2E_METRICS_CASE  # noqa: E402
-from golden_cases import SCENE_CASES, scene_inputs  # noqa: E402
+from golden_cases import SCENE_CASES, scene_inputs, COND_CASES  # noqa: E402
 
 
 def _run_online(ns, case):
@@ -298,6 +298,26 @@ def _run_scene(ns, case):
     return {'x': x, 'h': h, 'wet': wetAll, 'vad': vad[:, :, 0].T.astype(np.uint8), 'vad32': vad32.astype(np.uint8)}
 
 
+def _run_cond(ns, case):
+    """dv.condNumbers of the reference's online run (DANSE and local Ryy)."""
+    sc = make_scene(case['M'], sigDur=case['dur'], seed=case['seed'])
+    p = H.make_params(ns, case['M'], **case['danse'])
+    # (TestParameters.__post_init__ ties saveConditionNumber to
+    # exportParams.conditionNumberPlot, d_classes.py:226-230)
+    p.exportParams.conditionNumberPlot = True
+    p.danseParams.saveConditionNumber = True
+    w = H.to_ref_wasn(ns, sc)
+    p, w = H.prep(ns, p, w)
+    dv, w = ns.core.danse(w, p.danseParams)
+    cn = dv.condNumbers
+    out = {'digest': scene_digest(sc)}
+    for k in range(len(case['M'])):
+        for fam in ('DANSE', 'Local'):
+            out[f'cn_{fam}_{k}'] = np.asarray(getattr(cn, f'cn_Ryy{fam}')[k])
+            out[f'iter_{fam}_{k}'] = np.asarray(getattr(cn, f'iter_cn_Ryy{fam}')[k], dtype=np.int64)
+    return out
+
+
 def main():
     ns = H.load()
     only = sys.argv[1:]
@@ -314,6 +334,7 @@ def main():
            [('stoi', c, _run_stoi) for c in STOI_CASES] + \
            [('metrics', E2E_METRICS_CASE, _run_e2e_metrics)] + \
            [('scene', c, _run_scene) for c in SCENE_CASES] + \
+           [('cond', c, _run_cond) for c in COND_CASES] + \
            [('fields', dict(name=f'fields_{c}', src=c), lambda ns, c: _run_fields(ns, c['src'])) for c in FIELD_CASES]
     for kind, case, fn in jobs:
         name = case['name']

@@ -98,3 +98,54 @@ def test_round_engine_matches_oracle():
         d = np.stack([eng.st[s][k]['d'] for k in range(eng.K)], axis=1)
         err = np.max(np.abs(d - ov.d)) / np.max(np.abs(ov.d))
         assert err < 1e-4, err
+
+
+def _worker_subgroups(rank, world, port, outdir):
+    sys.path.insert(0, str(ROOT))
+    sys.path.insert(0, str(ROOT / 'tests'))
+    sys.path.insert(0, str(ROOT / 'tests' / 'golden'))
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from danse_amd.dist import ShardedRun, control_group, node_range
+    from _round_engine import RoundEngine
+    # two independent runs on the sub-groups {0, 1} and {2, 3} (every rank
+    # creates both groups, as new_group requires)
+    groups = [dist.new_group([0, 1]), dist.new_group([2, 3])]
+    mine = groups[rank // 2]
+    sub = rank % 2
+    case = _case()
+    k0, k1 = node_range(len(case['M']), 2, sub)
+    dp, scenes = _setup(case, nodes=list(range(k0, k1)))
+    eng = RoundEngine(scenes, dp, nodeRange=(k0, k1))
+    run = ShardedRun(eng, group=mine)
+    assert run.world == 2 and run.rank == sub
+    run.run()
+    # the RCCL-side control group: over this sub-group's ranks only, created
+    # by its members alone; a failing verdict on rank 3 stays inside {2, 3}
+    ctl = control_group(mine, 'nccl')
+    t = torch.tensor([0 if rank == 3 else 1], dtype=torch.int32)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=ctl)
+    np.save(Path(outdir) / f'verdict_{rank}.npy', t.numpy())
+    for s in range(eng.S):
+        for k in range(k0, k1):
+            np.save(Path(outdir) / f'd_{rank // 2}_{s}_{k}.npy', eng.st[s][k]['d'])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_subgroup_runs_and_control_groups():
+    """World size 4 as two sub-groups of 2: each sub-group's
+    ShardedRun equals the single-process run, and the control group of a
+    sub-group (dist.control_group, what an RCCL run uses for its gate
+    verdicts) only spans that sub-group's ranks."""
+    ref, _, _ = _single()
+    with tempfile.TemporaryDirectory() as td:
+        port = 29500 + (os.getpid() % 1000) + 31
+        mp.spawn(_worker_subgroups, args=(4, port, td), nprocs=4, join=True)
+        verd = [int(np.load(Path(td) / f'verdict_{r}.npy')[0]) for r in range(4)]
+        assert verd == [1, 1, 0, 0], verd
+        for g in range(2):
+            for s in range(ref.S):
+                for k in range(ref.K):
+                    assert np.array_equal(np.load(Path(td) / f'd_{g}_{s}_{k}.npy'), ref.st[s][k]['d']), (g, s, k)

@@ -38,6 +38,12 @@ CASES = {
                         danse=_d(BATTERY, nodeUpdating='asy', compensateSROs=True, includeFSDflags=True,
                                  estimateSROs='CohDrift', cohDrift=dict(estimationMethod='ls'))),
     'plain_k4': dict(name='plain_k4', M=[3, 3, 3, 3], dur=2.0, seed=2, danse=_d(BATTERY, nodeUpdating='asy')),
+    # DXCP-PhaT per (receiver, sender) on a node-sharded engine: the senders
+    # of the other rank reach the receivers' estimators through the per-round
+    # z-chunk all-gather (long enough for the estimators' first outputs)
+    'dxcp_k4': dict(name='dxcp_k4', M=[2, 2, 2, 2], dur=7.0, seed=16, sros=[0, 60, 120, 180],
+                    danse=_d(BATTERY, nodeUpdating='asy', compensateSROs=True, includeFSDflags=True,
+                             estimateSROs='DXCPPhaT')),
 }
 
 
@@ -123,7 +129,7 @@ def _compare(ref, td, K, passes):
                 assert np.array_equal(np.load(f), np.asarray(ref.SROsEstimates[k])), (i, k)
 
 
-@pytest.mark.parametrize('name', ['gate_delay_k4', 'cohdrift_k4'])
+@pytest.mark.parametrize('name', ['gate_delay_k4', 'cohdrift_k4', 'dxcp_k4'])
 def test_sharded_processes_match_single_engine(name):
     ref, td = _spawn(name, 2, 'gloo', 2)
     K = len(CASES[name]['M'])
@@ -132,6 +138,10 @@ def test_sharded_processes_match_single_engine(name):
         assert sorted(int(x) for x in ref.startRound) == [27, 28, 29, 54], ref.startRound
         assert int(np.load(td / 'specfail_0.npy')) == 1 and int(np.load(td / 'specfail_1.npy')) == 1
     _compare(ref, td, K, 2)
+    if name == 'dxcp_k4':
+        # the estimates reached the compensation on both ranks
+        for k in range(K):
+            assert np.count_nonzero(np.load(td / f'p0_sro_{k}.npy')) > 0, k
 
 
 @pytest.mark.parametrize('name', ['plain_k4', 'gate_delay_k4'])

@@ -4,7 +4,7 @@ import numpy as np
 import pytest
 
 from golden_cases import ONLINE_CASES, BATCH_CASES, SRO_EVENT_CASES, KAT_CASES, DXCP_CASES, TZ_CASES, kat_inputs
-from golden_cases import BESTPERF_CASES, SCENE_CASES, scene_inputs
+from golden_cases import BESTPERF_CASES, SCENE_CASES, scene_inputs, COND_CASES
 from danse_amd.scene import scene_digest
 from danse_amd.scheduler import initialize_events
 from oracle import danse_ref_cpu as O
@@ -264,3 +264,27 @@ def test_scene_vad_conv_vs_reference(case, golden_dir):
         v32 = SR.energy_vad(w32, case['fs'], case['vadWinLength'], case['vadEnergyDecrease_dB'])
         assert np.array_equal(v32, g['vad32'][j]), j
         assert 0.05 < v.mean() < 0.95
+
+
+@pytest.mark.parametrize('case', COND_CASES, ids=[c['name'] for c in COND_CASES])
+def test_condition_numbers_oracle_vs_reference(case, golden_dir):
+    """The oracle's condNumbers (ConditionNumbers, d_classes.py:19-130,
+    2126-2186) against the reference's own: the same saved iterations, and
+    np.linalg.cond of the same float64 SCMs (<= 1e-6 relative where the
+    reference's value is below 1e8; the rank-one first-frame basis gives
+    ~1e17, where both must be numerically singular)."""
+    g = _load(golden_dir, case['name'])
+    sc = make_case_scene(case)
+    assert scene_digest(sc) == str(g['digest'])
+    dp, wp = make_case_params(case)
+    ov = O.danse(sc, dp, vadMinProp=wp.vadMinProportionActive)
+    cn = ov.condNumbers
+    for k in range(len(case['M'])):
+        for fam in ('DANSE', 'Local'):
+            it = np.asarray(getattr(cn, f'iter_cn_Ryy{fam}')[k])
+            assert np.array_equal(it, g[f'iter_{fam}_{k}']), (fam, k)
+            a, b = np.asarray(getattr(cn, f'cn_Ryy{fam}')[k]), g[f'cn_{fam}_{k}']
+            assert a.shape == b.shape
+            ok = b < 1e8
+            assert np.max(np.abs(a[ok] - b[ok]) / b[ok]) <= 1e-6, (fam, k)
+            assert np.all(a[~ok] > 1e10), (fam, k)
