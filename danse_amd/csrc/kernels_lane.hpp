@@ -66,27 +66,32 @@ __global__ void __launch_bounds__(64) update_kernel_lane(const UpdateArgs a) {
   }
   const double beta = a.beta[s * a.K + d.k];
   const long long base = (long long)s * a.scmStride + d.scmOff + f;
+  // Ryy (float32) of this frame into A: load, the recursion when the VAD
+  // selects it, store
+  auto ryy_update = [&](PTri<D>& A) {
+    sfor<0, NT>([&](auto ec) { A.a[decltype(ec)::value] = a.Ryy[base + (long long)decltype(ec)::value * F]; });
+    if (opY) {
+      const float by = (float)beta, cy = (opY == DANSE_OP_SET) ? (float)(1.0 / D) : (float)((1.0 - beta) / D);
+      sfor<0, D>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        sfor<0, i + 1>([&](auto jc) {
+          constexpr int j = decltype(jc)::value;
+          const cf yy = cy * mulc(y[i], y[j]);
+          A.a[P(i, j)] = csel(opY == DANSE_OP_SET, yy, by * A.a[P(i, j)] + yy);
+          if constexpr (i == j) A.a[P(i, j)].im = 0.0f;
+        });
+      });
+      if (valid) {
+        sfor<0, NT>([&](auto ec) { a.Ryy[base + (long long)decltype(ec)::value * F] = A.a[decltype(ec)::value]; });
+      }
+    }
+  };
 
   // ---- SCM recursion (the VAD selects one of Ryy / Rnn per frame):
-  // SCM <- yy^H (first-frame basis) or beta SCM + (1 - beta) yy^H, yy^H = y y^H / D
-  if (opY) {
-    PTri<D> A;
-    sfor<0, NT>([&](auto ec) { A.a[decltype(ec)::value] = a.Ryy[base + (long long)decltype(ec)::value * F]; });
-    const float by = (float)beta, cy = (opY == DANSE_OP_SET) ? (float)(1.0 / D) : (float)((1.0 - beta) / D);
-    sfor<0, D>([&](auto ic) {
-      constexpr int i = decltype(ic)::value;
-      sfor<0, i + 1>([&](auto jc) {
-        constexpr int j = decltype(jc)::value;
-        const cf yy = cy * mulc(y[i], y[j]);
-        A.a[P(i, j)] = csel(opY == DANSE_OP_SET, yy, by * A.a[P(i, j)] + yy);
-        if constexpr (i == j) A.a[P(i, j)].im = 0.0f;
-      });
-    });
-    if (valid) {
-      sfor<0, NT>([&](auto ec) { a.Ryy[base + (long long)decltype(ec)::value * F] = A.a[decltype(ec)::value]; });
-    }
-  }
-  asm volatile("" ::: "memory");   // the Ryy work above is done before the float64 triangle loads
+  // SCM <- yy^H (first-frame basis) or beta SCM + (1 - beta) yy^H, yy^H = y y^H / D.
+  // Rnn (float64) first, with the factor of a solve; then Ryy, which a solve
+  // uses straight from the registers it was updated in (one Ryy read per
+  // frame: the recursion, the store and the congruence share it)
   PTriD<D> N;
   if (opN || (solve && !reuse)) {
     sfor<0, NT>([&](auto ec) { N.a[decltype(ec)::value] = a.Rnn[base + (long long)decltype(ec)::value * F]; });
@@ -115,6 +120,7 @@ __global__ void __launch_bounds__(64) update_kernel_lane(const UpdateArgs a) {
   bool ok = true;
   if (solve) {
   if constexpr (GEVD) {
+    asm volatile("" ::: "memory");   // (the float64 triangle is dead before the float32 work below)
     if (reuse) {
       sfor<0, NT>([&](auto ec) { Ls[decltype(ec)::value][threadIdx.x] = liC[(long long)decltype(ec)::value * F]; });
       sfor<0, D>([&](auto ic) { Gs[decltype(ic)::value][threadIdx.x] = liC[(long long)(NT + decltype(ic)::value) * F]; });
@@ -150,7 +156,7 @@ __global__ void __launch_bounds__(64) update_kernel_lane(const UpdateArgs a) {
     });
     asm volatile("" ::: "memory");
     PTri<D> A;
-    sfor<0, NT>([&](auto ec) { A.a[decltype(ec)::value] = a.Ryy[base + (long long)decltype(ec)::value * F]; });
+    ryy_update(A);
     cf w[D];
     ok = mwf_filter_mixed<D>(A, ncol, d.ref, w);
     const int slotNext = a.wHistory ? r + 1 : ((r + 1) & 1);
@@ -158,6 +164,10 @@ __global__ void __launch_bounds__(64) update_kernel_lane(const UpdateArgs a) {
     if (valid) sfor<0, D>([&](auto ic) { wNext[decltype(ic)::value] = w[decltype(ic)::value]; });
   }
   if (!ok && valid) atomicOr(&a.diag[(s * a.K + d.k) * kMaxFam + d.fam], 1);
+  }
+  if (!solve && opY) {   // (a solve updates Ryy where it uses it)
+    PTri<D> A;
+    ryy_update(A);
   }
   asm volatile("" ::: "memory");
   const bool pregiven = (fl & DANSE_FLAG_PREGIVEN) != 0;
@@ -177,7 +187,7 @@ __global__ void __launch_bounds__(64) update_kernel_lane(const UpdateArgs a) {
       cf g[D];
       sfor<0, D>([&](auto ic) { g[decltype(ic)::value] = Gs[decltype(ic)::value][threadIdx.x]; });
       PTri<D> A;
-      sfor<0, NT>([&](auto ec) { A.a[decltype(ec)::value] = a.Ryy[base + (long long)decltype(ec)::value * F]; });
+      ryy_update(A);
       congruence<D>(A, Li);
       gevd_filter_mixed<D, RMAX>(A, Li, g, a.rank, w);
     }
