@@ -563,9 +563,10 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
       else if (c->gevd && gridSmall) liOff += (long long)F * class_li_record(16);
       else if (c->gevd && class_grid(class_dmax(fn.D)) > 0) liOff += (long long)F * class_li_record(class_dmax(fn.D));
       fn.vOff = -1;
-      if (warm && !fn.packed && (gridSmall || class_grid(class_dmax(fn.D)) > 0)) {
+      // (grid classes of 20 and more: solver2d.hpp gevd2d_filter)
+      if (warm && !fn.packed && !gridSmall && class_grid(class_dmax(fn.D)) > 0 && class_dmax(fn.D) >= 20) {
         fn.vOff = vOff;
-        vOff += (long long)F * (gridSmall ? 16 : class_dmax(fn.D));
+        vOff += (long long)F * class_dmax(fn.D);
       }
       eng->fns.push_back(fn);
     }

@@ -403,10 +403,9 @@ resident_kernel(const ResArgs ra) {
 #ifndef RES_NOSOLVE2
     if (solve) {
       Blk<NB> A = Ry;
-      // (the warm-started rank-1 Lanczos path, its eigenvector record per bin
-      // in the engine's cache: 16 entries per bin, the grid class 16 layout)
-      cf* vC = (a.vCache && d.vOff >= 0) ? a.vCache + (long long)s * a.vStride + d.vOff + (long long)f * 16 : nullptr;
-      gevd2d_filter<NB, RMAX, G>(A, S, li, D, a.rank, w, vC, fvalid);
+      // (no warm-started Lanczos here: at D <= 12 the Householder path is
+      // short and the few Lanczos steps that fit were measured slower)
+      gevd2d_filter<NB, RMAX, G>(A, S, li, D, a.rank, w);
     }
 #endif
 

@@ -858,10 +858,10 @@ DANSE_DEV bool lanczos2d(const Blk<NB>& A, LDS2<NB, G>& S, int li, int D, const 
   const float s0 = ok ? frsq(n0) : 0.0f;
   sfor<0, NB>([&](auto tc) { vc[decltype(tc)::value] = s0 * vc[decltype(tc)::value]; });
   if (p == 0) sfor<0, NB>([&](auto tc) { Q[q + G * decltype(tc)::value] = vc[decltype(tc)::value]; });
-  cf pv[NB];
-  sfor<0, NB>([&](auto tc) { pv[decltype(tc)::value] = cf{0.0f, 0.0f}; });
-  float bprev = 0.0f, blast = 0.0f;
-  for (int k = 0; k < M; ++k) {
+  float blast = 0.0f;
+  // k = 0 .. M - 1, unrolled (the orthogonalisation's loops get static bounds)
+  sfor<0, M>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
     // w = C v: row-layout partial sums over the row group, then the column
     // layout through LDS
     sfor<0, NB>([&](auto sc) {
@@ -873,34 +873,36 @@ DANSE_DEV bool lanczos2d(const Blk<NB>& A, LDS2<NB, G>& S, int li, int D, const 
     });
     wsync();
     cf wc[NB];
-    float al = 0.0f;
-    sfor<0, NB>([&](auto tc) {
-      constexpr int t = decltype(tc)::value;
-      wc[t] = S.qb[k & 1][q + G * t];
-      al += vc[t].re * wc[t].re + vc[t].im * wc[t].im;
-    });
-    al = sumq<G>(al);
-    sfor<0, NB>([&](auto tc) {
-      constexpr int t = decltype(tc)::value;
-      wc[t] = wc[t] - al * vc[t] - bprev * pv[t];
-    });
-    // one reorthogonalisation pass against the basis so far
-    for (int j = 0; j <= k; ++j) {
-      cf qj[NB], h = cf{0.0f, 0.0f};
+    sfor<0, NB>([&](auto tc) { wc[decltype(tc)::value] = S.qb[k & 1][q + G * decltype(tc)::value]; });
+    // one classical Gram-Schmidt pass against the basis Q_0 .. Q_k: the
+    // coefficients are independent (one reduction each, side by side);
+    // h_k is the Lanczos alpha_k, h_(k-1) its beta_(k-1)
+    cf h[k + 1];
+    sfor<0, k + 1>([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      cf acc = cf{0.0f, 0.0f};
       sfor<0, NB>([&](auto tc) {
         constexpr int t = decltype(tc)::value;
-        qj[t] = Q[j * DM + q + G * t];
-        h = h + cmul(qj[t], wc[t]);
+        const cf qj = (j == k) ? vc[t] : Q[j * DM + q + G * t];
+        acc = acc + cmul(qj, wc[t]);
       });
-      h = sumq<G>(h);
-      sfor<0, NB>([&](auto tc) { fms_c(wc[decltype(tc)::value], h, qj[decltype(tc)::value]); });
-    }
+      h[j] = acc;
+    });
+    sfor<0, k + 1>([&](auto jc) { h[decltype(jc)::value] = sumq<G>(h[decltype(jc)::value]); });
+    sfor<0, k + 1>([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      sfor<0, NB>([&](auto tc) {
+        constexpr int t = decltype(tc)::value;
+        const cf qj = (j == k) ? vc[t] : Q[j * DM + q + G * t];
+        fms_c(wc[t], h[j], qj);
+      });
+    });
     float nb = 0.0f;
     sfor<0, NB>([&](auto tc) { nb += abs2(wc[decltype(tc)::value]); });
     nb = sumq<G>(nb);
     const float b = fsqrt(nb);
     if (li == 0) {
-      S.a[k] = al;
+      S.a[k] = h[k].re;
       if (k + 1 < M) {
         S.e2[k] = nb;
         S.ev[k] = b;
@@ -910,16 +912,11 @@ DANSE_DEV bool lanczos2d(const Blk<NB>& A, LDS2<NB, G>& S, int li, int D, const 
     // basis vectors zero: the small tridiagonal splits and its top Ritz pair
     // is exact)
     const float ib = (b > 1e-20f) ? frcp(b) : 0.0f;
-    sfor<0, NB>([&](auto tc) {
-      constexpr int t = decltype(tc)::value;
-      pv[t] = vc[t];
-      vc[t] = ib * wc[t];
-    });
+    sfor<0, NB>([&](auto tc) { vc[decltype(tc)::value] = ib * wc[decltype(tc)::value]; });
     if (k + 1 < M && p == 0) sfor<0, NB>([&](auto tc) { Q[(k + 1) * DM + q + G * decltype(tc)::value] = vc[decltype(tc)::value]; });
-    bprev = b;
     blast = b;
     wsync();
-  }
+  });
   // top Ritz pair of the M x M tridiagonal (the full path's eigen routines)
   float lam[kRMax], tnorm;
   top_eigvals2d<M, 1, G>(S.a, S.e2, li, M, 1, lam, tnorm);
@@ -1020,7 +1017,9 @@ DANSE_DEV void gevd2d_filter(Blk<NB>& A, LDS2<NB, G>& S, int li, int D, int R, c
                              cf* vCache = nullptr, bool store = false) {
   constexpr int V = vpl<NB, G>(), L = bin_lanes<G>(), DM = G * NB;
   congruence2d<NB, G>(A, S, li, D);
-  if (vCache && R == 1) {
+  // (classes below 20: too few Lanczos steps fit, and the D-step Householder
+  // path is short there -- measured slower with the warm start)
+  if (G * NB >= 20 && vCache && R == 1) {
     cf vv[V];
     float lam1;
     if (lanczos2d<NB, G>(A, S, li, D, vCache, vv, lam1)) {
