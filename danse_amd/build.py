@@ -34,7 +34,8 @@ def _units():
     u = [('danse_engine.o', CSRC / 'danse_engine.hip', []), ('batch.o', CSRC / 'batch.hip', []),
          ('dxcp.o', CSRC / 'dxcp.hip', []), ('tz.o', CSRC / 'tz.hip', []),
          ('metrics.o', CSRC / 'metrics.hip', []), ('stoi.o', CSRC / 'stoi.hip', []),
-         ('scene.o', CSRC / 'scene.hip', []), ('resident.o', CSRC / 'resident.hip', [])]
+         ('scene.o', CSRC / 'scene.hip', []), ('resident.o', CSRC / 'resident.hip', []),
+         ('wide.o', CSRC / 'wide.hip', [])]
     for n in CLASSES:
         # lane-per-bin classes: no SLP packing of the float32 complex math
         # (the packed pairs need swapped operand copies; with them the eigen

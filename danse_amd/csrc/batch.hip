@@ -13,6 +13,7 @@
 // sum(win): x = sum_t irfft(dhat_t) win / sum_t win^2 where that is > 1e-10.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <string>
 #include <vector>
@@ -20,6 +21,7 @@
 #include "../../include/danse_mi355x.h"
 #include "classes.hpp"
 #include "wfft.hpp"
+#include "wide_api.hpp"
 
 using namespace danse;
 
@@ -271,6 +273,80 @@ __global__ void __launch_bounds__(64) herk_kernel(const cf* __restrict__ Y, cons
           }
         }
         ++p;
+      }
+    }
+  }
+}
+
+// Ryy / Rnn of the wide classes (centralised estimates, 64 < D <= 256) in
+// float64: one wave per kWHP tile pairs (I >= J) of the 16 x 16 tiling of one
+// (scene, bin), v_mfma_f64_16x16x4_f64 on both passes (the f32 products are
+// exact in f64, the sums over the frames are not rounded to f32).  `rep` is
+// the node whose VAD frame list the SCM group uses.
+constexpr int kWHP = 8;
+__global__ void __launch_bounds__(64) wide_herk_kernel(const cf* __restrict__ Y, int S, int K, int MT, int nseg,
+                                                       int D, int rep, const int* __restrict__ frames,
+                                                       const int* __restrict__ nvad, cd* __restrict__ Ryy,
+                                                       cd* __restrict__ Rnn) {
+  constexpr int F = 513;
+  const int NT = (D + 15) / 16, NP = NT * (NT + 1) / 2, nPC = (NP + kWHP - 1) / kWHP;
+  const int pc = blockIdx.x % nPC;
+  const int f = (blockIdx.x / nPC) % F;
+  const int s = blockIdx.x / (nPC * F);
+  const int l = threadIdx.x, il = l & 15, tt = l >> 4;
+  int PI[kWHP], PJ[kWHP];
+#pragma unroll
+  for (int q = 0; q < kWHP; ++q) {
+    int p = pc * kWHP + q, I = 0;
+    if (p >= NP) p = NP - 1;   // (tail: recompute the last pair, store nothing)
+    while ((I + 1) * (I + 2) / 2 <= p) ++I;
+    PI[q] = I;
+    PJ[q] = p - I * (I + 1) / 2;
+  }
+  const int* fl = frames + ((long long)s * K + rep) * nseg;
+  const int nv = nvad[s * K + rep];
+  const cf* yb = Y + ((long long)s * F + f) * nseg * MT;
+  const long long o = ((long long)s * F + f) * D * D;
+  for (int pass = 0; pass < 2; ++pass) {
+    const int t0 = pass ? nv : 0;
+    const int cnt = pass ? nseg - nv : nv;
+    f64x4 re[kWHP], im[kWHP];
+#pragma unroll
+    for (int q = 0; q < kWHP; ++q) {
+      re[q] = f64x4(0.0);
+      im[q] = f64x4(0.0);
+    }
+    for (int b = 0; b < cnt; b += 4) {
+      const int ti = b + tt;
+      const bool ok = ti < cnt;
+      const cf* row = yb + (long long)(ok ? fl[t0 + ti] : 0) * MT;
+#pragma unroll
+      for (int q = 0; q < kWHP; ++q) {
+        const int i = 16 * PI[q] + il, j = 16 * PJ[q] + il;
+        const cf xi = (ok && i < D) ? row[i] : cf{0.0f, 0.0f};
+        const cf xj = (ok && j < D) ? row[j] : cf{0.0f, 0.0f};
+        const double ir = xi.re, ii = xi.im, jr = xj.re, ji = xj.im;
+        re[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(ir, jr, re[q], 0, 0, 0);
+        re[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(ii, ji, re[q], 0, 0, 0);
+        im[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(ii, jr, im[q], 0, 0, 0);
+        im[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(ir, -ji, im[q], 0, 0, 0);
+      }
+    }
+    const double sc = (cnt > 0) ? 1.0 / (double)cnt : __builtin_nan("");
+    cd* R = pass ? Rnn : Ryy;
+#pragma unroll
+    for (int q = 0; q < kWHP; ++q) {
+      if (pc * kWHP + q >= NP) continue;
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        const int row = 16 * PI[q] + tt + 4 * rg;   // f64 C/D map: col = lane & 15, row = (lane >> 4) + 4 reg
+        const int col = 16 * PJ[q] + il;
+        if (row < D && col < D && (PI[q] != PJ[q] || col <= row)) {
+          cd c = cd{sc * re[q][rg], sc * im[q][rg]};
+          if (row == col) c.im = 0.0;
+          R[o + (long long)row * D + col] = c;
+          if (row != col) R[o + (long long)col * D + row] = conjg(c);
+        }
       }
     }
   }
@@ -542,6 +618,13 @@ struct danse_batch {
   double* dCostPart = nullptr;   // [S][nOwn][kCostParts]
   int* dDiag = nullptr;
   int Dmax = 1;
+  // wide classes (centralised estimates with 64 < sum(M) <= 256, wide.hpp):
+  // nodes whose VAD frame lists agree share one SCM pair (group grp[k],
+  // first node grpRep); the solves run per group
+  bool wideMode = false;
+  std::vector<int> grp, grpRep;
+  cd* wideWork = nullptr;
+  long long wideChunk = 0;
   // per-phase timing of run_iters (danse_batch_set_timing): events after
   // every phase of every iteration, [iteration][kBatchPhases + 1]
   bool timing = false;
@@ -612,15 +695,38 @@ int danse_batch_create(const danse_batch_cfg* c, int device, danse_batch** out) 
     eng->refK[k] = c->obs == 2 ? eng->base[k] + c->ref : c->ref;
     eng->ybase[k] = c->obs == 2 ? 0 : eng->base[k];
     eng->ycnt[k] = c->obs == 2 ? mt : eng->M[k];
-    if (eng->D[k] > kMaxDMax) return bfail(eng, "filter dimension > 64 not supported");
+    if (eng->D[k] > kMaxDMax && !(c->obs == 2 && eng->D[k] <= wide::kMaxD))
+      return bfail(eng, "filter dimension > 64 not supported (centralised estimates: <= 256)");
     if (c->ref >= eng->M[k]) return bfail(eng, "referenceSensor must be < M_k for every node");
     if (c->gevd && c->rank > eng->D[k]) return bfail(eng, "GEVD rank larger than a filter dimension");
   }
   eng->MT = mt;
+  eng->wideMode = c->obs == 2 && mt > kMaxDMax;
+  if (eng->wideMode && K > wide::kMaxOut) return bfail(eng, "centralised estimates above 64 channels: at most 64 nodes");
   long long so = 0, wo = 0, eo = 0, to = 0;
   eng->scmOff.resize(K); eng->wOff.resize(K); eng->wExtOff.resize(K); eng->tgtOff.resize(K);
+  eng->grp.assign(K, -1);
   for (int k = 0; k < K; ++k) {
-    eng->scmOff[k] = so; so += (long long)S * F * eng->D[k] * eng->D[k];
+    if (eng->wideMode) {
+      // share the SCM pair of an earlier node with the same VAD in every scene
+      for (int q = 0; q < k && eng->grp[k] < 0; ++q) {
+        if (eng->grpRep[eng->grp[q]] != q) continue;
+        bool same = true;
+        for (int s2 = 0; s2 < S && same; ++s2)
+          same = std::equal(c->vad + ((size_t)s2 * K + k) * nseg, c->vad + ((size_t)s2 * K + k + 1) * nseg,
+                            c->vad + ((size_t)s2 * K + q) * nseg);
+        if (same) eng->grp[k] = eng->grp[q];
+      }
+      if (eng->grp[k] >= 0) {
+        eng->scmOff[k] = eng->scmOff[eng->grpRep[eng->grp[k]]];
+      } else {
+        eng->grp[k] = (int)eng->grpRep.size();
+        eng->grpRep.push_back(k);
+        eng->scmOff[k] = so; so += (long long)S * F * eng->D[k] * eng->D[k];
+      }
+    } else {
+      eng->scmOff[k] = so; so += (long long)S * F * eng->D[k] * eng->D[k];
+    }
     eng->wOff[k] = wo; wo += (long long)H * F * eng->D[k];
     eng->wExtOff[k] = eo; eo += (long long)H * F * eng->M[k];
     eng->tgtOff[k] = to; to += (long long)F * eng->M[k];
@@ -710,6 +816,10 @@ int danse_batch_create(const danse_batch_cfg* c, int device, danse_batch** out) 
   eng->Dmax = Dmax;
   BCHK(balloc(&eng->wTmp, (size_t)K * S * F * Dmax));   // one solve launch covers a run of nodes
   BCHK(balloc(&eng->dDiag, (size_t)K * S * F));
+  if (eng->wideMode) {
+    eng->wideChunk = std::min<long long>((long long)S * F, 1024);
+    BCHK(balloc(&eng->wideWork, (size_t)eng->wideChunk * wide::work_elems(mt)));
+  }
   (void)Mmax;
   *out = eng;
   return 0;
@@ -721,7 +831,7 @@ void danse_batch_destroy(danse_batch* eng) {
   void* ptrs[] = {eng->dM, eng->dBase, eng->dD, eng->dExtMode, eng->dFrames, eng->dNvad, eng->dWOff, eng->dWExtOff,
                   eng->dTgtOff, eng->dNodes, eng->dWin, eng->dBetaExt, eng->dTw, eng->Y, eng->Z, eng->Ryy, eng->Rnn,
                   eng->wHist, eng->wExtHist, eng->tgt, eng->dhat, eng->dFramesTD, eng->dD_, eng->dCost, eng->wTmp,
-                  eng->dDiag, eng->dCostPart, eng->dYBase, eng->dYCnt};
+                  eng->dDiag, eng->dCostPart, eng->dYBase, eng->dYCnt, eng->wideWork};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (hipEvent_t e : eng->ev) (void)hipEventDestroy(e);
@@ -813,7 +923,20 @@ int danse_batch_run_iters(danse_batch* eng, int32_t it0, int32_t it1, void* stre
       BCHK(hipGetLastError());
     }
     mark(it, 1);
-    launch_herk(eng, st);
+    if (eng->wideMode) {
+      const int D = eng->MT, NT = (D + 15) / 16, nPC = (NT * (NT + 1) / 2 + kWHP - 1) / kWHP;
+      for (size_t g = 0; g < eng->grpRep.size(); ++g) {
+        bool owned = false;
+        for (int k = eng->k0; k < eng->k1; ++k) owned = owned || eng->grp[k] == (int)g;
+        if (!owned) continue;
+        const int rep = eng->grpRep[g];
+        hipLaunchKernelGGL(wide_herk_kernel, dim3((unsigned)(S * F * nPC)), dim3(64), 0, st, eng->Y, S, K, eng->MT,
+                           nseg, D, rep, eng->dFrames, eng->dNvad, eng->Ryy + eng->scmOff[rep],
+                           eng->Rnn + eng->scmOff[rep]);
+      }
+    } else {
+      launch_herk(eng, st);
+    }
     BCHK(hipGetLastError());
     mark(it, 2);
     // Solves (perform_update, d_core.py:298-326): consecutive solving nodes
@@ -821,7 +944,36 @@ int danse_batch_run_iters(danse_batch* eng, int32_t it0, int32_t it1, void* stre
     // launch covers the whole run (K*S*F bins for equal D: a full chip
     // instead of S*F bins per launch).
     const size_t pitch = (size_t)eng->wStride * sizeof(cf);
-    for (int k = eng->k0; k < eng->k1;) {
+    if (eng->wideMode) {
+      // one wide launch per SCM group: its solving nodes' reference sensors
+      // are the outputs of one eigendecomposition per (scene, bin)
+      const int D = eng->MT;
+      for (size_t g = 0; g < eng->grpRep.size(); ++g) {
+        wide::WideArgs wa{};
+        wa.D = D; wa.rank = eng->rank; wa.gevd = eng->gevd; wa.F = F;
+        wa.nItems = (long long)S * F; wa.layout = 0;
+        wa.RyyD = eng->Ryy + eng->scmOff[eng->grpRep[g]];
+        wa.Rnn = eng->Rnn + eng->scmOff[eng->grpRep[g]];
+        wa.srcScene = (long long)F * D * D; wa.srcBin = (long long)D * D;
+        wa.w = eng->wHist; wa.wScene = eng->wStride; wa.wBin = D;
+        wa.diag = eng->dDiag + (size_t)g * S * F;
+        wa.work = eng->wideWork;
+        for (int k = eng->k0; k < eng->k1; ++k) {
+          if (eng->grp[k] != (int)g || !eng->doSolve[(size_t)it * K + k]) continue;
+          wa.refs[wa.nOut] = eng->refK[k];
+          wa.wOff[wa.nOut] = eng->wOff[k] + (long long)(it + 1) * F * D;
+          ++wa.nOut;
+        }
+        if (wa.nOut) BCHK(wide::launch_wide_filters(wa, eng->wideChunk, st));
+      }
+      for (int k = eng->k0; k < eng->k1; ++k) {
+        if (eng->doSolve[(size_t)it * K + k]) continue;
+        cf* wNext = eng->wHist + eng->wOff[k] + (long long)(it + 1) * F * D;
+        BCHK(hipMemcpy2DAsync(wNext, pitch, wNext - (long long)F * D, pitch, (size_t)F * D * sizeof(cf), S,
+                              hipMemcpyDeviceToDevice, st));
+      }
+    }
+    for (int k = eng->wideMode ? eng->k1 : eng->k0; k < eng->k1;) {
       const int D = eng->D[k];
       const size_t rowB = (size_t)F * D * sizeof(cf);
       if (!eng->doSolve[(size_t)it * K + k]) {

@@ -37,9 +37,7 @@ __global__ void __launch_bounds__(64) cond_kernel(const UpdateArgs a, const FamN
   if (act) {
     const int i = li;
     for (int j = 0; j <= i; ++j) {
-      long long e;
-      if (d.packed) e = (long long)s * a.scmStride + d.scmOff + (long long)(i * (i + 1) / 2 + j) * F + f;
-      else e = (long long)s * a.scmStride + d.scmOff + ((long long)f * D + i) * D + j;
+      const long long e = scm_lower(d, a.scmStride, s, F, f, i, j);
       cd x = cdk(a.Ryy[e]);
       if (i == j) x.im = 0.0;
       cA[i * P + j] = x;

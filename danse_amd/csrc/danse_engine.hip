@@ -12,6 +12,7 @@
 #include "../../include/danse_mi355x.h"
 #include "bcast.hpp"
 #include "fill.hpp"
+#include "wide_api.hpp"
 #include "classes.hpp"
 #include "gate.hpp"
 #include "cohdrift.hpp"
@@ -180,18 +181,20 @@ __global__ void reset_fam_kernel(const FamNode* fns, int nFN, const long long* w
   const int i = blockIdx.y % nFN;
   const FamNode fn = fns[i];
   const int D = fn.D;
-  const long long nS = fn.packed ? (long long)F * D * (D + 1) / 2 : (long long)F * D * D;
+  const long long T = (long long)D * (D + 1) / 2;
+  const long long nS = fn.packed ? F * T : (long long)F * D * D;
   const long long nW = (long long)F * D;
   for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < nS; e += (long long)gridDim.x * blockDim.x) {
     long long src;
     if (fn.packed) {
-      // packed entry t = i (i + 1) / 2 + j of bin e % F -> full slice element (i, j)
-      const int t = (int)(e / F);
+      // packed entry t = i (i + 1) / 2 + j of bin fb -> full slice element (i, j)
+      const int t = (int)(fn.packed == 1 ? e / F : e % T);
+      const long long fb = fn.packed == 1 ? e % F : e / T;
       int r = (int)((sqrtf(8.0f * (float)t + 1.0f) - 1.0f) * 0.5f);
       while (r * (r + 1) / 2 > t) --r;
       while ((r + 1) * (r + 2) / 2 <= t) ++r;
       src = (long long)r * D + (t - r * (r + 1) / 2);
-      if (perBin) src += (e % F) * D * D;
+      if (perBin) src += fb * D * D;
     } else {
       src = perBin ? e : e % ((long long)D * D);
     }
@@ -549,22 +552,23 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
       if (fn.D > kMaxDMax) return fail(eng, "filter dimension > 64 not supported");
       if (c->gevd && c->rank > fn.D) return fail(eng, "GEVD rank larger than a filter dimension");
       fn.scmOff = scmOff;
-      // smallDGrid: GEVD of D <= 12 on the 4 x 4 grid class 16 (full storage)
+      // smallDGrid: GEVD of D <= 12 on the 4 x 4 grid class 16; the grid and
+      // row classes keep bin-major triangles (FamNode.packed 2)
       const bool gridSmall = c->smallDGrid && c->gevd && fn.D <= kLaneMaxD;
-      fn.packed = (class_packed(fn.D) && !gridSmall) ? 1 : 0;
-      scmOff += fn.packed ? (long long)F * fn.D * (fn.D + 1) / 2 : (long long)F * fn.D * fn.D;
+      fn.packed = (class_packed(fn.D) && !gridSmall) ? 1 : 2;
+      scmOff += (long long)F * fn.D * (fn.D + 1) / 2;
       fn.wOff = wOff;
       wOff += histW * F * fn.D;
       fn.liOff = liOff;
       // (a split class's grid solves keep their own per-bin record in the region)
-      if (c->gevd && fn.packed)
+      if (c->gevd && fn.packed == 1)
         liOff += (long long)F * std::max<long long>(fn.D * (fn.D + 1) / 2 + fn.D,
                                                     class_split(class_dmax(fn.D)) ? class_split_li_record() : 0);
       else if (c->gevd && gridSmall) liOff += (long long)F * class_li_record(16);
       else if (c->gevd && class_grid(class_dmax(fn.D)) > 0) liOff += (long long)F * class_li_record(class_dmax(fn.D));
       fn.vOff = -1;
       // (grid classes of 20 and more: solver2d.hpp gevd2d_filter)
-      if (warm && !fn.packed && !gridSmall && class_grid(class_dmax(fn.D)) > 0 && class_dmax(fn.D) >= 20) {
+      if (warm && fn.packed == 2 && !gridSmall && class_grid(class_dmax(fn.D)) > 0 && class_dmax(fn.D) >= 20) {
         fn.vOff = vOff;
         vOff += (long long)F * class_dmax(fn.D);
       }
@@ -591,7 +595,7 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
   for (size_t i = 0; i < eng->fns.size(); ++i) {
     int G, DM;
     pick_class(eng->fns[i].D, G, DM);
-    if (!eng->fns[i].packed && DM <= kLaneMaxD) {   // smallDGrid (above)
+    if (eng->fns[i].packed == 2 && DM <= kLaneMaxD) {   // smallDGrid (above)
       G = class_group(16);
       DM = 16;
     }
@@ -1168,7 +1172,7 @@ static int resident_prepare(danse_engine* eng, int& NB) {
   if (2 * e->Ns != e->N || e->Ns > 512) return fail(e, "resident run: 50 % frame overlap (Ns = N / 2 = 512) only");
   int dmax = 1;
   for (const auto& fn : e->fns) {
-    if (fn.packed || fn.D > 12) return fail(e, "resident run: filter dimensions <= 12 in grid storage (smallDGrid)");
+    if (fn.packed == 1 || fn.D > 12) return fail(e, "resident run: filter dimensions <= 12 in grid storage (smallDGrid)");
     dmax = std::max(dmax, fn.D);
   }
   NB = 3;
@@ -1717,9 +1721,24 @@ int danse_wola_analysis(const float* x, int32_t C, int32_t T, const int32_t* end
 int danse_filter_update(const double* Ryy, const double* Rnn, int32_t B, int32_t D, int32_t gevd, int32_t rank,
                         int32_t ref, float* w, int32_t* diag, void* stream) {
   danse_engine* eng = nullptr;
-  if (D < 1 || D > 64) return fail(nullptr, "D must be in [1, 64]");
+  if (D < 1 || D > wide::kMaxD) return fail(nullptr, "D must be in [1, 256]");
   if (gevd && (rank < 1 || rank > kRMax || rank > D)) return fail(nullptr, "bad rank");
   if (ref < 0 || ref >= D) return fail(nullptr, "bad reference index");
+  if (D > kMaxDMax) {
+    // wide class (wide.hpp): one workgroup per bin, float64 workspace
+    // (stream-ordered, released behind the launches)
+    hipStream_t st = (hipStream_t)stream;
+    wide::WideArgs wa{};
+    wa.D = D; wa.rank = rank; wa.gevd = gevd; wa.F = 1; wa.nItems = B; wa.layout = 0;
+    wa.RyyD = (const cd*)Ryy; wa.Rnn = (const cd*)Rnn; wa.srcScene = (long long)D * D; wa.srcBin = 0;
+    wa.nOut = 1; wa.refs[0] = ref; wa.wOff[0] = 0; wa.w = (cf*)w; wa.wScene = D; wa.wBin = 0;
+    wa.diag = diag;
+    const long long chunk = std::min<long long>(B, 1024);
+    HIPCHK(hipMallocAsync((void**)&wa.work, (size_t)chunk * wide::work_elems(D) * sizeof(cd), st));
+    HIPCHK(wide::launch_wide_filters(wa, chunk, st));
+    HIPCHK(hipFreeAsync(wa.work, st));
+    return 0;
+  }
   int G, DM;
   pick_class(D, G, DM);
   hipStream_t st = (hipStream_t)stream;

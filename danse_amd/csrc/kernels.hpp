@@ -31,7 +31,9 @@ struct FamNode {
   int chanOff;        // offset into chanList
   int extMode;        // DANSE family only (else -1)
   int M;              // local mics of node k
-  int packed;         // SCM layout: 1 packed lower triangle [D(D+1)/2][F], 0 rows [F][D][D]
+  int packed;         // SCM layout (scm_lower): 1 packed lower triangles bin-minor [D(D+1)/2][F] (lane
+                      // classes), 2 packed lower triangles bin-major [F][D(D+1)/2] (D > 12), 0 rows
+                      // [F][D][D] (the D <= 12 grid classes of smallDGrid / the resident engine)
   long long scmOff;   // complex-element offset within one scene's SCM block
   long long wOff;     // complex-element offset within one scene's w-history block
   long long wExtOff;  // DANSE only: offset within one scene's wExt-history block
@@ -100,6 +102,17 @@ struct UpdateArgs {
 };
 
 DANSE_DEV bool node_in(unsigned mask, int k) { return ((mask >> k) & 1u) != 0u; }
+
+// Element (i, j), i >= j, of scene s's bin-f SCM of a family-node, in the
+// family-node's layout (FamNode.packed).  In the packed layouts only the lower
+// triangle exists: (j, i) is conj((i, j)), the diagonal is real.
+DANSE_DEV long long scm_lower(const FamNode& d, long long scmStride, int s, int F, int f, int i, int j) {
+  const long long b = (long long)s * scmStride + d.scmOff;
+  const int t = i * (i + 1) / 2 + j;
+  if (d.packed == 1) return b + (long long)t * F + f;
+  if (d.packed == 2) return b + (long long)f * (d.D * (d.D + 1) / 2) + t;
+  return b + ((long long)f * d.D + i) * d.D + j;
+}
 
 // Agent-coherent (sc1) 8-byte load / store of a complex value: the resident
 // engine's hand-offs between waves of one launch (payload stored sc1 and

@@ -29,10 +29,10 @@ namespace danse {
 //           round return at once, the solver is compiled out, so the launch
 //           is not held to the solver's register budget;
 //   SM = 2  the solving items only, launch item b / FG = solveItems[b / FG].
-// PK (with SM = 2): the SCMs of a lane class (packed lower triangles,
-// bin-minor, kernels_lane.hpp): the upper entries of a lane's blocks are the
+// SCMs: packed lower triangles (the upper entries of a lane's blocks are the
 // conjugates of the stored lower ones, only the lower ones are written back,
-// and the diagonals are kept real as the lane kernel keeps them.
+// the diagonals are kept real), bin-major; PK (with SM = 2): a lane class's
+// bin-minor triangles (kernels_lane.hpp).
 template <int NB, int RMAX, int G = 8, bool PK = false, int SM = 0>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NB <= 5 ? DANSE_2D_WPE : 1)))
 update_kernel_2d(const UpdateArgs a) {
@@ -94,18 +94,18 @@ update_kernel_2d(const UpdateArgs a) {
   });
   t2d::wsync();
   const double beta = a.beta[s * a.K + d.k];
-  const long long matOff = (long long)s * a.scmStride + d.scmOff + (long long)f * D * D;
-  // entry (i, c) of the SCM (both in range): full rows, or the packed lower
-  // triangle of the lane classes ([D(D+1)/2][F], bin-minor)
+  // entry (i, c) of the SCM (both in range): the stored lower entry (hi, lo)
+  // -- packed lower triangles, bin-major ([F][D(D+1)/2], FamNode.packed 2), or
+  // with PK the lane class's bin-minor [D(D+1)/2][F]; the upper entries are
+  // the conjugates of the stored lower ones
+  const long long triOff = PK ? (long long)s * a.scmStride + d.scmOff + f
+                              : (long long)s * a.scmStride + d.scmOff + (long long)f * (D * (D + 1) / 2);
   auto ent = [&](int i, int c) -> long long {
-    if constexpr (PK) {
-      const int hi = i >= c ? i : c, lo = i >= c ? c : i;
-      return (long long)s * a.scmStride + d.scmOff + (long long)(hi * (hi + 1) / 2 + lo) * F + f;
-    } else {
-      return matOff + (long long)i * D + c;
-    }
+    const int hi = i >= c ? i : c, lo = i >= c ? c : i;
+    const long long t = hi * (hi + 1) / 2 + lo;
+    return PK ? triOff + t * F : triOff + t;
   };
-  const long long safe = PK ? ent(0, 0) : matOff;   // (an in-bounds address for the padding entries)
+  const long long safe = triOff;   // (an in-bounds address for the padding entries)
 
   // ---- Rnn (float64): recursion, store, factor -> Li in S.Ls -------------
   bool ok = true;
@@ -120,17 +120,15 @@ update_kernel_2d(const UpdateArgs a) {
         const int i = p + G * sb, c = q + G * tb;
         const bool in = i < D && c < D;
         cd x = csel(in, a.Rnn[in ? ent(i, c) : safe], cd{0.0, 0.0});
-        if constexpr (PK) {
-          if (i < c) x = conjg(x);
-          if (i == c) x.im = 0.0;
-        }
+        if (i < c) x = conjg(x);
+        if (i == c) x.im = 0.0;
         if (opN) {
           cd yy = cd{0.0, 0.0};
           fma_cc(yy, cdk(yr[sb]), cdk(yc[tb]));
           x = cx * x;
           x.re = fma(cy, yy.re, x.re);
-          x.im = (PK && i == c) ? 0.0 : fma(cy, yy.im, x.im);
-          if (in && fvalid && (!PK || i >= c)) a.Rnn[ent(i, c)] = x;
+          x.im = (i == c) ? 0.0 : fma(cy, yy.im, x.im);
+          if (in && fvalid && i >= c) a.Rnn[ent(i, c)] = x;
         }
         M.v[sb][tb] = x;
       });
@@ -155,14 +153,12 @@ update_kernel_2d(const UpdateArgs a) {
         const int i = p + G * sb, c = q + G * tb;
         const bool in = i < D && c < D;
         cf x = csel(in, a.Ryy[in ? ent(i, c) : safe], cf{0.0f, 0.0f});
-        if constexpr (PK) {
-          if (i < c) x = conjg(x);
-        }
+        if (i < c) x = conjg(x);
         if (opY) {
           const cf yy = cy * mulc(yr[sb], yc[tb]);
           x = csel(opY == DANSE_OP_SET, yy, by * x + yy);
-          if (PK && i == c) x.im = 0.0f;
-          if (in && fvalid && (!PK || i >= c)) a.Ryy[ent(i, c)] = x;
+          if (i == c) x.im = 0.0f;
+          if (in && fvalid && i >= c) a.Ryy[ent(i, c)] = x;
         }
         A.v[sb][tb] = x;
       });

@@ -32,8 +32,13 @@ __global__ void __launch_bounds__(64) update_kernel_big(const UpdateArgs a) {
 
   const cf y = load_y(a, d, s, f, li, act);
   const double beta = a.beta[s * a.K + d.k];
-  const long long matOff = (long long)s * a.scmStride + d.scmOff + (long long)f * D * D;
+  // SCMs: packed lower triangles, bin-major (FamNode.packed 2): row li's
+  // entry c is (li, c) for c <= li, conj((c, li)) above the diagonal
+  const long long triOff = (long long)s * a.scmStride + d.scmOff + (long long)f * (D * (D + 1) / 2);
   const int rowc = act ? li : 0;
+  auto ent = [&](int c) -> long long {
+    return triOff + (c <= rowc ? rowc * (rowc + 1) / 2 + c : c * (c + 1) / 2 + rowc);
+  };
 
   // Ryy row in float32; Rnn row in float64
   Row<DMAX> A;
@@ -45,7 +50,9 @@ __global__ void __launch_bounds__(64) update_kernel_big(const UpdateArgs a) {
     cols_below<DMAX>(D, [&](auto cc) {
       constexpr int c = decltype(cc)::value;
       const int cl = (c < D) ? c : D - 1;
-      const cf v = a.Ryy[matOff + (long long)rowc * D + cl];
+      cf v = a.Ryy[ent(cl)];
+      if (cl > rowc) v = conjg(v);
+      if (cl == rowc) v.im = 0.0f;
       ws<c>(A, (act && c < D) ? v : cf{0.0f, 0.0f});
     });
   }
@@ -54,12 +61,14 @@ __global__ void __launch_bounds__(64) update_kernel_big(const UpdateArgs a) {
     cols_below<DMAX>(D, [&](auto cc) {
       constexpr int c = decltype(cc)::value;
       const cf yy = cy * mulc(y, rl(y, c));   // y = 0 on lanes >= D
-      ws<c>(A, (opY == DANSE_OP_SET) ? yy : by * rs<c>(A) + yy);
+      cf x = (opY == DANSE_OP_SET) ? yy : by * rs<c>(A) + yy;
+      if (c == li) x.im = 0.0f;
+      ws<c>(A, x);
     });
     if (act) {
       cols_below<DMAX>(D, [&](auto cc) {
         constexpr int c = decltype(cc)::value;
-        if (c < D) a.Ryy[matOff + (long long)li * D + c] = rs<c>(A);
+        if (c <= li) a.Ryy[ent(c)] = rs<c>(A);
       });
     }
   }
@@ -71,15 +80,17 @@ __global__ void __launch_bounds__(64) update_kernel_big(const UpdateArgs a) {
     cols_below<DMAX>(D, [&](auto cc) {
       constexpr int c = decltype(cc)::value;
       const int cl = (c < D) ? c : D - 1;
-      cd x = a.Rnn[matOff + (long long)rowc * D + cl];
+      cd x = a.Rnn[ent(cl)];
+      if (cl > rowc) x = conjg(x);
+      if (cl == rowc) x.im = 0.0;
       if (!(act && c < D)) x = cd{0.0, 0.0};
       if (opN) {
         cd yy = cd{0.0, 0.0};
         fma_cc(yy, yl, cdk(rl(y, c)));
         x = cx * x;
         x.re = fma(cy, yy.re, x.re);
-        x.im = fma(cy, yy.im, x.im);
-        if (act && c < D) a.Rnn[matOff + (long long)li * D + c] = x;
+        x.im = (c == li) ? 0.0 : fma(cy, yy.im, x.im);
+        if (act && c <= li) a.Rnn[ent(c)] = x;
       }
       wsd<c>(B, x);
     });

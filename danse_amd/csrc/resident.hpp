@@ -251,7 +251,12 @@ resident_kernel(const ResArgs ra) {
   const FamNode d = ra.fn[fni];
   const int D0 = d.D;
   const double beta = a.beta[s * K + d.k];
-  const long long matOff = (long long)s * a.scmStride + d.scmOff + (long long)f * D0 * D0;
+  // SCMs: packed lower triangles, bin-major (FamNode.packed 2); a lane's
+  // blocks above the diagonal start from the conjugates of the stored entries
+  const long long triOff = (long long)s * a.scmStride + d.scmOff + (long long)f * (D0 * (D0 + 1) / 2);
+  auto ent = [&](int i, int c) -> long long {
+    return triOff + (i >= c ? i * (i + 1) / 2 + c : c * (c + 1) / 2 + i);
+  };
   const int gateR = ra.gateRound ? ra.gateRound[s * ra.nFN + fni] : -1;
   const bool isDanse = d.fam == DANSE_FAM_DANSE;
 
@@ -264,8 +269,12 @@ resident_kernel(const ResArgs ra) {
       constexpr int tb = decltype(tc)::value;
       const int i = p0 + G * sb, c = q0 + G * tb;
       const bool in = i < D0 && c < D0;
-      Rn.v[sb][tb] = csel(in, a.Rnn[matOff + (in ? (long long)i * D0 + c : 0ll)], cd{0.0, 0.0});
-      Ry.v[sb][tb] = csel(in, a.Ryy[matOff + (in ? (long long)i * D0 + c : 0ll)], cf{0.0f, 0.0f});
+      cd xn = csel(in, a.Rnn[in ? ent(i, c) : triOff], cd{0.0, 0.0});
+      cf xy = csel(in, a.Ryy[in ? ent(i, c) : triOff], cf{0.0f, 0.0f});
+      if (i < c) { xn = conjg(xn); xy = conjg(xy); }
+      if (i == c) { xn.im = 0.0; xy.im = 0.0f; }
+      Rn.v[sb][tb] = xn;
+      Ry.v[sb][tb] = xy;
     });
   });
   bool liValid = false;     // S.Ls / S.g hold the factor of the current Rnn
@@ -352,9 +361,9 @@ resident_kernel(const ResArgs ra) {
         sfor<0, NB>([&](auto tc) {
           constexpr int tb = decltype(tc)::value;
           const int i = p + G * sb, c = q + G * tb;
-          if (i < D && c < D) {
-            ra.RnnG[matOff + (long long)i * D + c] = Rn.v[sb][tb];
-            ra.RyyG[matOff + (long long)i * D + c] = Ry.v[sb][tb];
+          if (i < D && c <= i) {
+            ra.RnnG[ent(i, c)] = Rn.v[sb][tb];
+            ra.RyyG[ent(i, c)] = Ry.v[sb][tb];
           }
         });
       });
@@ -449,9 +458,9 @@ resident_kernel(const ResArgs ra) {
       sfor<0, NB>([&](auto tc) {
         constexpr int tb = decltype(tc)::value;
         const int i = p0 + G * sb, c = q0 + G * tb;
-        if (i < D0 && c < D0) {
-          a.Rnn[matOff + (long long)i * D0 + c] = Rn.v[sb][tb];
-          a.Ryy[matOff + (long long)i * D0 + c] = Ry.v[sb][tb];
+        if (i < D0 && c <= i) {
+          a.Rnn[ent(i, c)] = Rn.v[sb][tb];
+          a.Ryy[ent(i, c)] = Ry.v[sb][tb];
         }
       });
     });

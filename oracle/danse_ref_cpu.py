@@ -205,6 +205,43 @@ def update_w_gevd(Ryy, Rnn, refSensorIdx, rank=1):
     return fullW[:, :, refSensorIdx]
 
 
+def update_w_gevd_refs(Ryy, Rnn, refs, rank=1):
+    """``update_w_gevd`` for several reference indices on the same SCMs (the
+    centralised filters of every node, ``d_batch.py:95-104``): the full
+    ``X D Q^H`` product is computed once and its columns picked, so each
+    result is bit-identical to a separate ``update_w_gevd`` call."""
+    n = Ryy.shape[-1]
+    nFreqs = Ryy.shape[0]
+    Xmat = np.zeros((nFreqs, n, n), dtype=complex)
+    sigma = np.zeros((nFreqs, n))
+    S, Xall = eigh_bins(Ryy, Rnn)
+    for kappa in range(nFreqs):
+        s, X = S[kappa], Xall[kappa]
+        idx = np.flip(np.argsort(s))
+        sigma[kappa, :] = s[idx]
+        Xmat[kappa] = X[:, idx]
+    Qmat = np.linalg.inv(np.transpose(Xmat.conj(), axes=[0, 2, 1]))
+    Dmat = np.zeros((nFreqs, n, n))
+    for r in range(rank):
+        Dmat[:, r, r] = np.squeeze(1 - 1 / sigma[:, r])
+    Qh = np.transpose(Qmat.conj(), axes=[0, 2, 1])
+    fullW = np.matmul(np.matmul(Xmat, Dmat), Qh)
+    return [fullW[:, :, r] for r in refs]
+
+
+def update_w_refs(Ryy, Rnn, refs, rank=None):
+    """``update_w`` for several reference indices (one inverse, bit-identical
+    per reference to separate calls)."""
+    Ryyinv = np.linalg.inv(Ryy)
+    out = []
+    for r in refs:
+        Evect = np.zeros(Ryy.shape[-1])
+        Evect[r] = 1
+        ryd = np.matmul(Ryy - Rnn, Evect)
+        out.append(np.matmul(Ryyinv, ryd[:, :, np.newaxis])[:, :, 0])
+    return out
+
+
 def update_covmats_batch(yAllFrames, vadAllFrames):
     """``d_classes.py:3272-3304``."""
     if len(vadAllFrames) > yAllFrames.shape[1]:
@@ -1097,7 +1134,6 @@ def batch_family_estimates(b, centr=True, local=True):
     vectors, stored in history slot i[k] + 1; estimates over all frames but
     the last, ISTFT / sum(win), and the untrimmed MMSE costs."""
     p = b.p
-    fn = update_w_gevd if p.performGEVD else update_w
     rank = p.GEVDrank if p.performGEVD else 1
     fi = dict(initType=p.filterInitType, fixedValue=p.filterInitFixedValue)
     K, F, Mt = b.K, b.F, int(sum(b.M))
@@ -1148,7 +1184,6 @@ def get_best_perf(scene, p, wCentr=None, vadMinProp=0.5):
     elif pg.active and pg.purpose == 'speech-only':
         b.yin = [nd.cleanspeech for nd in scene.wasn]
     b.yinSTFT = [get_stft(b.yin[k], b.fs[k], b.win, 1 - b.Ns / b.N) * np.sum(b.win) for k in range(b.K)]
-    fn = update_w_gevd if p.performGEVD else update_w
     rank = p.GEVDrank if p.performGEVD else 1
     fi = dict(initType=p.filterInitType, fixedValue=p.filterInitFixedValue)
     K, F, Mt = b.K, b.F, int(sum(b.M))
@@ -1159,11 +1194,15 @@ def get_best_perf(scene, p, wCentr=None, vadMinProp=0.5):
     b.dHatCentr = np.zeros((F, b.nIter, K), dtype=complex)
     nseg = b.yCentrBatch.shape[1]
     idx = np.arange(nseg) if nseg == b.nIter else np.arange(nseg - 1)
+    if wCentr is None:
+        # (every node's call sees the same SCMs: one decomposition, the
+        # references' columns -- bit-identical to K separate calls of fn)
+        fnR = update_w_gevd_refs if p.performGEVD else update_w_refs
+        wK = fnR(b.Ryycentr, b.Rnncentr, [int(np.sum(b.M[:k]) + p.referenceSensor) for k in range(K)], rank=rank)
     for k in range(K):
         i = b.i[k]
         if wCentr is None:
-            b.wCentr[k][:, i + 1, :] = fn(b.Ryycentr, b.Rnncentr,
-                                          refSensorIdx=int(np.sum(b.M[:k]) + p.referenceSensor), rank=rank)
+            b.wCentr[k][:, i + 1, :] = wK[k]
         else:
             b.wCentr[k][:, i + 1, :] = wCentr[k][:, i + 1, :]
         b.dHatCentr[:, :, k] = np.einsum('ik,ijk->ij', b.wCentr[k][:, i + 1, :].conj(), b.yCentrBatch[:, idx, :])

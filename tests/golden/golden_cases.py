@@ -158,6 +158,11 @@ SRO_EVENT_CASES = [
 KAT_CASES = [dict(name=f'kat_{"gevd" if g else "mwf"}_D{D}_r{r}', D=D, F=48, gevd=g, rank=r, ref=0, seed=100 + D + r)
              for (D, g, r) in [(2, True, 1), (11, True, 1), (11, True, 2), (19, True, 1), (39, True, 1),
                                (2, False, 1), (11, False, 1), (39, False, 1)]]
+# the wide classes (64 < D <= 256: centralised estimates at sum(M) up to 256;
+# kat_inputs takes ~25 s at D = 256, F = 8)
+KAT_CASES += [dict(name=f'kat_{"gevd" if g else "mwf"}_D{D}_r{r}', D=D, F=F, gevd=g, rank=r, ref=ref, seed=100 + D + r)
+              for (D, g, r, F, ref) in [(96, True, 1, 48, 0), (96, True, 2, 48, 5), (256, True, 1, 8, 0),
+                                        (96, False, 1, 48, 3), (256, False, 1, 8, 0)]]
 
 
 def kat_inputs(case):

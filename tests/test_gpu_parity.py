@@ -275,6 +275,40 @@ def test_best_perf_vs_oracle(case, golden_dir):
         assert e <= 1e-4, (purpose, e)
 
 
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize('M', [[8] * 12, [8] * 32], ids=['sumM96', 'sumM256'])
+def test_best_perf_wide_vs_oracle(M):
+    """get_best_perf at sum(M) > 64 (config D's K = 32 x 8 gives sum(M) =
+    256): the wide classes (csrc/wide.hpp: float64 HERK on MFMA, one
+    workgroup per bin for Cholesky, congruence, tridiagonalisation,
+    multisection and inverse iteration) against the float64 oracle, whose
+    get_best_perf is pinned to the reference's fixtures at K = 3 / 4
+    (bestperf_*; the wide KATs pin the filter update itself at D = 96 / 256)."""
+    from danse_amd import core
+    from oracle import danse_ref_cpu as O
+    from golden_cases import BATTERY
+    case = dict(name=f'bestperf_wide_{sum(M)}', M=M, dur=3.01, seed=62 + len(M),
+                danse=dict(BATTERY, nodeUpdating='asy', simType='batch'))
+    sc = make_case_scene(case)
+    dp, wp = make_case_params(case)
+    sc.get_vad_per_frame(dp.DFTsize, dp.Ns, wp.vadMinProportionActive)
+    bp = core.get_best_perf(sc, dp)
+    O.set_workers(8)
+    try:
+        ob = O.get_best_perf(sc, dp, vadMinProp=wp.vadMinProportionActive)
+    finally:
+        O.set_workers(0)
+    K = len(M)
+    assert bp.wCentr[0].shape[-1] == sum(M)
+    st = _stats(np.concatenate([_bin_rel(bp.wCentr[k][:, 1, :], ob.wCentr[k][:, 1, :]).ravel() for k in range(K)]))
+    de = rel_err(bp.dCentr, ob.dCentr)
+    cr = np.array(ob.mmseCostCentr, dtype=float)
+    ce = float(np.max(np.abs(np.array(bp.mmseCostCentr) - cr) / np.abs(cr)))
+    print(case['name'], 'w', st, 'd', de, 'cost', ce)
+    assert st['median'] <= 1e-5 and st['p99'] <= 1e-4, st
+    assert de <= 1e-4 and ce <= 1e-4
+
+
 def test_batch_covmats_op():
     """danse_batch_covmats (MFMA HERK) on random observations vs numpy."""
     L, lib = _lib()
