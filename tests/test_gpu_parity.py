@@ -82,7 +82,10 @@ def test_filter_update_kat(case, golden_dir):
     # generalized eigensolver for GEVD) on the same inputs; the device's
     # mixed-precision update (float64 factorisation of Rnn) beats it and is
     # held to the north-star tolerance itself
-    st32 = _stats(_bin_rel(_lapack_fp32_filters(Ryy, Rnn, case), g['w']))
+    try:
+        st32 = _stats(_bin_rel(_lapack_fp32_filters(Ryy, Rnn, case), g['w']))
+    except np.linalg.LinAlgError:   # (single-precision LAPACK: Rnn not positive definite at D = 256)
+        st32 = None
     print(case['name'], st, 'lapack-fp32', st32)
     assert int(diag.sum()) == 0
     assert st['median'] <= 1e-5 and st['p99'] <= 1e-4, (st, st32)
@@ -287,9 +290,13 @@ def test_best_perf_wide_vs_oracle(M):
     from danse_amd import core
     from oracle import danse_ref_cpu as O
     from golden_cases import BATTERY
-    case = dict(name=f'bestperf_wide_{sum(M)}', M=M, dur=3.01, seed=62 + len(M),
+    # the centralised VAD is active when any node's is (d_classes.py:905-911):
+    # with 12-32 nodes and the default 0.5 s pauses fewer frames than sum(M)
+    # are noise-only and Rnn is singular (the reference's eigh raises too), so
+    # the desired source pauses 1.5 s: 198 of 312 / 317 of 500 frames noise-only
+    case = dict(name=f'bestperf_wide_{sum(M)}', M=M, dur=10.01 if sum(M) <= 96 else 16.01, seed=62 + len(M),
                 danse=dict(BATTERY, nodeUpdating='asy', simType='batch'))
-    sc = make_case_scene(case)
+    sc = make_case_scene(case, pauseDuration=1.5)
     dp, wp = make_case_params(case)
     sc.get_vad_per_frame(dp.DFTsize, dp.Ns, wp.vadMinProportionActive)
     bp = core.get_best_perf(sc, dp)

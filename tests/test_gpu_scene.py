@@ -86,6 +86,8 @@ def test_scene_conv_vad_vs_reference(golden_dir):
     # the VAD kernel alone: identity IR on the float32-rounded reference signals
     _, v32 = convolve_vad(wet[ref].astype(np.float32), np.ones((len(ref), 1), np.float32), **kw)
     print('wet rel err', err, 'VAD mismatch (device wet)', mism, 'active', float(g['vad'].mean()))
-    assert err <= 2e-6, err
+    # (float32 accumulation over the 3200-tap IRs: ~sqrt(nIR) 2^-24 = 3.4e-6
+    # of the peak; measured 2.8e-6 on MI355X)
+    assert err <= 1e-5, err
     assert np.array_equal(v32, g['vad32'])
     assert mism <= 1e-3, mism
