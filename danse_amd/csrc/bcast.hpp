@@ -3,19 +3,20 @@
 // synthesis of z and of the estimates, and the analysis of the z frame that
 // every receiving node uses.  Host translation unit only (danse_engine.hip).
 //
-// One 256-thread workgroup per (scene, node); every 1024-point FFT is owned
-// by ONE wavefront (wfft.hpp), so the four waves run independent transforms
+// One workgroup of 4 or 8 waves per (scene, node); every 1024-point FFT is
+// owned by ONE wavefront (wfft.hpp), so the waves run independent transforms
 // side by side:
 //   phase 1  the broadcast-frame analyses of the node's M mics (and the
 //            update-frame analyses when the update frame is not the previous
 //            broadcast frame), round-robin over the waves; each wave keeps
 //            its partial sum of conj(wExt) yhat in registers;
-//   phase 2  wave 0: fused spectrum = sum of the partials (fixed order),
+//   phase 2  wave 0: fused spectrum = sum of the wave partials (wave order),
 //            z synthesis + OLA normalisation (d_base.py:1759-1868), stream
 //            append (fill_buffers, d_classes.py:1185-1224) and the analysis of
 //            the z frame the receivers consume (d_classes.py:1701-1807,
 //            1893-1934); waves 1..3: synthesis of the previous round's
 //            estimates (get_desired_sig_chunk, d_base.py:2027-2084).
+//            waves 1..NW-1 take the families round-robin.
 #pragma once
 #include "fft.hpp"
 #include "kernels.hpp"
@@ -23,7 +24,11 @@
 
 namespace danse {
 
-constexpr int kBcWaves = 4;
+constexpr int kBcWaves = 4;   // waves per (scene, node) of the resident broadcast / the default bcast_kernel
+// bcast_kernel's waves per workgroup: 8 when S K <= 128 workgroups would
+// leave most CUs idle (N2: 32, config C: 128), else 4 (decided on the global
+// S K so that node-sharded engines sum the fused spectra in the same order)
+inline int bcast_waves(int S, int K) { return S * K <= 128 ? 8 : 4; }
 
 struct BcastArgs {
   int S, K, MT, T, N, Ns, F, R;
@@ -100,9 +105,12 @@ DANSE_DEV cf herm_ext_conj(const cf* __restrict__ X, int n, int F) {
 }
 
 #ifndef DANSE_BCAST_HELPERS_ONLY   // resident.hip uses the helpers above, not the kernel
-__global__ void __launch_bounds__(256) bcast_kernel(const BcastArgs a) {
-  __shared__ cf fftLds[kBcWaves][wfft::kLdsElems];
-  __shared__ cf part[kBcWaves][513];
+// NW waves per (scene, node): 4, or 8 when the grid is small (few scenes x
+// nodes: one analysis per wave instead of two; bcast_waves)
+template <int NW>
+__global__ void __launch_bounds__(NW * 64) bcast_kernel(const BcastArgs a) {
+  __shared__ cf fftLds[NW][wfft::kLdsElems];
+  __shared__ cf part[NW][513];
   __shared__ float zq[1024];
   const int wv = threadIdx.x >> 6;
   const int N = a.N, Ns = a.Ns, F = a.F;
@@ -136,7 +144,7 @@ __global__ void __launch_bounds__(256) bcast_kernel(const BcastArgs a) {
     const int nBc = a.zOnly ? 0 : Mk;
     const int nUp = (needUp && !a.zOnly) ? Mk : 0;
     const int nJobs = nBc + nUp + ((a.cEnd && zk) ? Mk : 0);
-    for (int j = wv; j < nJobs; j += kBcWaves) {
+    for (int j = wv; j < nJobs; j += NW) {
       const int kind = (j < nBc) ? 0 : (j < nBc + nUp ? 1 : 2);
       const bool up = kind == 1;
       const int m = j - (kind == 0 ? 0 : (kind == 1 ? nBc : nBc + nUp));
@@ -206,7 +214,7 @@ __global__ void __launch_bounds__(256) bcast_kernel(const BcastArgs a) {
       const int nn = (n < F) ? n : N - n;
       cf z = part[0][nn];
 #pragma unroll
-      for (int w = 1; w < kBcWaves; ++w) z = z + part[w][nn];
+      for (int w = 1; w < NW; ++w) z = z + part[w][nn];
       if (nn == 0 || nn == F - 1) z.im = 0.0f;
       v[j] = (n < F) ? conjg(z) : z;
     }
@@ -262,7 +270,7 @@ __global__ void __launch_bounds__(256) bcast_kernel(const BcastArgs a) {
     const int rp = r - 1;
     const int end = a.upEnd[rp * a.K + k];
     const int w0 = a.doBcast ? 1 : 0;
-    const int nW = kBcWaves - w0;
+    const int nW = NW - w0;
     int job = 0;
     for (int fam = 0; fam < kMaxFam; ++fam) {
       if (!((a.families >> fam) & 1)) continue;

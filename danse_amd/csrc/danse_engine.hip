@@ -100,6 +100,8 @@ struct danse_engine {
   long long liStride = 0;
   cf* vCache = nullptr;      // lane-grid GEVD classes: eigenvector of C per bin (warm start)
   long long vStride = 0;
+  cd* l64Cache = nullptr;    // lane-grid GEVD classes: float64 factor record per bin (rank-one updates)
+  long long l64Stride = 0;
   int scmPerBin = 0;   // dScm0 holds [F][D][D] per family-node (else [D][D])
   FamNode* dFnAll = nullptr;
   long long *dInitW0Off = nullptr, *dInitScmOff = nullptr, *dExtSrcOff = nullptr, *dTgtOff = nullptr;
@@ -520,7 +522,7 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
   // ---- family-node table (owned nodes), channel lists; with cEnd the other
   // nodes' channels of the centralised / SSBC vectors are raw-frame codes
   // (MT + K + channel, kernels.hpp load_y)
-  long long scmOff = 0, wOff = 0, liOff = 0, vOff = 0;
+  long long scmOff = 0, wOff = 0, liOff = 0, vOff = 0, l64Off = 0;
   // warm-started rank-1 Lanczos on the lane-grid classes (DANSE_NO_WARM=1: off)
   const bool warm = c->gevd && c->rank == 1 && !std::getenv("DANSE_NO_WARM");
   const int rawBase = mt + K;
@@ -567,6 +569,16 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
       else if (c->gevd && gridSmall) liOff += (long long)F * class_li_record(16);
       else if (c->gevd && class_grid(class_dmax(fn.D)) > 0) liOff += (long long)F * class_li_record(class_dmax(fn.D));
       fn.vOff = -1;
+      fn.l64Off = -1;
+      // float64 factor records (li_rank1_2d) of the one-bin-per-wave grid
+      // classes (DMAX 24-48; at G = 4, DMAX <= 20, the O(D^3) factor is short
+      // and the update measured slower: C 360 -> 372 us, N2 263 -> 255 us)
+      if (c->gevd && fn.packed == 2 && !gridSmall && class_grid(class_dmax(fn.D)) > 0 &&
+          class_dmax(fn.D) >= 24 && !std::getenv("DANSE_NO_R1")) {
+        const int DMr = class_dmax(fn.D);
+        fn.l64Off = l64Off;
+        l64Off += (long long)F * (DMr * (DMr + 1) / 2 + DMr);
+      }
       // (grid classes of 20 and more: solver2d.hpp gevd2d_filter)
       if (warm && fn.packed == 2 && !gridSmall && class_grid(class_dmax(fn.D)) > 0 && class_dmax(fn.D) >= 20) {
         fn.vOff = vOff;
@@ -579,6 +591,7 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
   eng->wStride = wOff;
   eng->liStride = liOff;
   eng->vStride = vOff;
+  eng->l64Stride = l64Off;
   eng->wExtNodeOff.assign(K, 0);
   long long eo = 0, to = 0;
   for (int k = 0; k < K; ++k) {
@@ -735,6 +748,7 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
   HIPCHK(dalloc(&eng->diag, (size_t)S * K * kMaxFam));
   if (eng->liStride > 0) HIPCHK(dalloc(&eng->liCache, (size_t)S * eng->liStride));
   if (eng->vStride > 0) HIPCHK(dalloc(&eng->vCache, (size_t)S * eng->vStride));
+  if (eng->l64Stride > 0) HIPCHK(dalloc(&eng->l64Cache, (size_t)S * eng->l64Stride));
   if (c->dxcp) {
     if (c->cohDrift) return fail(eng, "DXCP-PhaT and CohDrift estimation are exclusive");
     if (c->fsTab) return fail(eng, "DXCP-PhaT estimation runs on wholeChunk broadcasts");
@@ -865,7 +879,7 @@ void danse_engine_destroy(danse_engine* eng) {
                   eng->dxEst, eng->resYB, eng->resYU, eng->resZall, eng->resZhat, eng->resRyyG, eng->resRnnG,
                   eng->resUFlag, eng->resZFlag, eng->resGateRound, eng->resDanseFni, eng->resErr, eng->resFams,
                   eng->resFrames, eng->resChanNode, eng->resTrace, eng->condHist, eng->dxRecFrames,
-                  eng->dxRecOut, eng->dFsEv, eng->rawStream, eng->vCache};
+                  eng->dxRecOut, eng->dFsEv, eng->rawStream, eng->vCache, eng->l64Cache};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (eng->dx) danse_dxcp_destroy(eng->dx);
@@ -913,6 +927,7 @@ static UpdateArgs make_update(danse_engine* e, int r) {
   a.betaExt = e->dBetaExt; a.alphaExt = e->alphaExt; a.gevd = e->gevd; a.rank = e->rank; a.diag = e->diag;
   a.liCache = e->liCache; a.liStride = e->liStride;
   a.vCache = e->vCache; a.vStride = e->vStride;
+  a.l64Cache = e->l64Cache; a.l64Stride = e->l64Stride;
   a.cdPhase = e->cdPhase;
   a.Cspec = e->Cspec; a.chanNode = e->dChanNode; a.cPhase = e->dCPhase;
   a.nodeMask = ~0u;
@@ -1006,7 +1021,8 @@ static void launch_bcast(danse_engine* e, int r, int synth, int bc, hipStream_t 
   a.zMask = zMask;
   a.zOnly = zOnly;
   const unsigned grid = (unsigned)(e->S * (e->k1 - e->k0));
-  hipLaunchKernelGGL(bcast_kernel, dim3(grid), dim3(256), 0, st, a);
+  if (bcast_waves(e->S, e->K) == 8) hipLaunchKernelGGL(bcast_kernel<8>, dim3(grid), dim3(512), 0, st, a);
+  else hipLaunchKernelGGL(bcast_kernel<4>, dim3(grid), dim3(256), 0, st, a);
 }
 
 // the installed speculative gate candidates of round r (danse_engine_set_gate)
@@ -1282,7 +1298,8 @@ int danse_engine_run_resident(danse_engine* eng, void* stream) {
   {
     BcastArgs b = make_bcast(eng, 0, 0, 1);
     b.Zspec = eng->resZall + (size_t)K * S * F;
-    hipLaunchKernelGGL(bcast_kernel, dim3((unsigned)(S * K)), dim3(256), 0, st, b);
+    // (four waves: the resident kernel's own broadcasts sum the fused spectra in that order)
+    hipLaunchKernelGGL(bcast_kernel<4>, dim3((unsigned)(S * K)), dim3(256), 0, st, b);
     HIPCHK(hipGetLastError());
   }
   if (resident_launch(NB, eng->rank == 1, ra, grid, st, false, &fits) != 0) return fail(eng, "resident launch failed");

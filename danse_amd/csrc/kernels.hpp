@@ -40,6 +40,7 @@ struct FamNode {
   long long tgtOff;   // DANSE only: offset within one scene's target block
   long long liOff;    // lane classes, GEVD: offset of the factor cache (Li, g) within one scene's block
   long long vOff;     // lane-grid classes, GEVD: offset of the eigenvector cache (solver2d.hpp lanczos2d), -1 none
+  long long l64Off;   // lane-grid classes, GEVD: offset of the float64 factor record (solver2d.hpp li_rank1_2d), -1 none
 };
 
 struct UpdateArgs {
@@ -99,6 +100,12 @@ struct UpdateArgs {
   // vStride), the warm start of the rank-1 Lanczos path; null = off
   cf* vCache;
   long long vStride;
+  // lane-grid GEVD classes: per bin the float64 factor of the last
+  // factorisation (Li packed + row ref of L, [F][l64_record] per family-node
+  // at FamNode.l64Off, per scene stride l64Stride): a solve one noise frame
+  // after it updates it by rank one instead of refactoring; null = off
+  cd* l64Cache;
+  long long l64Stride;
 };
 
 DANSE_DEV bool node_in(unsigned mask, int k) { return ((mask >> k) & 1u) != 0u; }
@@ -154,6 +161,19 @@ DANSE_DEV cf sro_rotate(cf v, int f, int F, double ph) {
 constexpr int kLiScan = 64;
 DANSE_DEV bool li_reusable(const UpdateArgs& a, const FamNode& d, int s, int opN) {
   if (!a.liCache || opN != DANSE_OP_KEEP) return false;
+  for (int rr = a.r - 1; rr >= 0 && rr >= a.r - kLiScan; --rr) {
+    const uint8_t f2 = a.flags[(((long long)rr * a.S + s) * kMaxFam + d.fam) * a.K + d.k];
+    if ((f2 & DANSE_FLAG_SOLVE) && !(f2 & DANSE_FLAG_PREGIVEN)) return true;
+    if (((f2 >> 2) & 3) != DANSE_OP_KEEP) return false;
+  }
+  return false;
+}
+
+// The float64 factor record of the last solve is the factor of Rnn before
+// this round's single rank-one update (opN == AVG; every round since that
+// solve left Rnn alone): solver2d.hpp li_rank1_2d moves it to this round's.
+DANSE_DEV bool li_updatable(const UpdateArgs& a, const FamNode& d, int s, int opN) {
+  if (!a.l64Cache || d.l64Off < 0 || opN != DANSE_OP_AVG) return false;
   for (int rr = a.r - 1; rr >= 0 && rr >= a.r - kLiScan; --rr) {
     const uint8_t f2 = a.flags[(((long long)rr * a.S + s) * kMaxFam + d.fam) * a.K + d.k];
     if ((f2 & DANSE_FLAG_SOLVE) && !(f2 & DANSE_FLAG_PREGIVEN)) return true;

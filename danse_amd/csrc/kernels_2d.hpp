@@ -73,6 +73,11 @@ update_kernel_2d(const UpdateArgs a) {
   // and g (solver2d.hpp li_record / li_store2d)
   const bool reuse = solve && li_reusable(a, d, s, opN);
   cf* liC = a.liCache ? a.liCache + (long long)s * a.liStride + d.liOff + (long long)f * li_record<NB, G>() : nullptr;
+  // float64 factor record (solver2d.hpp li_rank1_2d): a solve one noise
+  // frame after the last factorisation updates it by rank one
+  cd* l64 = (!PK && SM == 0 && a.l64Cache && d.l64Off >= 0)
+                ? a.l64Cache + (long long)s * a.l64Stride + d.l64Off + (long long)f * l64_record<NB, G>()
+                : nullptr;
   // eigenvector cache of the warm-started rank-1 path (solver2d.hpp lanczos2d)
   cf* vC = (!PK && SM == 0 && a.vCache && d.vOff >= 0)
                ? a.vCache + (long long)s * a.vStride + d.vOff + (long long)f * (G * NB)
@@ -134,7 +139,11 @@ update_kernel_2d(const UpdateArgs a) {
       });
     });
     if (solve && !reuse) {
-      ok = gevd2d_factor<NB, G>(M, S, li, D, d.ref);
+      if (l64 && beta > 0.0 && li_updatable(a, d, s, opN)) {
+        ok = li_rank1_2d<NB, G>(S, li, yc, beta, cy, l64, fvalid);
+      } else {
+        ok = gevd2d_factor<NB, G>(M, S, li, D, d.ref, fvalid ? l64 : nullptr);
+      }
       if (liC && fvalid) li_store2d<NB, G>(S, liC, li);
     }
   }

@@ -44,6 +44,19 @@ template <int NB>
 struct Blk {
   cf v[NB][NB];
 };
+DANSE_DEV cd cmulx2(cd a, cd b) { return cd{a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re}; }
+// complex double to / from global memory as two doubles (a struct copy of a
+// register-array element becomes a memcpy from its address, which moves the
+// whole array to scratch)
+DANSE_DEV void st_cd(cd* p, cd v) {
+  double* o = reinterpret_cast<double*>(p);
+  o[0] = v.re;
+  o[1] = v.im;
+}
+DANSE_DEV cd ld_cd(const cd* p) {
+  const double* o = reinterpret_cast<const double*>(p);
+  return cd{o[0], o[1]};
+}
 
 // LDS of one bin.  The float64 factor phase, the congruence and the float32
 // phases never overlap, so their scratch shares one union; inside the
@@ -279,9 +292,181 @@ DANSE_DEV void trinv2d(BlkD<NB>& M, LDS2<NB, G>& S, int li, int D) {
   });
 }
 
+// ---- float64 factor record (kernels.hpp li_updatable): Li packed by
+// columns (ls_col order) + g64 = conj(L[ref][:]) = L^H e_ref, DM entries
+template <int NB, int G = 8>
+constexpr int l64_record() { return G * NB * (G * NB + 1) / 2 + G * NB; }
+template <int NB, int G = 8>
+DANSE_DEV void l64_store2d(const BlkD<NB>& M, cd* l64, int li) {
+  constexpr int DM = G * NB;
+  const int p = li / G, q = li % G;
+  sfor<0, NB>([&](auto tc) {
+    constexpr int t = decltype(tc)::value;
+    const int c = q + G * t;
+    const int col = ls_col<DM>(c) - c;
+    sfor<t, NB>([&](auto sc) {
+      constexpr int s = decltype(sc)::value;
+      const int i = p + G * s;
+      if (s > t || i >= c) st_cd(l64 + col + i, M.v[s][t]);
+    });
+  });
+}
+// scans over the lanes of a bin (float64): inclusive prefix over the row
+// groups p' <= p (lanes q + G p'), and the suffix over q' >= q inside the row
+// group
+template <int G>
+DANSE_DEV double scan_p(double x, int p) {
+#pragma unroll
+  for (int o = 1; o < G; o <<= 1) {
+    const double u = __shfl_up(x, o * G, G * G);
+    if (p >= o) x += u;
+  }
+  return x;
+}
+template <int G>
+DANSE_DEV double scan_q_down(double x, int q) {
+#pragma unroll
+  for (int o = 1; o < G; o <<= 1) {
+    const double u = __shfl_down(x, o, G);
+    if (q + o < G) x += u;
+  }
+  return x;
+}
+
+// ---- rank-one update of the float64 factor (a noise frame one solve after
+// the last factorisation): Rnn' = beta Rnn + cy y y^H.  With L the Cholesky
+// factor of Rnn, Li = L^-1, p = Li y and alpha = cy / beta,
+//   L' = sqrt(beta) L Mf,   Mf Mf^H = I + alpha p p^H,
+// whose factor has closed forms (t_0 = 1, t_(i+1) = t_i + alpha |p_i|^2):
+//   Mf[c][c] = sqrt(t_(c+1) / t_c),  Mf[k][c] = alpha p_k conj(p_c) / sqrt(t_c t_(c+1))  (k > c),
+//   Mf^-1[i][i] = sqrt(t_i / t_(i+1)),  Mf^-1[i][k] = -alpha p_i conj(p_k) / sqrt(t_i t_(i+1))  (k < i), so
+//   Li'[i][c] = (sqrt(t_i / t_(i+1)) Li[i][c] - alpha p_i / sqrt(t_i t_(i+1)) P[i][c]) / sqrt(beta),
+//     P[i][c] = sum_(k < i) conj(p_k) Li[k][c]          (a column prefix sum)
+//   L'[ref][c] = sqrt(beta) (sqrt(t_(c+1) / t_c) L[ref][c]
+//                + alpha conj(p_c) / sqrt(t_c t_(c+1)) sum_(c < k <= ref) L[ref][k] p_k)
+// O(D^2) with running sums (LDS, shuffles), instead of the O(D^3) Cholesky and
+// inverse (alpha > 0: an update, the stable direction).  The record l64 holds
+// Li and g64 = conj(L[ref][:]) on entry and (store) this frame's on exit;
+// Li' (float32) and g go to S.Ls / S.g as gevd2d_factor leaves them.
+template <int NB, int G = 8>
+DANSE_DEV bool li_rank1_2d(LDS2<NB, G>& S, int li, const cf (&yc)[NB], double beta, double cy, cd* l64,
+                           bool store) {
+  constexpr int DM = G * NB, L = bin_lanes<G>(), V = vpl<NB, G>();
+  const int p = li / G, q = li % G;
+  const double alpha = cy / beta;
+  double* av = S.invd;    // a_i = alpha |p_i|^2
+  cd* pv = S.rb64[0];     // p_i
+  // Li entry (p + G sb, q + G t) of the record (zero above the diagonal):
+  // the blocks are streamed from the record (L2) as they are needed, never
+  // all held in registers (the register budget of the 2 waves / SIMD kernel)
+  auto li_at = [&](int sb, int t) -> cd {
+    const int i = p + G * sb, c = q + G * t;
+    const bool lo = sb > t || (sb == t && i >= c);
+    return csel(lo, ld_cd(l64 + (lo ? ls_col<DM>(c) - c + i : 0)), cd{0.0, 0.0});
+  };
+  // p_i (to LDS: pv[i], and a_i in av[i])
+  sfor<0, NB>([&](auto sc) {
+    constexpr int sb = decltype(sc)::value;
+    cd acc = cd{0.0, 0.0};
+    sfor<0, sb + 1>([&](auto tc) { fma_c(acc, li_at(sb, decltype(tc)::value), cdk(yc[decltype(tc)::value])); });
+    const cd pi = sumq<G>(acc);
+    if (q == 0) {
+      av[p + G * sb] = alpha * (pi.re * pi.re + pi.im * pi.im);
+      pv[p + G * sb] = pi;
+    }
+  });
+  wsync();
+  // t_i = 1 + sum_(k < i) a_k (exclusive prefix) of this lane's rows, in the
+  // row order i = p + G s: a scan over the row groups plus the carry over the
+  // block rows
+  double tlo[NB];
+  {
+    double carry = 1.0;
+    sfor<0, NB>([&](auto sc) {
+      constexpr int sb = decltype(sc)::value;
+      const double a = av[p + G * sb];
+      const double inc = scan_p<G>(a, p);
+      tlo[sb] = carry + (inc - a);
+      carry += __shfl(inc, (G - 1) * G + q, G * G);
+    });
+  }
+  // Li' block row by block row: P[i][c] = sum_(k < i) conj(p_k) Li[k][c],
+  // a prefix over the row groups of the block row (shuffles) plus the earlier
+  // block rows' column sums carried in carP
+  const double rb = 1.0 / sqrt(beta);
+  {
+    cd carP[NB];
+    sfor<0, NB>([&](auto tc) { carP[decltype(tc)::value] = cd{0.0, 0.0}; });
+    sfor<0, NB>([&](auto sc) {
+      constexpr int sb = decltype(sc)::value;
+      const cd ps = pv[p + G * sb];
+      const double thi = tlo[sb] + av[p + G * sb];
+      const double dd = sqrt(tlo[sb] / thi);
+      const cd pe = (alpha / sqrt(tlo[sb] * thi)) * ps;
+      sfor<0, sb + 1>([&](auto tc) {   // (blocks right of the diagonal block are zero)
+        constexpr int t = decltype(tc)::value;
+        const int c = q + G * t;
+        const cd m = li_at(sb, t);
+        const cd u = cd{ps.re * m.re + ps.im * m.im, ps.re * m.im - ps.im * m.re};   // conj(p_i) Li[i][c]
+        // prefix over the row groups of this block row (lanes q + G p', p' < p)
+        const double ire = scan_p<G>(u.re, p), iim = scan_p<G>(u.im, p);
+        const double tre = __shfl(ire, (G - 1) * G + q, G * G), tim = __shfl(iim, (G - 1) * G + q, G * G);
+        const cd ex = cd{carP[t].re + (ire - u.re), carP[t].im + (iim - u.im)};
+        carP[t] = cd{carP[t].re + tre, carP[t].im + tim};
+        cd x = dd * m;
+        fms_c(x, pe, ex);
+        x = rb * x;
+        // float32 Li where gevd2d_factor leaves it (S.Ls), float64 record
+        // (this block row's old entries were all read above)
+        const int i = p + G * sb;
+        if (sb > t || i >= c) {
+          S.Ls[ls_col<DM>(c) - c + i] = cfk(x);
+          if (store) st_cd(l64 + ls_col<DM>(c) - c + i, x);
+        }
+      });
+    });
+  }
+  const double tN = tlo[NB - 1] + av[p + G * (NB - 1)];
+  // row ref of L (its record entries are read and rewritten here):
+  // L'[ref][c] = sqrt(beta) (sqrt(t_(c+1) / t_c) L[ref][c] + alpha conj(p_c) / sqrt(t_c t_(c+1)) sum_(k > c) L[ref][k] p_k)
+  // column c = q + G t: t_c, t_(c+1) from row group q (block t), the suffix
+  // sum over the columns by a scan inside the row group plus the carry over
+  // the blocks (descending)
+  {
+    const double sbeta = sqrt(beta);
+    double czr = 0.0, czi = 0.0;
+    sfor_down<NB, 0>([&](auto tc) {
+      constexpr int t = decltype(tc)::value;
+      const int c = q + G * t;
+      const double t0 = __shfl(tlo[t], G * q, G * G);
+      const double t1 = t0 + av[c];
+      const cd pc = pv[c];
+      const cd lr = conjg(ld_cd(l64 + DM * (DM + 1) / 2 + c));   // L[ref][c]
+      const cd z = cmulx2(lr, pc);
+      const double sre = scan_q_down<G>(z.re, q), sim = scan_q_down<G>(z.im, q);
+      const cd sfx = cd{czr + (sre - z.re), czi + (sim - z.im)};   // sum_(k > c) L[ref][k] p_k
+      czr += __shfl(sre, 0, G);
+      czi += __shfl(sim, 0, G);
+      cd x = sqrt(t1 / t0) * lr;
+      fma_c(x, (alpha / sqrt(t0 * t1)) * conjg(pc), sfx);
+      const cd g = conjg(sbeta * x);
+      if (p == 0) {
+        S.g[c] = cfk(g);
+        if (store) st_cd(l64 + DM * (DM + 1) / 2 + c, g);
+      }
+    });
+    sfor<0, V>([&](auto vc) {
+      const int i = li + L * decltype(vc)::value;
+      if (i >= DM) S.g[i] = cf{0.0f, 0.0f};
+    });
+  }
+  wsync();
+  return tN > 0.0 && tN < 1e300;
+}
+
 // ---- phase 1: Rnn block (float64, destroyed) -> Li (float32, S.Ls), g in LDS
 template <int NB, int G = 8>
-DANSE_DEV bool gevd2d_factor(BlkD<NB>& M, LDS2<NB, G>& S, int li, int D, int ref) {
+DANSE_DEV bool gevd2d_factor(BlkD<NB>& M, LDS2<NB, G>& S, int li, int D, int ref, cd* l64 = nullptr) {
   constexpr int DM = G * NB;
   const int p = li / G, q = li % G;
   constexpr int L = bin_lanes<G>(), V = vpl<NB, G>();
@@ -297,10 +482,25 @@ DANSE_DEV bool gevd2d_factor(BlkD<NB>& M, LDS2<NB, G>& S, int li, int D, int ref
       constexpr int t = decltype(tc)::value;
       cd v = M.v[0][t];
       sfor<1, NB>([&](auto sc) { v = csel(decltype(sc)::value == sr, M.v[decltype(sc)::value][t], v); });
-      if (p == (ref % G)) S.g[q + G * t] = conjg(cfk(v));
+      if (p == (ref % G)) {
+        S.g[q + G * t] = conjg(cfk(v));
+        if (l64) st_cd(l64 + DM * (DM + 1) / 2 + q + G * t, conjg(v));
+      }
     });
   }
   trinv2d<NB, G>(M, S, li, D);
+  if (l64) {
+    sfor<0, NB>([&](auto tc) {
+      constexpr int t = decltype(tc)::value;
+      const int c = q + G * t;
+      const int col = ls_col<DM>(c) - c;
+      sfor<t, NB>([&](auto sc) {
+        constexpr int s = decltype(sc)::value;
+        const int i = p + G * s;
+        if (s > t || i >= c) st_cd(l64 + col + i, M.v[s][t]);
+      });
+    });
+  }
   sfor<0, NB>([&](auto tc) {
     constexpr int t = decltype(tc)::value;
     const int c = q + G * t;

@@ -1134,6 +1134,7 @@ def batch_family_estimates(b, centr=True, local=True):
     vectors, stored in history slot i[k] + 1; estimates over all frames but
     the last, ISTFT / sum(win), and the untrimmed MMSE costs."""
     p = b.p
+    fn = update_w_gevd if p.performGEVD else update_w
     rank = p.GEVDrank if p.performGEVD else 1
     fi = dict(initType=p.filterInitType, fixedValue=p.filterInitFixedValue)
     K, F, Mt = b.K, b.F, int(sum(b.M))
