@@ -192,6 +192,8 @@ def main():
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
     ap.add_argument('--no-graph', action='store_true')
     ap.add_argument('--resident', action='store_true', help='online workloads: the resident engine (one persistent launch)')
+    ap.add_argument('--small-grid', action='store_true',
+                    help='online workloads: GEVD of D <= 12 on the 4 x 4 lane-grid class instead of one bin per lane')
     ap.add_argument('--no-traffic', action='store_true', help='skip the rocprofv3 PMC passes')
     ap.add_argument('--no-extra', action='store_true',
                     help='N=1, workload B: skip the extra single-WASN lines (B at S=1, N2 K=32x8 at S=1)')
@@ -206,6 +208,7 @@ def main():
         w['extra'] = dict(w['extra'], broadcastLength=int(args.L))
         w['desc'] = w['desc'].replace('fewSamples L=64', f'fewSamples L={args.L}').replace('fewSamples L,', f'fewSamples L={args.L},')
     _CHILD_ARGS.extend(['--L', str(args.L)] if args.L is not None else [])
+    _CHILD_ARGS.extend(['--small-grid'] if args.small_grid else [])
     if args.cpu_only:
         wl = WORKLOADS[args.workload]
         if wl.get('batch'):
@@ -237,9 +240,9 @@ def main():
     if wl.get('batch'):
         return bench_batch(args, wl, S, rank, world, local, dist)
     if args.pmc_child:
-        run_online(args, wl, S, rank, world, local, dist, pmc_child=True)
+        run_online(args, wl, S, rank, world, local, dist, pmc_child=True, small_grid=args.small_grid)
         return
-    res = run_online(args, wl, S, rank, world, local, dist, resident=args.resident)
+    res = run_online(args, wl, S, rank, world, local, dist, resident=args.resident, small_grid=args.small_grid)
     extra = {}
     if world == 1 and args.workload == 'B' and not args.no_extra:
         # single-WASN lines: config B at S=1 and the

@@ -38,6 +38,9 @@ struct Class {
   bool split = false;
   int* dSolveItems = nullptr;
   std::vector<int> solveCount;
+  // per round: does any item of the class solve (else the recursion-only
+  // kernel variant runs)
+  std::vector<uint8_t> anySolve;
 };
 
 template <typename T>
@@ -79,6 +82,7 @@ struct danse_engine {
   int graphR0 = -1, graphR1 = -1;
   void* graphStream = nullptr;
   bool ownZspec = true;
+  bool noRO = false;     // DANSE_NO_RO: never the recursion-only update variants (A/B timing)
   int bcastAblate = 0;   // DANSE_BCAST_ABLATE (diagnostics only; results are wrong when set)
   // initial-state copies for danse_engine_reset
   std::vector<long long> initW0Off, initScmOff, extSrcOff, tgtOff;
@@ -408,6 +412,14 @@ const char* danse_last_error(const danse_engine* eng) {
 static int build_split_lists(danse_engine* eng, const uint8_t* flags) {
   const int S = eng->S, K = eng->K, R = eng->R;
   for (auto& cl : eng->classes) {
+    const int nn = (int)cl.host.size();
+    cl.anySolve.assign(R, 0);
+    for (int r = 0; r < R; ++r)
+      for (int t = 0; t < S * nn && !cl.anySolve[r]; ++t) {
+        const FamNode& d = cl.host[t % nn];
+        const uint8_t fl = flags[(((size_t)r * S + t / nn) * kMaxFam + d.fam) * K + d.k];
+        if ((fl & DANSE_FLAG_SOLVE) && !(fl & DANSE_FLAG_PREGIVEN)) cl.anySolve[r] = 1;
+      }
     if (!cl.split) continue;
     const int n = (int)cl.host.size();
     std::vector<int> items((size_t)R * S * n, 0);
@@ -434,6 +446,7 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
   eng = new danse_engine();
   eng->dev = device;
   if (const char* ab = std::getenv("DANSE_BCAST_ABLATE")) eng->bcastAblate = std::atoi(ab);
+  eng->noRO = std::getenv("DANSE_NO_RO") != nullptr;
   HIPCHK(hipSetDevice(device));
   eng->S = c->S; eng->K = c->K; eng->N = c->N; eng->Ns = c->Ns; eng->F = c->N / 2 + 1; eng->T = c->T;
   eng->R = c->R; eng->k0 = c->k0; eng->k1 = c->k1; eng->gevd = c->gevd; eng->rank = c->rank; eng->ref = c->ref;
@@ -944,6 +957,7 @@ static void launch_update(danse_engine* e, int r, hipStream_t st, unsigned mask 
     a.fn = cl.dev;
     a.famNodeId = cl.devIds;
     a.splitSolve = cl.split ? 1 : 0;
+    a.noSolve = (!e->noRO && (int)cl.anySolve.size() > r && !cl.anySolve[r]) ? 1 : 0;
     launch_update_class(cl.DMAX, a, st);   // D > kMaxDMax rejected at create time
     if (cl.split && cl.solveCount[r] > 0) {
       a.solveItems = cl.dSolveItems + (size_t)r * e->S * cl.host.size();

@@ -92,6 +92,10 @@ struct UpdateArgs {
   // lane-grid kernel runs them, one launch item per entry of solveItems
   int splitSolve;
   const int* solveItems;   // this round's solving items (s * nFN + fni)
+  // no item of this launch's class solves this round (host, from the flag
+  // table): the recursion-only kernel variants run, not held to the solver's
+  // registers / LDS
+  int noSolve;
   // fewSamples step lists (compile_rounds_fs): the nodes this launch updates
   // (bit k: node k); the others are left untouched
   unsigned nodeMask;

@@ -40,7 +40,11 @@ DANSE_DEV LaneIdx lane_index(const UpdateArgs& a) {
   return x;
 }
 
-template <int D, int RMAX, bool GEVD>
+// RO: the recursion-only variant for rounds in which no item of the launch
+// solves (UpdateArgs.noSolve): the SCM entries are updated one at a time, so
+// the launch runs at the occupancy of a streaming kernel instead of the
+// solver's one wave per SIMD
+template <int D, int RMAX, bool GEVD, bool RO = false>
 __global__ void __launch_bounds__(64) update_kernel_lane(const UpdateArgs a) {
   using namespace lane;
   constexpr int NT = tri_n(D);
@@ -51,7 +55,7 @@ __global__ void __launch_bounds__(64) update_kernel_lane(const UpdateArgs a) {
   const bool valid = ix.valid && node_in(a.nodeMask, d.k);
   const uint8_t fl = a.flags[(((long long)r * a.S + s) * kMaxFam + d.fam) * a.K + d.k];
   const int opY = fl & 3, opN = (fl >> 2) & 3;
-  const bool solve = (fl & DANSE_FLAG_SOLVE) != 0 && (fl & DANSE_FLAG_PREGIVEN) == 0;
+  const bool solve = !RO && (fl & DANSE_FLAG_SOLVE) != 0 && (fl & DANSE_FLAG_PREGIVEN) == 0;
   if (a.splitSolve && solve) return;   // this item's round runs on update_kernel_2d<.., PK = true>
   // GEVD: reuse the cached float32 Li / g when Rnn has not changed since the
   // last factorisation (skips the float64 load, Cholesky and inverse)
@@ -92,12 +96,42 @@ __global__ void __launch_bounds__(64) update_kernel_lane(const UpdateArgs a) {
   // Rnn (float64) first, with the factor of a solve; then Ryy, which a solve
   // uses straight from the registers it was updated in (one Ryy read per
   // frame: the recursion, the store and the congruence share it)
+  if constexpr (RO) {
+    // one entry at a time (loads, recursion, store): no triangle is held
+    if (opY || opN) {
+      const bool isY = opY != 0;
+      const int op = isY ? opY : opN;
+      const double cy = (op == DANSE_OP_SET) ? 1.0 / D : (1.0 - beta) / D;
+      const double cx = (op == DANSE_OP_SET) ? 0.0 : beta;
+      sfor<0, D>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        sfor<0, i + 1>([&](auto jc) {
+          constexpr int j = decltype(jc)::value;
+          const long long e = base + (long long)P(i, j) * F;
+          if (isY) {
+            const cf yy = (float)cy * mulc(y[i], y[j]);
+            cf x = csel(op == DANSE_OP_SET, yy, (float)beta * a.Ryy[e] + yy);
+            if constexpr (i == j) x.im = 0.0f;
+            if (valid) a.Ryy[e] = x;
+          } else {
+            cd yy = cd{0.0, 0.0};
+            fma_cc(yy, cdk(y[i]), cdk(y[j]));
+            cd x = cx * a.Rnn[e];
+            if constexpr (i == j) x.im = 0.0;
+            x.re = fma(cy, yy.re, x.re);
+            x.im = (i == j) ? 0.0 : fma(cy, yy.im, x.im);
+            if (valid) a.Rnn[e] = x;
+          }
+        });
+      });
+    }
+  }
   PTriD<D> N;
-  if (opN || (solve && !reuse)) {
+  if (!RO && (opN || (solve && !reuse))) {
     sfor<0, NT>([&](auto ec) { N.a[decltype(ec)::value] = a.Rnn[base + (long long)decltype(ec)::value * F]; });
     sfor<0, D>([&](auto ic) { N.a[P(decltype(ic)::value, decltype(ic)::value)].im = 0.0; });
   }
-  if (opN) {
+  if (!RO && opN) {
     const double cy = (opN == DANSE_OP_SET) ? 1.0 / D : (1.0 - beta) / D;
     const double cx = (opN == DANSE_OP_SET) ? 0.0 : beta;
     sfor<0, D>([&](auto ic) {
@@ -165,13 +199,13 @@ __global__ void __launch_bounds__(64) update_kernel_lane(const UpdateArgs a) {
   }
   if (!ok && valid) atomicOr(&a.diag[(s * a.K + d.k) * kMaxFam + d.fam], 1);
   }
-  if (!solve && opY) {   // (a solve updates Ryy where it uses it)
+  if (!RO && !solve && opY) {   // (a solve updates Ryy where it uses it)
     PTri<D> A;
     ryy_update(A);
   }
   asm volatile("" ::: "memory");
   const bool pregiven = (fl & DANSE_FLAG_PREGIVEN) != 0;
-  const bool solveT = (fl & DANSE_FLAG_SOLVE) != 0;
+  const bool solveT = !RO && (fl & DANSE_FLAG_SOLVE) != 0;   // (RO: pre-given histories only)
   const long long wBase = (long long)s * a.wStride + d.wOff;
   const int slotPrev = a.wHistory ? r : (r & 1);
   const int slotNext = a.wHistory ? r + 1 : ((r + 1) & 1);

@@ -34,7 +34,8 @@ void DANSE_CAT(launch_update_d, DANSE_DMAX)(const UpdateArgs& a, hipStream_t st)
   if constexpr (kG == 1) {
     const long long lanes = (long long)a.S * a.nFN * a.F;
     const unsigned grid = (unsigned)((lanes + 63) / 64);
-    if (!a.gevd) hipLaunchKernelGGL((update_kernel_lane<kD, 1, false>), dim3(grid), dim3(64), 0, st, a);
+    if (a.noSolve) hipLaunchKernelGGL((update_kernel_lane<kD, 1, true, true>), dim3(grid), dim3(64), 0, st, a);
+    else if (!a.gevd) hipLaunchKernelGGL((update_kernel_lane<kD, 1, false>), dim3(grid), dim3(64), 0, st, a);
     else if (r1) hipLaunchKernelGGL((update_kernel_lane<kD, 1, true>), dim3(grid), dim3(64), 0, st, a);
     else hipLaunchKernelGGL((update_kernel_lane<kD, kRMax, true>), dim3(grid), dim3(64), 0, st, a);
   } else if constexpr (kG == 64) {
@@ -43,7 +44,7 @@ void DANSE_CAT(launch_update_d, DANSE_DMAX)(const UpdateArgs& a, hipStream_t st)
       hipLaunchKernelGGL((update_kernel_big<kDBig, 1, false>), dim3(grid), dim3(64), 0, st, a);
     } else if constexpr (k2D) {
       const unsigned g2 = (unsigned)(a.S * a.nFN * ((a.F + kBinsPerWave - 1) / kBinsPerWave));
-      if (a.splitSolve) {   // the recursion-only launch of the split solves
+      if (a.splitSolve || a.noSolve) {   // recursion only: the split solves' first launch, or no solver this round
         if (r1) hipLaunchKernelGGL((update_kernel_2d<kNB, 1, kGrid, false, 1>), dim3(g2), dim3(64), 0, st, a);
         else hipLaunchKernelGGL((update_kernel_2d<kNB, kRMax, kGrid, false, 1>), dim3(g2), dim3(64), 0, st, a);
       } else if (r1) {
