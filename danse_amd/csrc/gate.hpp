@@ -19,7 +19,7 @@
 // matrix_rank tolerance sigma_max max(M, N) eps with sigma_max <= trace).
 // MWF runs the rank test alone: a signed elimination that accepts negative
 // pivots (an indefinite full-rank SCM passes, as in the reference).
-// One (candidate, bin) per wavefront, the matrix in LDS, lane i owns row i.
+// One (candidate, bin) per wavefront, the matrix in LDS.
 #pragma once
 #include "kernels.hpp"
 
@@ -32,6 +32,18 @@ struct GateCand {
   double qN;    // ... of Rnn's
 };
 
+// (lower) triangle entry e = i (i + 1) / 2 + j -> (i, j)
+DANSE_DEV void tri_ij(int e, int& i, int& j) {
+  int r = (int)((sqrtf(8.0f * (float)e + 1.0f) - 1.0f) * 0.5f);
+  while (r * (r + 1) / 2 > e) --r;
+  while ((r + 1) * (r + 2) / 2 <= e) ++r;
+  i = r;
+  j = e - r * (r + 1) / 2;
+}
+
+// All 64 lanes share every step: the loads, the recursion and the Hermitian
+// test go over the packed lower triangle in storage order (coalesced), the
+// Cholesky's trailing updates over the trailing triangle's entries.
 __global__ void __launch_bounds__(64) gate_kernel(const UpdateArgs a, const FamNode* fns, const GateCand* cand,
                                                  const long long* initOff, const cd* scm0, int perBin, int* verdict) {
   extern __shared__ cd gX[];   // [D][D + 1]
@@ -42,11 +54,11 @@ __global__ void __launch_bounds__(64) gate_kernel(const UpdateArgs a, const FamN
   if (!node_in(a.nodeMask, d.k)) return;   // (fewSamples: checked before its node's update step)
   const int D = d.D, s = c.s, F = a.F;
   const int P = D + 1;
-  const bool act = li < D;
+  const int T = D * (D + 1) / 2;
   const uint8_t fl = a.flags[(((long long)a.r * a.S + s) * kMaxFam + d.fam) * a.K + d.k];
   __shared__ cf gy[64];
-  const cf y = load_y(a, d, s, f, li, act);
-  gy[li] = y;
+  __shared__ double gd[64];   // diagonal entries (the trace)
+  gy[li] = load_y(a, d, s, f, li, li < D);
   __syncthreads();
   const double beta = a.beta[s * a.K + d.k];
   const cd* R0 = scm0 + initOff[c.fni] + (perBin ? (long long)f * D * D : 0ll);
@@ -57,66 +69,64 @@ __global__ void __launch_bounds__(64) gate_kernel(const UpdateArgs a, const FamN
     const double cy = (op == DANSE_OP_SET) ? 1.0 / D : (1.0 - beta) / D;
     const double cx = (op == DANSE_OP_SET) ? 0.0 : beta;
     bool herm = true;
-    double diag = 0.0;
-    if (act) {
-      const int i = li;
-      for (int j = 0; j <= i; ++j) {
-        const long long e = scm_lower(d, a.scmStride, s, F, f, i, j);
-        cd x = which == 0 ? cdk(a.Ryy[e]) : a.Rnn[e];
-        if (i == j) x.im = 0.0;   // the stored diagonal is real; its init residue is Q_ii
-        if (op != DANSE_OP_KEEP) {
-          const cf yj = gy[j];
-          cd yy = cd{0.0, 0.0};
-          fma_cc(yy, cdk(y), cdk(yj));
-          x = cx * x;
-          x.re = fma(cy, yy.re, x.re);
-          x.im = fma(cy, (i == j) ? 0.0 : yy.im, x.im);
-        }
-        const cd r0ij = R0[i * D + j], r0ji = R0[j * D + i];
-        const cd Q = cd{0.5 * q * (r0ij.re - r0ji.re), 0.5 * q * (r0ij.im + r0ji.im)};   // q (R0 - R0^H)_ij / 2
-        if (i == j) {
-          const double qi = q * r0ij.im;   // X_ii = x.re + i qi
-          herm = herm && (2.0 * fabs(qi) <= 1e-8 + 1e-5 * sqrt(x.re * x.re + qi * qi));
-          diag = x.re;
-          gX[i * P + j] = cd{x.re, 0.0};
-        } else {
-          const double aq = 2.0 * sqrt(Q.re * Q.re + Q.im * Q.im);
-          const double xr = x.re, xi = x.im;                        // X_ij = H_ij + Q_ij (stored)
-          const double mr = xr - 2.0 * Q.re, mi = xi - 2.0 * Q.im;   // conj(X_ji) = X_ij - 2 Q_ij
-          herm = herm && (aq <= 1e-8 + 1e-5 * sqrt(xr * xr + xi * xi)) && (aq <= 1e-8 + 1e-5 * sqrt(mr * mr + mi * mi));
-          gX[i * P + j] = cd{xr, xi};
-        }
+    if (li < D) gd[li] = 0.0;
+    __syncthreads();
+    for (int e = li; e < T; e += 64) {
+      int i, j;
+      tri_ij(e, i, j);
+      const long long ee = scm_lower(d, a.scmStride, s, F, f, i, j);
+      cd x = which == 0 ? cdk(a.Ryy[ee]) : a.Rnn[ee];
+      if (i == j) x.im = 0.0;   // the stored diagonal is real; its init residue is Q_ii
+      if (op != DANSE_OP_KEEP) {
+        cd yy = cd{0.0, 0.0};
+        fma_cc(yy, cdk(gy[i]), cdk(gy[j]));
+        x = cx * x;
+        x.re = fma(cy, yy.re, x.re);
+        x.im = fma(cy, (i == j) ? 0.0 : yy.im, x.im);
+      }
+      const cd r0ij = R0[i * D + j], r0ji = R0[j * D + i];
+      const cd Q = cd{0.5 * q * (r0ij.re - r0ji.re), 0.5 * q * (r0ij.im + r0ji.im)};   // q (R0 - R0^H)_ij / 2
+      if (i == j) {
+        const double qi = q * r0ij.im;   // X_ii = x.re + i qi
+        herm = herm && (2.0 * fabs(qi) <= 1e-8 + 1e-5 * sqrt(x.re * x.re + qi * qi));
+        gd[i] = x.re;
+        gX[i * P + j] = cd{x.re, 0.0};
+      } else {
+        const double aq = 2.0 * sqrt(Q.re * Q.re + Q.im * Q.im);
+        const double xr = x.re, xi = x.im;                        // X_ij = H_ij + Q_ij (stored)
+        const double mr = xr - 2.0 * Q.re, mi = xi - 2.0 * Q.im;   // conj(X_ji) = X_ij - 2 Q_ij
+        herm = herm && (aq <= 1e-8 + 1e-5 * sqrt(xr * xr + xi * xi)) && (aq <= 1e-8 + 1e-5 * sqrt(mr * mr + mi * mi));
+        gX[i * P + j] = cd{xr, xi};
       }
     }
     // GEVD: Hermitian over every entry of every bin
-    if (a.gevd && __ballot(act && !herm) != 0ull) pass = false;
+    if (a.gevd && __ballot(!herm) != 0ull) pass = false;
+    __syncthreads();
     // full rank (+ positive definite): float64 Cholesky of the lower triangle
-    double tr = diag;
+    double tr = (li < D) ? gd[li] : 0.0;
     for (int o = 32; o >= 1; o >>= 1) tr += __shfl_xor(tr, o);
     const double tol = (double)D * 2.220446049250313e-16 * fabs(tr);
-    __syncthreads();
     // GEVD (eigvalsh >= 0 and full rank): every pivot above tol.  MWF (rank
     // only, _check_validity_nogevd, d_classes.py:1473-1480): a signed
     // (LDL^H) elimination -- negative pivots are accepted, |pivot| > tol
-    for (int j = 0; j < D; ++j) {
+    for (int j = 0; j < D && pass; ++j) {
       const double pj = gX[j * P + j].re;
       if (!(a.gevd ? pj > tol : fabs(pj) > tol)) {
-        pass = false;
+        pass = false;   // (wave-uniform: every lane read the same pivot)
         break;
       }
       const double inv = 1.0 / sqrt(fabs(pj));
-      if (li > j && li < D) {
-        const cd v = gX[li * P + j];
-        gX[li * P + j] = inv * v;
-      }
+      if (li > j && li < D) gX[li * P + j] = inv * gX[li * P + j];
       __syncthreads();
-      if (li > j && li < D) {
-        const cd lij = gX[li * P + j];
-        if (pj > 0.0) {
-          for (int k = j + 1; k <= li; ++k) fms_cc(gX[li * P + k], lij, gX[k * P + j]);
-        } else {
-          for (int k = j + 1; k <= li; ++k) fma_cc(gX[li * P + k], lij, gX[k * P + j]);
-        }
+      // trailing lower triangle (rows and columns j + 1 .. D - 1), entry by entry
+      const int n = D - 1 - j;
+      for (int e = li; e < n * (n + 1) / 2; e += 64) {
+        int i2, k2;
+        tri_ij(e, i2, k2);
+        const int row = j + 1 + i2, col = j + 1 + k2;
+        const cd lij = gX[row * P + j];
+        if (pj > 0.0) fms_cc(gX[row * P + col], lij, gX[col * P + j]);
+        else fma_cc(gX[row * P + col], lij, gX[col * P + j]);
       }
       __syncthreads();
     }

@@ -1,0 +1,16 @@
+#!/bin/bash
+# round 4: the gate kernel with all 64 lanes on every step -- parity (the
+# gate decides every start round), N2 / B / C timing
+set -o pipefail
+export TMPDIR=/tmp
+mkdir -p gpurun_out/r4q
+timeout -k 10 1000 python -u -m pytest -x -v -s --timeout 600 --timeout-method thread -m gpu tests/test_gpu_parity.py tests/test_gpu_engine_modes.py tests/test_gpu_dist.py -k "online or large_D or headline or shape or resident or gate or sharded or dist" > gpurun_out/r4q/pytest.log 2>&1
+rc=$?
+grep -E "passed|failed|FAILED|Error" gpurun_out/r4q/pytest.log | tail -6
+[ $rc -ne 0 ] && exit $rc
+for W in N2 C B; do
+  timeout -k 10 400 python -u bench.py --workload $W --steps 4 --warmup 2 --no-traffic --no-cpu-baseline --no-extra > gpurun_out/r4q/bench_${W}.log 2>&1 || { echo "bench $W failed"; tail -5 gpurun_out/r4q/bench_${W}.log; exit 1; }
+  python -c "import json; d=json.loads(open('gpurun_out/r4q/bench_${W}.log').read().strip().splitlines()[-1]); r=d['roofline']; print('$W', round(d['value']/1e6,1), 'M FU/s', round(d['ms_per_step'],1), 'ms', r['kernel'], round(r['avg_launch_ms']*1e3,1), 'us', r['frac'])"
+done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r4q/ktN2 -o kt -- python bench.py --workload N2 --steps 2 --warmup 1 --no-traffic --no-cpu-baseline > gpurun_out/r4q/ktN2.log 2>&1 || { echo "kt failed"; exit 1; }
+head -6 $(find gpurun_out/r4q/ktN2 -name "*kernel_stats.csv" | head -1) | cut -d, -f1-4
