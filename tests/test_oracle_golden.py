@@ -288,3 +288,19 @@ def test_condition_numbers_oracle_vs_reference(case, golden_dir):
             ok = b < 1e8
             assert np.max(np.abs(a[ok] - b[ok]) / b[ok]) <= 1e-6, (fam, k)
             assert np.all(a[~ok] > 1e10), (fam, k)
+
+
+def test_multi_ref_filters_bit_identical():
+    """The oracle's one-decomposition centralised filters (update_w_gevd_refs /
+    update_w_refs, used by get_best_perf for all nodes' references) equal
+    separate update_w_gevd / update_w calls bit for bit."""
+    case = next(c for c in KAT_CASES if c['name'] == 'kat_gevd_D19_r1')
+    Ryy, Rnn = kat_inputs(case)
+    refs = [0, 3, 18]
+    for rank in (1, 2):
+        many = O.update_w_gevd_refs(Ryy, Rnn, refs, rank=rank)
+        for r, w in zip(refs, many):
+            assert np.array_equal(w, O.update_w_gevd(Ryy, Rnn, r, rank))
+    many = O.update_w_refs(Ryy, Rnn, refs)
+    for r, w in zip(refs, many):
+        assert np.array_equal(w, O.update_w(Ryy, Rnn, r))
