@@ -11,7 +11,9 @@ import os
 from pathlib import Path
 
 LIB_NAME = 'libdanse_mi355x.so'
-LIB_PATH = Path(__file__).resolve().parent / LIB_NAME
+# (DANSE_LIB: an alternative build of the same library, for A/B timing of
+# compile-time variants; the in-tree library otherwise)
+LIB_PATH = Path(os.environ['DANSE_LIB']) if os.environ.get('DANSE_LIB') else Path(__file__).resolve().parent / LIB_NAME
 
 _c_i32 = ctypes.c_int32
 _p_i32 = ctypes.POINTER(ctypes.c_int32)
