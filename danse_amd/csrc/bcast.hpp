@@ -101,7 +101,8 @@ DANSE_DEV void load_frame_wave(cf (&v)[16], const float* __restrict__ x, int end
 // sqrt(Ns) * real(ifft(Hermitian extension of X[0..F))) through a forward
 // FFT of the conjugate: input element n of the wave layout.
 DANSE_DEV cf herm_ext_conj(const cf* __restrict__ X, int n, int F) {
-  return (n < F) ? conjg(X[n]) : X[1024 - n];
+  const cf x = X[(n < F) ? n : 1024 - n];   // (one load at a selected index: no branch)
+  return (n < F) ? conjg(x) : x;
 }
 
 #ifndef DANSE_BCAST_HELPERS_ONLY   // resident.hip uses the helpers above, not the kernel
@@ -161,14 +162,27 @@ __global__ void __launch_bounds__(NW * 64) bcast_kernel(const BcastArgs a) {
       if (!(a.dbg & 64)) wfft::fft1024(v, L, a.tw);
       cf* dst = (kind == 2) ? a.Cspec + (((long long)(r & 1) * a.S + s) * a.MT + ch) * F
                             : a.Yspec + (((long long)((up ? r + 1 : r) & 1) * a.S + s) * a.MT + ch) * F;
+      // (fewSamples: z comes from the T(z) chunk, no fused spectrum here)
+      const bool zk0 = kind == 0 && !a.fsTab;
+      if (zk0) {
+        cf w[16];   // the weights first, at clamped bins (hold())
 #pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        const int f = wfft::out_index(c);
-        if (f < F) {
-          const cf Y = invSqNs * v[c];
-          if (!(a.dbg & 32)) dst[f] = Y;
-          // (fewSamples: z comes from the T(z) chunk, no fused spectrum here)
-          if (kind == 0 && !a.fsTab) zp[c] = zp[c] + ((a.dbg & 16) ? Y : cmul(wx[(long long)f * Mk + m], Y));
+        for (int c = 0; c < 16; ++c) w[c] = wx[(long long)min(wfft::out_index(c), F - 1) * Mk + m];
+        hold(w);
+#pragma unroll
+        for (int c = 0; c < 16; ++c) {
+          const int f = wfft::out_index(c);
+          if (f < F) {
+            const cf Y = invSqNs * v[c];
+            if (!(a.dbg & 32)) dst[f] = Y;
+            zp[c] = zp[c] + ((a.dbg & 16) ? Y : cmul(w[c], Y));
+          }
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < 16; ++c) {
+          const int f = wfft::out_index(c);
+          if (f < F && !(a.dbg & 32)) dst[f] = invSqNs * v[c];
         }
       }
     }
@@ -189,13 +203,17 @@ __global__ void __launch_bounds__(NW * 64) bcast_kernel(const BcastArgs a) {
     const int l = __lane_id();
     const float* zs = a.zStream + ((long long)s * a.K + k) * a.zLen;
     const int zEnd = a.fsTab[((long long)r * a.K + k) * DANSE_FS_FIELDS + DANSE_FS_ZEND];
-    cf v[16];
+    float t[16], h[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
-      const int n = l + 64 * j;
-      const int idx = zEnd - N + n;
-      v[j] = cf{(idx >= 0) ? zs[idx] * a.hA[n] : 0.0f, 0.0f};
+      t[j] = zs[max(zEnd - N + l + 64 * j, 0)];
+      h[j] = a.hA[l + 64 * j];
     }
+    hold(t);
+    hold(h);
+    cf v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = cf{(zEnd - N + l + 64 * j >= 0) ? t[j] * h[j] : 0.0f, 0.0f};
     wfft::fft1024(v, L, a.tw);
     cf* Zs = a.Zspec + (((long long)(r & 1) * a.K + k) * a.S + s) * F;
 #pragma unroll
@@ -220,29 +238,64 @@ __global__ void __launch_bounds__(NW * 64) bcast_kernel(const BcastArgs a) {
     }
     wfft::fft1024(v, L, a.tw);
     float* zpv = a.zPrev + ((long long)s * a.K + k) * N;
+    float* zs = a.zStream + ((long long)s * a.K + k) * a.zLen;
+    // every global read of the chain in one straight run (hold()): the OLA
+    // state (the previous frame), the synthesis window and normalisation at
+    // this lane's output positions, and the old stream samples and analysis
+    // window of the z frame analysed below.  (The old samples lie before
+    // r Ns; the append below writes [r Ns, (r+1) Ns).)
+    const long long rs = (long long)r * Ns;
+    float zpr[16], hsv[16], nvv[16], olds[16], hav[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int n = l + 64 * j, o = wfft::out_index(j);
+      const long long idx = (long long)(r + 1) * Ns - N + n;
+      zpr[j] = zpv[n];
+      hsv[j] = a.hS[o];
+      nvv[j] = a.normVal[min(o, Ns - 1)];
+      olds[j] = zs[(idx >= 0 && idx < rs) ? idx : 0];
+      hav[j] = a.hA[n];
+    }
+    hold(zpr);
+    hold(hsv);
+    hold(nvv);
+    hold(olds);
+    hold(hav);
+    // the previous frame through LDS (zq is free until the new frame is built)
     bool nz = false;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) nz = nz || (zpv[l + 64 * j] != 0.0f);
+    for (int j = 0; j < 16; ++j) {
+      nz |= (zpr[j] != 0.0f);
+      zq[l + 64 * j] = zpr[j];
+    }
     const bool prevNZ = __ballot(nz) != 0ull;
+    wfft::wave_sync();
+    float zo[16];
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
       const int n = wfft::out_index(c);
-      float zc = sc * v[c].re * a.hS[n];
+      const float t = zq[min(n + Ns, N - 1)];
+      zo[c] = (n < N - Ns) ? t : 0.0f;
+    }
+    wfft::wave_sync();
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      const int n = wfft::out_index(c);
+      float zc = sc * v[c].re * hsv[c];
       if (prevNZ) {
-        float t = (n < N - Ns) ? zpv[n + Ns] : 0.0f;
+        float t = zo[c];
         t += zc;
-        if (n < Ns) t = t / a.normVal[n];
+        if (n < Ns) t = t / nvv[c];
         zc = t;
       }
       zq[n] = zc;
     }
     wfft::wave_sync();
-    float* zs = a.zStream + ((long long)s * a.K + k) * a.zLen;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       const int n = l + 64 * j;
       zpv[n] = zq[n];
-      if (n < Ns) zs[(long long)r * Ns + n] = zq[n];
+      if (n < Ns) zs[rs + n] = zq[n];
       if (n < Ns && a.zChunk) a.zChunk[((long long)k * a.S + s) * Ns + n] = zq[n];
     }
     // ---- z frame the receivers consume at round r: stream samples [(r+1)Ns - N, (r+1)Ns)
@@ -250,11 +303,9 @@ __global__ void __launch_bounds__(NW * 64) bcast_kernel(const BcastArgs a) {
     for (int j = 0; j < 16; ++j) {
       const int n = l + 64 * j;
       const long long idx = (long long)(r + 1) * Ns - N + n;
-      float t;
-      if (idx < 0) t = 0.0f;
-      else if (idx >= (long long)r * Ns) t = zq[idx - (long long)r * Ns];
-      else t = zs[idx];
-      v[j] = cf{t * a.hA[n], 0.0f};
+      const float cur = zq[(idx >= rs) ? (int)(idx - rs) : 0];
+      const float t = (idx < 0) ? 0.0f : (idx >= rs ? cur : olds[j]);
+      v[j] = cf{t * hav[j], 0.0f};
     }
     wfft::fft1024(v, L, a.tw);
     cf* Zs = a.Zspec + (((long long)(r & 1) * a.K + k) * a.S + s) * F;
@@ -282,11 +333,21 @@ __global__ void __launch_bounds__(NW * 64) bcast_kernel(const BcastArgs a) {
         for (int j = 0; j < 16; ++j) v[j] = herm_ext_conj(dh, l + 64 * j, F);
         wfft::fft1024(v, L, a.tw);
         float* dd = a.d + (((long long)fam * a.S + s) * a.K + k) * a.T;
+        // (all reads first, at clamped indices: distinct n, so no element
+        // is both read and written twice)
+        float old[16], hsv[16];
 #pragma unroll
         for (int c = 0; c < 16; ++c) {
           const int n = wfft::out_index(c);
-          const int idx = end - N + n;
-          if (idx >= 0 && idx < a.T) dd[idx] += sc * a.hS[n] * v[c].re;
+          old[c] = dd[min(max(end - N + n, 0), a.T - 1)];
+          hsv[c] = a.hS[n];
+        }
+        hold(old);
+        hold(hsv);
+#pragma unroll
+        for (int c = 0; c < 16; ++c) {
+          const int idx = end - N + wfft::out_index(c);
+          if (idx >= 0 && idx < a.T) dd[idx] = old[c] + sc * hsv[c] * v[c].re;
         }
       }
       ++job;

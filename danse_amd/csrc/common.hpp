@@ -155,6 +155,23 @@ DANSE_DEV cd csel(bool c, cd a, cd b) { return cd{c ? a.re : b.re, c ? a.im : b.
 
 DANSE_DEV int lane_id() { return __lane_id(); }
 
+// Register values a straight run of loads just produced, pinned here: the
+// loads issue back to back and are waited for once.  Without it the compiler
+// sinks each load into the branch (or next to the store) that uses it, and an
+// unrolled 16-element loop becomes 16 serial memory round trips -- the z
+// chain of bcast_kernel and the observation loads of the lane kernels spent
+// most of their time that way.
+DANSE_DEV void hold1(float& x) { asm volatile("" : "+v"(x)); }
+DANSE_DEV void hold1(int& x) { asm volatile("" : "+v"(x)); }
+DANSE_DEV void hold1(double& x) { asm volatile("" : "+v"(x)); }
+DANSE_DEV void hold1(cf& x) { asm volatile("" : "+v"(x.re), "+v"(x.im)); }
+DANSE_DEV void hold1(cd& x) { asm volatile("" : "+v"(x.re), "+v"(x.im)); }
+template <typename T, int n>
+DANSE_DEV void hold(T (&x)[n]) {
+#pragma unroll
+  for (int i = 0; i < n; ++i) hold1(x[i]);
+}
+
 // ---------------------------------------------------------------------------
 // Lane-group broadcast: value of lane `SRC` of my group of G lanes.
 //   G == 64 : v_readlane_b32 (wave-uniform SGPR result)

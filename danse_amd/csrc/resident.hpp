@@ -146,16 +146,19 @@ DANSE_DEV void z_role(const ResArgs& ra, int s, int k, cf* L, float* zqb, float*
     wfft::fft1024_tw(v, L, tw);
     bool nz = false;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) nz = nz || (zp[l + 64 * j] != 0.0f);
+    for (int j = 0; j < 16; ++j) nz |= (zp[l + 64 * j] != 0.0f);
     const bool prevNZ = __ballot(nz) != 0ull;
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
       const int n = wfft::out_index(c);
       float zc = sc * v[c].re * hS[c];
+      // (unconditional reads at clamped indices: no read waited for under a branch)
+      const float zo = zp[min(n + Ns, N - 1)];
+      const float nv = nvL[min(n, Ns - 1)];
       if (prevNZ) {
-        float t = (n < N - Ns) ? zp[n + Ns] : 0.0f;
+        float t = (n < N - Ns) ? zo : 0.0f;
         t += zc;
-        if (n < Ns) t = t / nvL[n];
+        if (n < Ns) t = t / nv;
         zc = t;
       }
       zq[n] = zc;
