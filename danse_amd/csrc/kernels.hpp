@@ -226,6 +226,89 @@ DANSE_DEV cf load_y(const UpdateArgs& a, const FamNode& d, int s, int f, int li,
   return csel(act, v, cf{0.0f, 0.0f});
 }
 
+// load_y of entries 0..D-1 (all active) of one lane, for the lane kernels:
+// the same values and arithmetic, the loads issued stage by stage over all
+// entries -- channel ids; sender node, lag and phases; the spectra -- so that
+// each stage is one memory round trip (hold()) instead of a dependent chain
+// per entry under per-entry branches.  Indices of the loads an entry does not
+// need are clamped to valid ones and their values discarded.
+template <int D>
+DANSE_DEV void load_y_all(const UpdateArgs& a, const FamNode& d, int s, int f, cf (&y)[D]) {
+  const int F = a.F, r = a.r, K = a.K, MT = a.MT;
+  const int rawBase = MT + K;
+  int c[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) c[i] = a.chanList[d.chanOff + i];
+  hold(c);
+  // sender node q (fused spectra) / raw channel's node (centralised vector)
+  int q[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) {
+    const bool raw = c[i] >= rawBase;
+    q[i] = (c[i] >= MT && !raw) ? c[i] - MT : 0;
+    if (a.chanNode) {
+      const int nq = a.chanNode[raw ? c[i] - rawBase : 0];
+      q[i] = raw ? nq : q[i];
+    }
+  }
+  if (a.chanNode) hold(q);
+  const long long lk0 = ((long long)r * K + d.k) * K;
+  // (the optional tables tested once, outside the unrolled loops: a test
+  // per element is a branch per element, and a wait inside each)
+  int lag[D];
+  double ph[D], cph[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) lag[i] = 0, ph[i] = 0.0, cph[i] = 0.0;
+  // (each table's loads issued before the previous table's are waited for)
+  if (a.zLag) {
+#pragma unroll
+    for (int i = 0; i < D; ++i) lag[i] = a.zLag[lk0 + q[i]];
+  }
+  if (a.zPhase) {
+#pragma unroll
+    for (int i = 0; i < D; ++i) ph[i] = a.zPhase[lk0 + q[i]];
+  }
+  if (a.cPhase) {
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      const int ch = (c[i] < MT) ? c[i] : (c[i] >= rawBase ? c[i] - rawBase : 0);
+      cph[i] = a.cPhase[((long long)r * K + d.k) * MT + ch];
+    }
+  }
+  if (a.zLag) hold(lag);
+  if (a.zPhase) hold(ph);
+  if (a.cPhase) hold(cph);
+  if (a.cdPhase) {
+#pragma unroll
+    for (int i = 0; i < D; ++i) ph[i] += a.cdPhase[((long long)s * K + d.k) * K + q[i]];
+  }
+  cf v[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) {
+    const bool loc = c[i] < MT, raw = c[i] >= rawBase;
+    const cf* p;
+    if (loc) {
+      p = a.Yall ? a.Yall + (((long long)r * a.S + s) * MT + c[i]) * F + f
+                 : a.Yspec + (((long long)((r + 1) & 1) * a.S + s) * MT + c[i]) * F + f;
+    } else if (raw) {
+      p = a.Cspec + (((long long)((r - lag[i]) & 1) * a.S + s) * MT + (c[i] - rawBase)) * F + f;
+    } else {
+      p = a.zAll ? a.Zspec + ((((long long)(r - lag[i] + 1)) * K + q[i]) * a.S + s) * F + f
+                 : a.Zspec + ((((long long)((r - lag[i]) & 1)) * K + q[i]) * a.S + s) * F + f;
+    }
+    v[i] = a.zAll ? ld_sc1(p) : *p;
+  }
+  hold(v);
+#pragma unroll
+  for (int i = 0; i < D; ++i) {
+    const bool loc = c[i] < MT, raw = c[i] >= rawBase;
+    cf x = v[i];
+    if (!loc && !raw && a.zPhase) x = sro_rotate(x, f, F, ph[i]);
+    if (a.cPhase && d.fam == DANSE_FAM_CENTR) x = sro_rotate(x, f, F, cph[i]);
+    y[i] = x;
+  }
+}
+
 // Relaxed external filter entry b wExt[i] + (1 - b) target (one function
 // for every caller, so that every caller rounds it alike)
 DANSE_DEV cf ext_relax(float be, cf ep, cf tg) { return be * ep + (1.0f - be) * tg; }

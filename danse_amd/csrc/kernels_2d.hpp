@@ -118,13 +118,34 @@ update_kernel_2d(const UpdateArgs a) {
     BlkD<NB> M;
     const double cy = (opN == DANSE_OP_SET) ? 1.0 / D : (1.0 - beta) / D;
     const double cx = (opN == DANSE_OP_SET) ? 0.0 : beta;
-    sfor<0, NB>([&](auto sc) {
+    // (every block entry loaded before the first store -- a load after a
+    // store to the same array is not moved above it, and the block was one
+    // memory round trip per entry; the recursion-only variant SM = 1 loads
+    // row by row, its register budget is a streaming kernel's)
+    auto ld_row_Rnn = [&](auto sc) {
       constexpr int sb = decltype(sc)::value;
       sfor<0, NB>([&](auto tc) {
         constexpr int tb = decltype(tc)::value;
         const int i = p + G * sb, c = q + G * tb;
         const bool in = i < D && c < D;
-        cd x = csel(in, a.Rnn[in ? ent(i, c) : safe], cd{0.0, 0.0});
+        M.v[sb][tb] = a.Rnn[in ? ent(i, c) : safe];
+      });
+    };
+    if constexpr (SM != 1) {
+      sfor<0, NB>(ld_row_Rnn);
+      sfor<0, NB>([&](auto sc) { hold(M.v[decltype(sc)::value]); });
+    }
+    sfor<0, NB>([&](auto sc) {
+      constexpr int sb = decltype(sc)::value;
+      if constexpr (SM == 1) {
+        ld_row_Rnn(sc);
+        hold(M.v[sb]);
+      }
+      sfor<0, NB>([&](auto tc) {
+        constexpr int tb = decltype(tc)::value;
+        const int i = p + G * sb, c = q + G * tb;
+        const bool in = i < D && c < D;
+        cd x = csel(in, M.v[sb][tb], cd{0.0, 0.0});
         if (i < c) x = conjg(x);
         if (i == c) x.im = 0.0;
         if (opN) {
@@ -155,13 +176,30 @@ update_kernel_2d(const UpdateArgs a) {
   if (opY || solve) {
     Blk<NB> A;
     const float by = (float)beta, cy = (opY == DANSE_OP_SET) ? (float)(1.0 / D) : (float)((1.0 - beta) / D);
-    sfor<0, NB>([&](auto sc) {
+    auto ld_row_Ryy = [&](auto sc) {
       constexpr int sb = decltype(sc)::value;
       sfor<0, NB>([&](auto tc) {
         constexpr int tb = decltype(tc)::value;
         const int i = p + G * sb, c = q + G * tb;
         const bool in = i < D && c < D;
-        cf x = csel(in, a.Ryy[in ? ent(i, c) : safe], cf{0.0f, 0.0f});
+        A.v[sb][tb] = a.Ryy[in ? ent(i, c) : safe];
+      });
+    };
+    if constexpr (SM != 1) {
+      sfor<0, NB>(ld_row_Ryy);
+      sfor<0, NB>([&](auto sc) { hold(A.v[decltype(sc)::value]); });
+    }
+    sfor<0, NB>([&](auto sc) {
+      constexpr int sb = decltype(sc)::value;
+      if constexpr (SM == 1) {
+        ld_row_Ryy(sc);
+        hold(A.v[sb]);
+      }
+      sfor<0, NB>([&](auto tc) {
+        constexpr int tb = decltype(tc)::value;
+        const int i = p + G * sb, c = q + G * tb;
+        const bool in = i < D && c < D;
+        cf x = csel(in, A.v[sb][tb], cf{0.0f, 0.0f});
         if (i < c) x = conjg(x);
         if (opY) {
           const cf yy = cy * mulc(yr[sb], yc[tb]);

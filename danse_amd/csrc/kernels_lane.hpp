@@ -66,7 +66,7 @@ __global__ void __launch_bounds__(64) update_kernel_lane(const UpdateArgs a) {
 
   cf y[D];
   if (opY || opN) {
-    sfor<0, D>([&](auto ic) { y[decltype(ic)::value] = load_y(a, d, s, f, decltype(ic)::value, true); });
+    load_y_all<D>(a, d, s, f, y);
   }
   const double beta = a.beta[s * a.K + d.k];
   const long long base = (long long)s * a.scmStride + d.scmOff + f;
@@ -103,26 +103,36 @@ __global__ void __launch_bounds__(64) update_kernel_lane(const UpdateArgs a) {
       const int op = isY ? opY : opN;
       const double cy = (op == DANSE_OP_SET) ? 1.0 / D : (1.0 - beta) / D;
       const double cx = (op == DANSE_OP_SET) ? 0.0 : beta;
+      // row by row: the row's entries loaded first (one round trip per
+      // row, hold()), then the recursion and the stores
       sfor<0, D>([&](auto ic) {
         constexpr int i = decltype(ic)::value;
-        sfor<0, i + 1>([&](auto jc) {
-          constexpr int j = decltype(jc)::value;
-          const long long e = base + (long long)P(i, j) * F;
-          if (isY) {
+        if (isY) {
+          cf old[i + 1];
+          sfor<0, i + 1>([&](auto jc) { old[decltype(jc)::value] = a.Ryy[base + (long long)P(i, decltype(jc)::value) * F]; });
+          hold(old);
+          sfor<0, i + 1>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
             const cf yy = (float)cy * mulc(y[i], y[j]);
-            cf x = csel(op == DANSE_OP_SET, yy, (float)beta * a.Ryy[e] + yy);
+            cf x = csel(op == DANSE_OP_SET, yy, (float)beta * old[j] + yy);
             if constexpr (i == j) x.im = 0.0f;
-            if (valid) a.Ryy[e] = x;
-          } else {
+            if (valid) a.Ryy[base + (long long)P(i, j) * F] = x;
+          });
+        } else {
+          cd old[i + 1];
+          sfor<0, i + 1>([&](auto jc) { old[decltype(jc)::value] = a.Rnn[base + (long long)P(i, decltype(jc)::value) * F]; });
+          hold(old);
+          sfor<0, i + 1>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
             cd yy = cd{0.0, 0.0};
             fma_cc(yy, cdk(y[i]), cdk(y[j]));
-            cd x = cx * a.Rnn[e];
+            cd x = cx * old[j];
             if constexpr (i == j) x.im = 0.0;
             x.re = fma(cy, yy.re, x.re);
             x.im = (i == j) ? 0.0 : fma(cy, yy.im, x.im);
-            if (valid) a.Rnn[e] = x;
-          }
-        });
+            if (valid) a.Rnn[base + (long long)P(i, j) * F] = x;
+          });
+        }
       });
     }
   }
@@ -244,16 +254,26 @@ __global__ void __launch_bounds__(64) update_kernel_lane(const UpdateArgs a) {
     cf* enext = a.wExtHist + eb + ((long long)eN * F + f) * M;
     cf* tgt = a.wExtTarget + (long long)s * a.tgtStride + d.tgtOff + (long long)f * M;
     const float be = a.betaExt[s * a.K + d.k];
+    // the previous entries and targets first (clamped, hold())
+    cf ep[D], tq[D];
+#pragma unroll
+    for (int m = 0; m < D; ++m) ep[m] = eprev[min(m, M - 1)], tq[m] = cf{0.0f, 0.0f};
+    if (a.wExtTarget) {
+#pragma unroll
+      for (int m = 0; m < D; ++m) tq[m] = tgt[min(m, M - 1)];
+    }
+    hold(ep);
+    hold(tq);
     sfor<0, D>([&](auto ic) {
       constexpr int m = decltype(ic)::value;
       if (m < M) {
         cf ne;
         if (d.extMode == 0) ne = w[m];
-        else if (d.extMode == 2) ne = eprev[m];
+        else if (d.extMode == 2) ne = ep[m];
         else if (d.extMode == 3) ne = cf{(m == d.ref) ? 1.0f : 0.0f, 0.0f};
         else {
-          const cf tg = tgt[m];
-          ne = be * eprev[m] + (1.0f - be) * tg;
+          const cf tg = tq[m];
+          ne = be * ep[m] + (1.0f - be) * tg;
           if (fl & DANSE_FLAG_EXT_TARGET) tgt[m] = (1.0f - a.alphaExt) * tg + a.alphaExt * w[m];
         }
         enext[m] = ne;
@@ -262,10 +282,11 @@ __global__ void __launch_bounds__(64) update_kernel_lane(const UpdateArgs a) {
   }
   // dhat = w^H yhat, DC / Nyquist forced real (quirk Q7)
   cf dh = cf{0.0f, 0.0f};
-  sfor<0, D>([&](auto ic) {
-    constexpr int i = decltype(ic)::value;
-    dh = dh + cmul(w[i], load_y(a, d, s, f, i, true));
-  });
+  {
+    cf yo[D];
+    load_y_all<D>(a, d, s, f, yo);
+    sfor<0, D>([&](auto ic) { dh = dh + cmul(w[decltype(ic)::value], yo[decltype(ic)::value]); });
+  }
   if (f == 0 || f == F - 1) dh.im = 0.0f;
   if (valid) a.dhat[((((long long)d.fam * a.S + s) * a.K + d.k) * a.R + r) * F + f] = dh;
 }
