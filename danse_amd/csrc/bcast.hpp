@@ -18,6 +18,8 @@
 //            estimates (get_desired_sig_chunk, d_base.py:2027-2084).
 //            waves 1..NW-1 take the families round-robin.
 #pragma once
+#include <cstdlib>
+
 #include "fft.hpp"
 #include "kernels.hpp"
 #include "wfft.hpp"
@@ -28,7 +30,15 @@ constexpr int kBcWaves = 4;   // waves per (scene, node) of the resident broadca
 // bcast_kernel's waves per workgroup: 8 when S K <= 128 workgroups would
 // leave most CUs idle (N2: 32, config C: 128), else 4 (decided on the global
 // S K so that node-sharded engines sum the fused spectra in the same order)
-inline int bcast_waves(int S, int K) { return S * K <= 128 ? 8 : 4; }
+// (DANSE_BCAST_WAVES=4 / 8 forces one form: A/B timing only)
+inline int bcast_waves(int S, int K) {
+  static const int forced = [] {
+    const char* e = std::getenv("DANSE_BCAST_WAVES");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (forced == 4 || forced == 8) return forced;
+  return S * K <= 128 ? 8 : 4;
+}
 
 struct BcastArgs {
   int S, K, MT, T, N, Ns, F, R;
@@ -159,15 +169,19 @@ __global__ void __launch_bounds__(NW * 64) bcast_kernel(const BcastArgs a) {
       } else {
         load_frame_wave(v, a.y + ((long long)s * a.MT + ch) * a.T, fend, a.T, a.hA);
       }
+      // (fewSamples: z comes from the T(z) chunk, no fused spectrum here)
+      const bool zk0 = kind == 0 && !a.fsTab;
+      // the weights, at clamped bins, issued before the FFT: their round trip
+      // hides under it (held after it)
+      cf w[16];
+      if (zk0) {
+#pragma unroll
+        for (int c = 0; c < 16; ++c) w[c] = wx[(long long)min(wfft::out_index(c), F - 1) * Mk + m];
+      }
       if (!(a.dbg & 64)) wfft::fft1024(v, L, a.tw);
       cf* dst = (kind == 2) ? a.Cspec + (((long long)(r & 1) * a.S + s) * a.MT + ch) * F
                             : a.Yspec + (((long long)((up ? r + 1 : r) & 1) * a.S + s) * a.MT + ch) * F;
-      // (fewSamples: z comes from the T(z) chunk, no fused spectrum here)
-      const bool zk0 = kind == 0 && !a.fsTab;
       if (zk0) {
-        cf w[16];   // the weights first, at clamped bins (hold())
-#pragma unroll
-        for (int c = 0; c < 16; ++c) w[c] = wx[(long long)min(wfft::out_index(c), F - 1) * Mk + m];
         hold(w);
 #pragma unroll
         for (int c = 0; c < 16; ++c) {

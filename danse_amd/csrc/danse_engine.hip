@@ -283,10 +283,10 @@ __global__ void __launch_bounds__(tzc::kThr) fs_chunk_kernel(const FsArgs a) {
   const int T = a.T, N = a.N;
   tzc::conv_block(
       sm, Mk, L,
-      [&](int q, int m) {   // local_chunk_for_broadcast: y[end - N + q], zero before sample 0
-        const int idx = end - N + q;
-        return (idx >= 0 && idx < T) ? y[(long long)m * T + idx] : 0.0f;
+      [&](int q, int m) {   // local_chunk_for_broadcast: y[end - N + q] (clamped read), zero before sample 0
+        return y[(long long)m * T + min(max(end - N + q, 0), T - 1)];
       },
+      [&](int q, int) { return end - N + q >= 0 && end - N + q < T; },
       [&](int i, int m) { return ir[(long long)m * tzc::kA + i]; }, [&](int i, float v) { z[i] = v; });
   if (a.rawStream) {
     // the raw samples the centralised buffers receive with the chunk

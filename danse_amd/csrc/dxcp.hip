@@ -162,29 +162,53 @@ __global__ void __launch_bounds__(kThreads) dxcp_kernel(const float* __restrict_
   const int slotNew = (ell - 1) % kCont, slotOld = ell % kCont;
   const bool do2 = ell >= kStart;
   cf avgr[kN / kThreads], g2r[kN / kThreads];
+  // the state a chunk of this thread's bins reads, loaded before the chunk's
+  // first store (a store holds every later load behind it: one memory round
+  // trip per bin); init / do2 are uniform per pair.  Two chunks of eight:
+  // the registers of all sixteen would spill.
+  constexpr int kPer = kN / kThreads, kChunk = 8;
 #pragma unroll
-  for (int i = 0; i < kN / kThreads; ++i) {
-    const int k = tid + i * kThreads;
-    const cf zk = buf[k], zm = buf[(kN - k) & (kN - 1)];
-    const cf x1 = 0.5f * (zk + conjg(zm));
-    const cf dd = zk - conjg(zm);
-    const cf x2 = cf{0.5f * dd.im, -0.5f * dd.re};   // (zk - conj zm) / (2i)
-    const cf x12 = mulc(x1, x2);
-    float a = sqrtf(abs2(x12));
-    if (a < 1e-12f) a = 1e-12f;
-    const cf g = cf{x12.re / a, x12.im / a};
-    const cf avg = init ? 0.53f * gavg[k] + 0.47f * g : g;
-    gavg[k] = avg;
-    avgr[i] = avg;
-    if (do2) {
-      const cf old = cont[(size_t)slotOld * kN + k];
-      const cf act = mulc(avg, old);
-      cf v = init ? 0.99f * g2[k] + 0.01f * act : act;
-      if (incoherent(k)) v = cf{0.0f, 0.0f};
-      g2[k] = v;
-      g2r[i] = conjg(v);
+  for (int i0 = 0; i0 < kPer; i0 += kChunk) {
+    cf gavgOld[kChunk], contOld[kChunk], g2Old[kChunk];
+    if (init) {
+#pragma unroll
+      for (int u = 0; u < kChunk; ++u) gavgOld[u] = gavg[tid + (i0 + u) * kThreads];
+      hold(gavgOld);
     }
-    cont[(size_t)slotNew * kN + k] = avg;
+    if (do2) {
+#pragma unroll
+      for (int u = 0; u < kChunk; ++u) contOld[u] = cont[(size_t)slotOld * kN + tid + (i0 + u) * kThreads];
+      hold(contOld);
+    }
+    if (do2 && init) {
+#pragma unroll
+      for (int u = 0; u < kChunk; ++u) g2Old[u] = g2[tid + (i0 + u) * kThreads];
+      hold(g2Old);
+    }
+#pragma unroll
+    for (int u = 0; u < kChunk; ++u) {
+      const int i = i0 + u;
+      const int k = tid + i * kThreads;
+      const cf zk = buf[k], zm = buf[(kN - k) & (kN - 1)];
+      const cf x1 = 0.5f * (zk + conjg(zm));
+      const cf dd = zk - conjg(zm);
+      const cf x2 = cf{0.5f * dd.im, -0.5f * dd.re};   // (zk - conj zm) / (2i)
+      const cf x12 = mulc(x1, x2);
+      float a = sqrtf(abs2(x12));
+      if (a < 1e-12f) a = 1e-12f;
+      const cf g = cf{x12.re / a, x12.im / a};
+      const cf avg = init ? 0.53f * gavgOld[u] + 0.47f * g : g;
+      gavg[k] = avg;
+      avgr[i] = avg;
+      if (do2) {
+        const cf act = mulc(avg, contOld[u]);
+        cf v = init ? 0.99f * g2Old[u] + 0.01f * act : act;
+        if (incoherent(k)) v = cf{0.0f, 0.0f};
+        g2[k] = v;
+        g2r[i] = conjg(v);
+      }
+      cont[(size_t)slotNew * kN + k] = avg;
+    }
   }
   __syncthreads();
 
@@ -202,12 +226,15 @@ __global__ void __launch_bounds__(kThreads) dxcp_kernel(const float* __restrict_
       // window, zero-padded irfft times 644 / 161
       if (tid < 81) {
         cf acc = cf{0.0f, 0.0f};
+        // (unrolled: the table reads of 7 taps issue together, the sum keeps its order)
+#pragma unroll 7
         for (int m = 0; m < 2 * kLam + 1; ++m) acc = acc + g161[m] * c.t161[(tid * m) % 161];
         X81[tid] = c.wres[tid] * acc;
       }
       __syncthreads();
       for (int n = tid; n < kNUp; n += kThreads) {
         float acc = X81[0].re;
+#pragma unroll 8
         for (int k = 1; k < 81; ++k) {
           const cf e = c.t644[(k * n) % kNUp];
           acc += 2.0f * (X81[k].re * e.re - X81[k].im * e.im);
@@ -246,13 +273,19 @@ __global__ void __launch_bounds__(kThreads) dxcp_kernel(const float* __restrict_
       float ar[16];
       float bv1 = -1.0f;
       int bi1 = 0x7fffffff;
+      float c1Old[16];   // (read before the stores below, clamped; hold())
+      if (init) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) c1Old[i] = c1[min(tid + i * kThreads, 2 * kUps)];
+        hold(c1Old);
+      }
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int j = tid + i * kThreads;
         ar[i] = 0.0f;
         if (j < 2 * kUps + 1) {
           const float cur = buf[(j - kUps + kN) & (kN - 1)].re * (1.0f / kN);
-          const float a = init ? 0.99f * c1[j] + 0.01f * cur : cur;
+          const float a = init ? 0.99f * c1Old[i] + 0.01f * cur : cur;
           c1[j] = a;
           ar[i] = fabsf(a);
           if (ar[i] > bv1) { bv1 = ar[i]; bi1 = j; }

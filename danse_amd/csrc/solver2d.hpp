@@ -403,10 +403,16 @@ DANSE_DEV bool li_rank1_2d(LDS2<NB, G>& S, int li, const cf (&yc)[NB], double be
       const double thi = tlo[sb] + av[p + G * sb];
       const double dd = sqrt(tlo[sb] / thi);
       const cd pe = (alpha / sqrt(tlo[sb] * thi)) * ps;
+      // the block row's old entries first (one round trip, hold()): the
+      // record stores below would otherwise keep each load behind the
+      // previous entry's store
+      cd mrow[sb + 1];
+      sfor<0, sb + 1>([&](auto tc) { mrow[decltype(tc)::value] = li_at(sb, decltype(tc)::value); });
+      hold(mrow);
       sfor<0, sb + 1>([&](auto tc) {   // (blocks right of the diagonal block are zero)
         constexpr int t = decltype(tc)::value;
         const int c = q + G * t;
-        const cd m = li_at(sb, t);
+        const cd m = mrow[t];
         const cd u = cd{ps.re * m.re + ps.im * m.im, ps.re * m.im - ps.im * m.re};   // conj(p_i) Li[i][c]
         // prefix over the row groups of this block row (lanes q + G p', p' < p)
         const double ire = scan_p<G>(u.re, p), iim = scan_p<G>(u.im, p);
@@ -435,13 +441,16 @@ DANSE_DEV bool li_rank1_2d(LDS2<NB, G>& S, int li, const cf (&yc)[NB], double be
   {
     const double sbeta = sqrt(beta);
     double czr = 0.0, czi = 0.0;
+    cd lrv[NB];   // L[ref][q + G t], all read before the first store (hold())
+    sfor<0, NB>([&](auto tc) { lrv[decltype(tc)::value] = ld_cd(l64 + DM * (DM + 1) / 2 + q + G * decltype(tc)::value); });
+    hold(lrv);
     sfor_down<NB, 0>([&](auto tc) {
       constexpr int t = decltype(tc)::value;
       const int c = q + G * t;
       const double t0 = __shfl(tlo[t], G * q, G * G);
       const double t1 = t0 + av[c];
       const cd pc = pv[c];
-      const cd lr = conjg(ld_cd(l64 + DM * (DM + 1) / 2 + c));   // L[ref][c]
+      const cd lr = conjg(lrv[t]);   // L[ref][c]
       const cd z = cmulx2(lr, pc);
       const double sre = scan_q_down<G>(z.re, q), sim = scan_q_down<G>(z.im, q);
       const cd sfx = cd{czr + (sre - z.re), czi + (sim - z.im)};   // sum_(k > c) L[ref][k] p_k

@@ -45,7 +45,7 @@ __global__ __launch_bounds__(kThr) void tz_compress_kernel(const float* __restri
   const float* y = yq + (size_t)b * kN * M;
   const float* a = wIR + (size_t)b * kA * M;
   float* zb = z + (size_t)b * L;
-  tzc::conv_block(sm, M, L, [&](int q, int m) { return y[(size_t)q * M + m]; },
+  tzc::conv_block(sm, M, L, [&](int q, int m) { return y[(size_t)q * M + m]; }, [](int, int) { return true; },
                   [&](int i, int m) { return a[(size_t)i * M + m]; }, [&](int e, float v) { zb[e] = v; });
 }
 

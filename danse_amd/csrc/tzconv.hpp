@@ -51,36 +51,48 @@ union ConvLds {
 template <class WF, class OF>
 DANSE_DEV void ir_wave(cf* lds, const cf* __restrict__ tw, const float* __restrict__ sn, WF wAt, OF out) {
   const int l = __lane_id();
+  // (every read issued unconditionally, then held: a read under a branch, or
+  // after a store, is one memory round trip per element)
   cf v[16];
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
     const int k = l + 64 * j;
-    cf y;
-    if (k == 0 || k == kN / 2) {
-      y = cf{wAt(k).re, 0.f};            // DC / Nyquist forced real (d_base.py:1522-1523)
-    } else if (k < kN / 2) {
-      y = wAt(k);
-    } else {
-      y = conjg(wAt(kN - k));
-    }
-    v[j] = y;
+    v[j] = wAt(k <= kN / 2 ? k : kN - k);
+  }
+  hold(v);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int k = l + 64 * j;
+    if (k == 0 || k == kN / 2) v[j].im = 0.f;   // DC / Nyquist forced real (d_base.py:1522-1523)
+    else if (k > kN / 2) v[j] = conjg(v[j]);
+  }
+  float s0[16], s1[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    const int t = wfft::out_index(c);
+    s0[c] = sn[t];
+    s1[c] = sn[min(t + kN, kA - 1)];
   }
   wfft::fft1024(v, lds, tw);
+  hold(s0);
+  hold(s1);
 #pragma unroll
   for (int c = 0; c < 16; ++c) {
     const int t = wfft::out_index(c);
     const float wt = v[c].re;
-    out(t, wt * sn[t]);
-    if (t < kN - 1) out(t + kN, wt * sn[t + kN]);
+    out(t, wt * s0[c]);
+    if (t < kN - 1) out(t + kN, wt * s1[c]);
   }
 }
 
 // One workgroup (kThr threads): the last L (1 <= L <= N) outputs of the
-// M-sensor convolution.  yAt(q, m): frame sample q of sensor m; aAt(i, m): IR
-// tap i < kA of sensor m; out(e, v): output e in [0, L).
+// M-sensor convolution.  yAt(q, m): frame sample q of sensor m, read at a
+// valid address for every q < N (yKeep(q, m) false: the sample is zero, its
+// read value discarded -- the read stays unconditional); aAt(i, m): IR tap
+// i < kA of sensor m; out(e, v): output e in [0, L).
 // nTiles = ceil(L / kR) output tiles, G = kThr / nTiles q ranges (G >= 1).
-template <class YF, class AF, class OF>
-DANSE_DEV void conv_block(ConvLds& sm, int M, int L, YF yAt, AF aAt, OF out) {
+template <class YF, class YK, class AF, class OF>
+DANSE_DEV void conv_block(ConvLds& sm, int M, int L, YF yAt, YK yKeep, AF aAt, OF out) {
   const int t = threadIdx.x;
   const int nTiles = (L + kR - 1) / kR;
   const int G = kThr / nTiles;
@@ -95,13 +107,42 @@ DANSE_DEV void conv_block(ConvLds& sm, int M, int L, YF yAt, AF aAt, OF out) {
   for (int m0 = 0; m0 < M; m0 += kMC) {
     const int mc = min(kMC, M - m0);
     __syncthreads();   // previous pass's reads are done
-    for (int e = t; e < kN * mc; e += kThr) {
-      const int q = e / mc, mm = e - q * mc;
-      sm.in.ys[mm][q] = yAt(q, m0 + mm);
+    // staging: every thread's reads issued together at clamped (valid)
+    // indices and held, then the LDS writes -- a strided loop keeps one read
+    // in flight per thread (one memory round trip per iteration)
+    {
+      constexpr int kYIt = kN * kMC / kThr;
+      float yv[kYIt];
+#pragma unroll
+      for (int u = 0; u < kYIt; ++u) {
+        const int e = min(t + u * kThr, kN * mc - 1);
+        const int q = e / mc, mm = e - q * mc;
+        yv[u] = yAt(q, m0 + mm);
+      }
+      hold(yv);
+#pragma unroll
+      for (int u = 0; u < kYIt; ++u) {
+        const int e = t + u * kThr;
+        const int q = e / mc, mm = e - q * mc;
+        if (e < kN * mc) sm.in.ys[mm][q] = yKeep(q, m0 + mm) ? yv[u] : 0.0f;
+      }
     }
-    for (int e = t; e < kIrSlots * mc; e += kThr) {
-      const int i = e / mc, mm = e - i * mc;
-      sm.in.as[mm][phys(i)] = i < kA ? aAt(i, m0 + mm) : 0.f;
+    {
+      constexpr int kAIt = (kIrSlots * kMC + kThr - 1) / kThr;
+      float av[kAIt];
+#pragma unroll
+      for (int u = 0; u < kAIt; ++u) {
+        const int e = t + u * kThr;
+        const int i = min(e / mc, kA - 1), mm = min(e - (e / mc) * mc, mc - 1);
+        av[u] = aAt(i, m0 + mm);
+      }
+      hold(av);
+#pragma unroll
+      for (int u = 0; u < kAIt; ++u) {
+        const int e = t + u * kThr;
+        const int i = e / mc, mm = e - i * mc;
+        if (e < kIrSlots * mc) sm.in.as[mm][phys(i)] = i < kA ? av[u] : 0.f;
+      }
     }
     __syncthreads();
     if (active) {

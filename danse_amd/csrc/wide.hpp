@@ -62,7 +62,10 @@ DANSE_DEV double bsum(double x, double* red) {
 // chunk, the L entries are the same for every thread), then the chunk's own
 // triangle.  invd[i] = 1 / L[i][i].
 template <bool FWD>
-DANSE_DEV void trsv_col(const cd* Lc, const double* invd, int D, cd* Cw, int c) {
+// (restrict: the factor and the workspace are distinct buffers, so the L
+// reads of the chunk's triangle need not wait behind the solved-row stores;
+// the reads are unconditional at clamped rows, their values selected)
+DANSE_DEV void trsv_col(const cd* __restrict__ Lc, const double* __restrict__ invd, int D, cd* __restrict__ Cw, int c) {
   for (int b0 = 0; b0 < D; b0 += kCh) {
     cd acc[kCh];
 #pragma unroll
@@ -79,7 +82,8 @@ DANSE_DEV void trsv_col(const cd* Lc, const double* invd, int D, cd* Cw, int c) 
         const int i = FWD ? b0 + r : D - 1 - (b0 + r);
         const bool ok = FWD ? i < D : i >= 0;
         // FWD: L[i][k] = Lc[k][i];  !FWD: (L^H)[i][k] = conj(L[k][i]) = conj(Lc[i][k])
-        const cd l = ok ? (FWD ? Lc[(long long)k * D + i] : conjg(Lc[(long long)i * D + k])) : cd{0.0, 0.0};
+        const int ic = ok ? i : (FWD ? D - 1 : 0);
+        const cd l = csel(ok, FWD ? Lc[(long long)k * D + ic] : conjg(Lc[(long long)ic * D + k]), cd{0.0, 0.0});
         fms_c(acc[r], l, xk);
       }
     }
@@ -90,7 +94,8 @@ DANSE_DEV void trsv_col(const cd* Lc, const double* invd, int D, cd* Cw, int c) 
 #pragma unroll
       for (int q = 0; q < r; ++q) {
         const int k = FWD ? b0 + q : D - 1 - (b0 + q);
-        const cd l = ok ? (FWD ? Lc[(long long)k * D + i] : conjg(Lc[(long long)i * D + k])) : cd{0.0, 0.0};
+        const int ic = ok ? i : (FWD ? D - 1 : 0);
+        const cd l = csel(ok, FWD ? Lc[(long long)k * D + ic] : conjg(Lc[(long long)ic * D + k]), cd{0.0, 0.0});
         fms_c(acc[r], l, acc[q]);
       }
       if (ok) {

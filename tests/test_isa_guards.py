@@ -8,6 +8,9 @@ parity tests cannot see but that cost the GPU dearly.
   register-array element to global memory, or an over-full register budget,
   silently moves arrays to scratch.  (That check
   compiles two size classes, about 3.5 minutes: opt-in, DANSE_ISA_FULL=1.)
+* The broadcast, fewSamples and DXCP kernels must not use scratch either:
+  their loads are issued as held straight runs, and a run
+  too long for the registers spills.
 """
 import os
 import re
@@ -77,3 +80,15 @@ def test_update_kernels_use_no_scratch():
         assert sizes, f'no update kernels found for DMAX {dmax}'
         bad = {k: v for k, v in sizes.items() if v != 0}
         assert not bad, (dmax, bad)
+
+
+def test_broadcast_and_dxcp_kernels_use_no_scratch():
+    # the broadcast kernels hold five 16-element preload runs next to the FFT
+    # registers; DXCP's state preloads spill at 16 per chunk
+    asm = _device_asm(CSRC / 'danse_engine.hip')
+    sizes = _scratch_sizes(asm, r'bcast_kernel|fs_chunk_kernel|fs_ir_kernel')
+    assert len(sizes) >= 4, sizes
+    assert not {k: v for k, v in sizes.items() if v != 0}, sizes
+    asm = _device_asm(CSRC / 'dxcp.hip')
+    sizes = _scratch_sizes(asm, r'dxcp_kernel')
+    assert sizes and not {k: v for k, v in sizes.items() if v != 0}, sizes
