@@ -169,19 +169,15 @@ __global__ void __launch_bounds__(NW * 64) bcast_kernel(const BcastArgs a) {
       } else {
         load_frame_wave(v, a.y + ((long long)s * a.MT + ch) * a.T, fend, a.T, a.hA);
       }
-      // (fewSamples: z comes from the T(z) chunk, no fused spectrum here)
-      const bool zk0 = kind == 0 && !a.fsTab;
-      // the weights, at clamped bins, issued before the FFT: their round trip
-      // hides under it (held after it)
-      cf w[16];
-      if (zk0) {
-#pragma unroll
-        for (int c = 0; c < 16; ++c) w[c] = wx[(long long)min(wfft::out_index(c), F - 1) * Mk + m];
-      }
       if (!(a.dbg & 64)) wfft::fft1024(v, L, a.tw);
       cf* dst = (kind == 2) ? a.Cspec + (((long long)(r & 1) * a.S + s) * a.MT + ch) * F
                             : a.Yspec + (((long long)((up ? r + 1 : r) & 1) * a.S + s) * a.MT + ch) * F;
+      // (fewSamples: z comes from the T(z) chunk, no fused spectrum here)
+      const bool zk0 = kind == 0 && !a.fsTab;
       if (zk0) {
+        cf w[16];   // the weights first, at clamped bins (hold())
+#pragma unroll
+        for (int c = 0; c < 16; ++c) w[c] = wx[(long long)min(wfft::out_index(c), F - 1) * Mk + m];
         hold(w);
 #pragma unroll
         for (int c = 0; c < 16; ++c) {
