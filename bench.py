@@ -41,6 +41,7 @@ sys.path.insert(0, str(ROOT))
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md, chip-level parameters
 FP32_VALU_PEAK_TFS = 157.3    # ibid., peak FP32 (vector)
 FP32_MFMA_PEAK_TFS = 157.3    # ibid., peak FP32 (matrix, f32-input MFMA: the vector rate on gfx950)
+OP_KEEP, OP_SET, OP_AVG = 0, 1, 2   # include/danse_mi355x_defs.h DANSE_OP_* (danse_amd._lib OP_*)
 
 
 def _battery_params(M, nodeUpdating='asy', **extra):
@@ -141,19 +142,33 @@ def update_kernel_name(Dmax, gevd=True):
 
 
 def alg_bytes_update(D, opY, opN, solve):
-    """Algorithmic HBM bytes of one node x bin x frame of update_kernel
-    (in the engine's storage: packed Hermitian Ryy complex64 =
-    4 D(D+1) B, packed Rnn complex128 = 8 D(D+1) B, DESIGN.md "Data layout"):
-    read y, read (or write) w, write dhat; read + write the SCM this frame's
-    VAD updates (write only when it is set from the first frame); on solve
-    frames also read the other SCM.  Arrays of per-frame flags in, bytes out."""
+    """Algorithmic HBM bytes of one node x bin x frame of update_kernel,
+    SURVEY §8d (complex64, packed Hermitian: one SCM one way = 4 D(D+1) B):
+    read y (8 D), write dhat (8); read + write the SCM this frame's VAD
+    updates (DANSE_OP_AVG: 8 D(D+1)), or write it only when the first frame
+    sets it (DANSE_OP_SET: 4 D(D+1)); on solve frames also read the SCM left
+    alone (4 D(D+1)) and write w (8 D).  Arrays of per-frame op codes / solve
+    flags in, bytes out."""
     opY, opN, solve = np.asarray(opY), np.asarray(opN), np.asarray(solve)
     t = D * (D + 1)
-    b = 16.0 * D + 8.0
-    b = b + np.where(opY == 0, 0.0, np.where(opY == 2, 4.0 * t, 8.0 * t))
-    b = b + np.where(opN == 0, 0.0, np.where(opN == 2, 8.0 * t, 16.0 * t))
-    b = b + np.where(solve & (opY == 0), 4.0 * t, 0.0) + np.where(solve & (opN == 0), 8.0 * t, 0.0)
-    return b
+    one = 4.0 * t
+
+    def scm(op):
+        return np.where(op == OP_AVG, 2.0 * one, np.where(op == OP_SET, one, np.where(solve, one, 0.0)))
+    return 8.0 * D + 8.0 + scm(opY) + scm(opN) + np.where(solve, 8.0 * D, 0.0)
+
+
+def storage_bytes_update(D, opY, opN, solve):
+    """The same frame in the engine's storage: Ryy packed
+    complex64 (4 D(D+1) B one way), Rnn packed complex128 (8 D(D+1) B), w
+    read from the previous slot and written to the next on frames without a
+    solve (16 D) or written only (8 D); the GEVD factor caches not counted."""
+    opY, opN, solve = np.asarray(opY), np.asarray(opN), np.asarray(solve)
+    t = D * (D + 1)
+
+    def scm(op, one):
+        return np.where(op == OP_AVG, 2.0 * one, np.where(op == OP_SET, one, np.where(solve, one, 0.0)))
+    return (8.0 * D + 8.0 + scm(opY, 4.0 * t) + scm(opN, 8.0 * t) + np.where(solve, 8.0 * D, 16.0 * D))
 
 
 def alg_flops_update(D, opY, opN, solve):
@@ -253,11 +268,21 @@ def main():
         # N1: the whole run in one persistent launch, SCMs resident in registers
         extra['B_S1_resident'] = run_online(args, wl, 1, rank, world, local, dist, traffic=False, resident=True)
         extra['N2'] = run_online(args, WORKLOADS['N2'], 1, rank, world, local, dist)
+        # the other BASELINE.json configs, each on its own shape: C as named
+        # (DXCP-PhaT estimation + compensation, K = 16 x 4, SROs 0..200 ppm),
+        # D (batch K = 32 x 8, 20 iterations) and E at the battery's SRO
+        # setting (K = 2, MK = [2, 3], fewSamples L = 64, 512 scenes)
+        extra['C_dxcp'] = run_online(args, WORKLOADS['C_dxcp'], WORKLOADS['C_dxcp']['scenes'], rank, world, local,
+                                     dist, traffic=False)
+        extra['D'] = run_batch(args, WORKLOADS['D'], 1, rank, world, local, dist)
+        extra['E_L64_sro200'] = run_online(args, WORKLOADS['E_L64_sro200'], 512, rank, world, local, dist,
+                                           traffic=False)
     cpu = {}
     if rank == 0 and not args.no_cpu_baseline:
         cpu[args.workload] = cpu_child(args.workload, args.cpu_seconds, res['rounds'])
-        if 'N2' in extra:
-            cpu['N2'] = cpu_child('N2', args.cpu_seconds, extra['N2']['rounds'])
+        for key in ('N2', 'C_dxcp', 'D', 'E_L64_sro200'):
+            if key in extra:
+                cpu[key] = cpu_child(key, args.cpu_seconds, extra[key].get('rounds'))
     if rank == 0:
         line = {
             'metric': 'DANSE frame-updates/sec (nodes x bins)',
@@ -441,19 +466,35 @@ def run_online(args, wl, S, rank, world, local, dist, traffic=True, pmc_child=Fa
     solve = ((fl & L.FLAG_SOLVE) != 0) & ((fl & L.FLAG_PREGIVEN) == 0)
     Dl = np.array(Dk[k0:k1], dtype=np.float64)[None, None, :]
     byts = F * alg_bytes_update(Dl, opY, opN, solve).sum(axis=(1, 2))       # per launch (round)
+    sbyts = F * storage_bytes_update(Dl, opY, opN, solve).sum(axis=(1, 2))
     flops = F * alg_flops_update(Dl, opY, opN, solve).sum(axis=(1, 2))
+    # the dominant kernel: the update launches of the rounds with a solving
+    # item (the solver instantiation); the recursion-only rounds run the
+    # recursion-only variants (UpdateArgs.noSolve) and are reported apart
+    solveRound = solve.any(axis=(1, 2))
     if resident:
         # per launch = every round of the run
-        byts, flops = np.array([byts.sum()]), np.array([flops.sum()])
-    avg_ms = float(upd_ms.mean())
-    gbs = float(byts.mean() / (avg_ms * 1e-3) / 1e9)
-    tfs = float(flops.mean() / (avg_ms * 1e-3) / 1e12)
+        byts, sbyts, flops = np.array([byts.sum()]), np.array([sbyts.sum()]), np.array([flops.sum()])
+        dom = np.array([True])
+    else:
+        dom = solveRound if solveRound.any() else np.ones_like(solveRound)
+    avg_ms = float(upd_ms[dom].mean())
+    gbs = float(byts[dom].mean() / (avg_ms * 1e-3) / 1e9)
+    sgbs = float(sbyts[dom].mean() / (avg_ms * 1e-3) / 1e9)
+    tfs = float(flops[dom].mean() / (avg_ms * 1e-3) / 1e12)
+    rec = None
+    if not resident and (~dom).any():
+        rms = float(upd_ms[~dom].mean())
+        rec = {'rounds': int((~dom).sum()), 'avg_launch_ms': rms,
+               'alg_bytes_per_launch': float(byts[~dom].mean()),
+               'hbm_GBs': float(byts[~dom].mean() / (rms * 1e-3) / 1e9)}
     diag = eng.diagnostics()
+    lz = eng.lanczos_stats()
     eng.close()
 
     tr = None
     if traffic and rank == 0 and world == 1 and not args.no_traffic:
-        tr = pmc_traffic(wl, S, 'update_kernel')
+        tr = pmc_traffic(wl, S, 'update_kernel', dom if not resident else None)
     valu = max(Dk) > VALU_RIDGE_D
     roof = {'bound': 'valu' if valu else 'hbm',
             'achieved': tfs if valu else gbs,
@@ -464,10 +505,19 @@ def run_online(args, wl, S, rank, world, local, dist, traffic=True, pmc_child=Fa
             'traffic_detail': tr,
             'kernel': ('resident_kernel (one persistent launch per run; achieved = all rounds\' algorithmic bytes '
                        '/ the run)' if resident else
-                       'update_kernel_2d (4 x 4 grid)' if small_grid and max(Dk) <= 12
-                       else update_kernel_name(max(Dk), gevd=bool(wl.get('gevd', True)))), 'avg_launch_ms': avg_ms,
-            'alg_bytes_per_launch': float(byts.mean()), 'alg_flops_per_launch': float(flops.mean()),
-            'hbm_GBs': gbs, 'hbm_frac': gbs / HBM_PEAK_GBS, 'valu_TFs': tfs, 'valu_frac': tfs / FP32_VALU_PEAK_TFS}
+                       ('update_kernel_2d (4 x 4 grid)' if small_grid and max(Dk) <= 12
+                        else update_kernel_name(max(Dk), gevd=bool(wl.get('gevd', True))))
+                       + f', solve rounds ({int(dom.sum())} of {R})'),
+            'avg_launch_ms': avg_ms,
+            'alg_bytes_per_launch': float(byts[dom].mean()), 'alg_flops_per_launch': float(flops[dom].mean()),
+            'bytes_model': 'SURVEY §8d: complex64 packed Hermitian SCMs (achieved); storage_* = the engine\'s '
+                           'storage (Ryy c64, Rnn c128, w ring), factor caches not counted',
+            'storage_bytes_per_launch': float(sbyts[dom].mean()), 'storage_GBs': sgbs,
+            'hbm_GBs': gbs, 'hbm_frac': gbs / HBM_PEAK_GBS, 'valu_TFs': tfs, 'valu_frac': tfs / FP32_VALU_PEAK_TFS,
+            'recursion_rounds': rec}
+    if lz.any():
+        roof['lanczos'] = {'accepted': int(lz[:, 0].sum()), 'sent_back': int(lz[:, 1].sum()),
+                           'max_sent_back_per_launch': int(lz[:, 1].max())}
     return {
         'value': value, 'ms_per_step': el / args.steps * 1e3, 'rounds': R,
         'data': f'synthetic random-IR scenes (seeded, {gen} generator{", SRO-resampled" if gen == "device" and wl.get("sros") else ""}), '
@@ -480,15 +530,35 @@ def run_online(args, wl, S, rank, world, local, dist, traffic=True, pmc_child=Fa
 
 
 def bench_batch(args, wl, S, rank, world, local, dist):
+    """The batch workload (config D) as the bench line: run_batch + the CPU
+    leg of rank 0."""
+    res = run_batch(args, wl, S, rank, world, local, dist)
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        cpu = cpu_child(args.workload, args.cpu_seconds, None)
+    if rank == 0:
+        line = {
+            'metric': 'DANSE frame-updates/sec (nodes x bins)', 'value': res['value'],
+            'unit': 'frame-updates/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
+            'ms_per_step': res['ms_per_step'], 'higher_is_better': True,
+            'scaling': res['scaling'], 'vs_baseline': None, 'dtype': 'c64',
+            'data': res['data'], 'config': res['config'], 'roofline': res['roofline'],
+            'cpu_baseline': cpu, 'scene_gen_s': res['scene_gen_s'],
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def run_batch(args, wl, S, rank, world, local, dist):
     """Batch DANSE (config D): a step is one full danse_batch run (STFT, then
     per iteration z, the MFMA Y.Y^H covariance contraction over VAD / non-VAD
     frames, every node's solve, external filters, estimates, ISTFT and MMSE
     cost) over S WASNs per GPU.  value = iterations x nodes x STFT frames x
-    bins / s.  Roofline of the dominant kernel (herk_kernel) comes from the
-    rocprofv3 kernel statistics of the same command, not from live
-    events: the kernel is internal to danse_batch_run."""
+    bins / s.  Roofline of the dominant kernel (herk_kernel) from live HIP
+    events at the run's phase boundaries (danse_batch_set_timing), in a
+    separate pass after the timed steps."""
     import torch
-    from danse_amd import params as P
     from danse_amd.batch import BatchEngine
     from danse_amd.scene import make_scene
     M, K = wl['M'], len(wl['M'])
@@ -533,9 +603,6 @@ def bench_batch(args, wl, S, rank, world, local, dist):
     F = eng.F
     fu_per_step = S * (1 if byNodes else world) * K * eng.nseg * F * eng.iters
     D = M[0] + K - 1
-    # ---- roofline of the dominant kernels from live HIP events on the run's
-    # stream (danse_batch_set_timing: one event per phase boundary of every
-    # iteration), in a separate pass after the timed steps
     eng.set_timing(True)
     step()
     torch.cuda.synchronize()
@@ -560,28 +627,16 @@ def bench_batch(args, wl, S, rank, world, local, dist):
                       'peak': FP32_VALU_PEAK_TFS, 'unit': 'TFLOP/s', 'frac': solve_tfs / FP32_VALU_PEAK_TFS},
             'dhat': {'kernel': 'batch_dhat_kernel', 'bound': 'hbm', 'achieved': dhat_gbs, 'peak': HBM_PEAK_GBS,
                      'unit': 'GB/s', 'frac': dhat_gbs / HBM_PEAK_GBS}}
-    cpu = None
-    if rank == 0 and not args.no_cpu_baseline:
-        cpu = cpu_child(args.workload, args.cpu_seconds, None)
-    if rank == 0:
-        line = {
-            'metric': 'DANSE frame-updates/sec (nodes x bins)', 'value': fu_per_step * args.steps / el,
-            'unit': 'frame-updates/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
-            'ms_per_step': el / args.steps * 1e3, 'higher_is_better': True,
-            'scaling': 'strong' if byNodes else 'weak', 'vs_baseline': None, 'dtype': 'c64',
-            'data': f'synthetic random-IR scenes (seeded), {S * (1 if byNodes else world)} WASNs x {K} nodes x {eng.nseg} frames x {F} '
-                    f'bins x {eng.iters} iterations per step',
-            'config': {'workload': wl['desc'], 'wasns_per_gpu': S, 'K': K, 'M': M[0], 'D': D, 'bins': F,
-                       'frames': eng.nseg, 'iterations': eng.iters,
-                       'shard': 'nodes' if byNodes else 'replicas'},
-            'roofline': roof,
-            'cpu_baseline': cpu,
-            'scene_gen_s': tScene,
-        }
-        print(json.dumps(line), flush=True)
     eng.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    return {
+        'value': fu_per_step * args.steps / el, 'ms_per_step': el / args.steps * 1e3,
+        'scaling': 'strong' if byNodes else 'weak',
+        'data': f'synthetic random-IR scenes (seeded), {S * (1 if byNodes else world)} WASNs x {K} nodes x {eng.nseg} '
+                f'frames x {F} bins x {eng.iters} iterations per step',
+        'config': {'workload': wl['desc'], 'wasns_per_gpu': S, 'K': K, 'M': M[0], 'D': D, 'bins': F,
+                   'frames': eng.nseg, 'iterations': eng.iters, 'shard': 'nodes' if byNodes else 'replicas'},
+        'roofline': roof, 'scene_gen_s': tScene,
+    }
 
 
 def cpu_baseline_batch(M, wl, dp, wp, seconds):
@@ -622,7 +677,7 @@ def cpu_baseline_batch(M, wl, dp, wp, seconds):
             't_node_s': tn, 'nodes_sampled': n, 'projected_run_s': total}
 
 
-def pmc_traffic(wl, S, kernel_substr):
+def pmc_traffic(wl, S, kernel_substr, rounds=None):
     """HBM bytes per launch of the dominant kernel from two rocprofv3 PMC
     passes over the same workload (MI355X_MICROARCH.md, HBM section):
     FETCH_SIZE and WRITE_SIZE (KiB) in separate passes, FETCH_SIZE doubled
@@ -647,12 +702,19 @@ def pmc_traffic(wl, S, kernel_substr):
         except Exception as e:   # profiler unavailable or refused: report null, never fail the bench
             return {'error': f'{counter}: {type(e).__name__}'}
         files = [os.path.join(r, f) for r, _, fs in os.walk(d) for f in fs if f.endswith('counter_collection.csv')]
-        vals = [float(row['Counter_Value']) * 1024.0 for fn in files for row in csv.DictReader(open(fn))
+        rows = [row for fn in files for row in csv.DictReader(open(fn))
                 if row['Counter_Name'] == counter and kernel_substr in row['Kernel_Name']]
-        if not vals:
+        if not rows:
             return {'error': f'{counter}: no samples'}
+        if 'Dispatch_Id' in rows[0]:
+            rows.sort(key=lambda row: int(row['Dispatch_Id']))
+        vals = np.array([float(row['Counter_Value']) * 1024.0 for row in rows])
+        # (one update dispatch per round in the un-graphed pass: the rounds
+        # mask picks the solve rounds the roofline's duration is taken over)
+        if rounds is not None and len(vals) == len(rounds):
+            vals = vals[np.asarray(rounds, dtype=bool)]
         out[counter] = float(np.mean(vals))
-        out['dispatches'] = len(vals)
+        out['dispatches'] = int(len(vals))
     shutil.rmtree(tmp, ignore_errors=True)
     b = 2.0 * out['FETCH_SIZE'] + out['WRITE_SIZE']
     return {'bytes_per_launch': b, 'fetch_bytes_raw': out['FETCH_SIZE'], 'write_bytes': out['WRITE_SIZE'],

@@ -102,6 +102,7 @@ SIGNATURES = {
     'danse_engine_dxcp_recorded': (_c_i32, [ctypes.c_void_p, ctypes.POINTER(_c_i32), ctypes.POINTER(_c_i32),
                                             ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t]),
     'danse_engine_resident_trace': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_size_t)]),
+    'danse_engine_lanczos_stats': (_c_i32, [ctypes.c_void_p, _p_i32, ctypes.c_size_t]),
     'danse_engine_bcast': (_c_i32, [ctypes.c_void_p, _c_i32, ctypes.c_void_p]),
     'danse_engine_update': (_c_i32, [ctypes.c_void_p, _c_i32, ctypes.c_void_p]),
     'danse_engine_finish': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p]),

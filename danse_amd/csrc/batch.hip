@@ -817,7 +817,7 @@ int danse_batch_create(const danse_batch_cfg* c, int device, danse_batch** out) 
   BCHK(balloc(&eng->wTmp, (size_t)K * S * F * Dmax));   // one solve launch covers a run of nodes
   BCHK(balloc(&eng->dDiag, (size_t)K * S * F));
   if (eng->wideMode) {
-    eng->wideChunk = std::min<long long>((long long)S * F, 1024);
+    eng->wideChunk = wide::chunk_for(mt, (long long)S * F);
     BCHK(balloc(&eng->wideWork, (size_t)eng->wideChunk * wide::work_elems(mt)));
   }
   (void)Mmax;

@@ -106,6 +106,7 @@ struct danse_engine {
   long long vStride = 0;
   cd* l64Cache = nullptr;    // lane-grid GEVD classes: float64 factor record per bin (rank-one updates)
   long long l64Stride = 0;
+  int* lzStats = nullptr;    // [R][2] warm Lanczos solves accepted / sent back (danse_engine_lanczos_stats)
   int scmPerBin = 0;   // dScm0 holds [F][D][D] per family-node (else [D][D])
   FamNode* dFnAll = nullptr;
   long long *dInitW0Off = nullptr, *dInitScmOff = nullptr, *dExtSrcOff = nullptr, *dTgtOff = nullptr;
@@ -390,6 +391,7 @@ int danse_engine_reset(danse_engine* eng, void* stream) {
   HIPCHK(fill_async(eng->d, 0, (size_t)kMaxFam * S * K * eng->T * sizeof(float), st));
   HIPCHK(fill_async(eng->diag, 0, (size_t)S * K * kMaxFam * sizeof(int), st));
   if (eng->vCache) HIPCHK(fill_async(eng->vCache, 0, (size_t)S * eng->vStride * sizeof(cf), st));
+  if (eng->lzStats) HIPCHK(fill_async(eng->lzStats, 0, (size_t)2 * eng->R * sizeof(int), st));
   const int nFN = (int)eng->fns.size();
   hipLaunchKernelGGL(reset_fam_kernel, dim3(64, S * nFN), dim3(256), 0, st, eng->dFnAll, nFN, eng->dInitW0Off,
                      eng->dInitScmOff, eng->dW0, eng->dScm0, eng->wHist, eng->wStride, eng->Ryy, eng->Rnn,
@@ -466,7 +468,9 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
     if (K > 31) return fail(eng, "fewSamples steps: at most 31 nodes (node masks)");
     const int all = (1 << K) - 1;
     if (c->fsSteps) {
-      if (!c->fsEv || c->nFsSteps < 3 * R || c->nFsEv < 0) return fail(eng, "fewSamples steps without chunk rows");
+      // (a round is at least BCAST + UPDATE; chunk steps only where a stream
+      // needs one -- the per-step validation below checks every round)
+      if (!c->fsEv || c->nFsSteps < 2 * R || c->nFsEv < 0) return fail(eng, "fewSamples steps: too few steps or no chunk rows");
       eng->fsEv.assign(c->fsEv, c->fsEv + (size_t)c->nFsEv * K * DANSE_FS_FIELDS);
       eng->fsSteps.assign(c->fsSteps, c->fsSteps + (size_t)c->nFsSteps * DANSE_FS_STEP_FIELDS);
     } else {   // one CHUNK (fsTab row r), BCAST, UPDATE per round
@@ -761,6 +765,7 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
   HIPCHK(dalloc(&eng->diag, (size_t)S * K * kMaxFam));
   if (eng->liStride > 0) HIPCHK(dalloc(&eng->liCache, (size_t)S * eng->liStride));
   if (eng->vStride > 0) HIPCHK(dalloc(&eng->vCache, (size_t)S * eng->vStride));
+  if (eng->vStride > 0) HIPCHK(dalloc(&eng->lzStats, (size_t)2 * R));
   if (eng->l64Stride > 0) HIPCHK(dalloc(&eng->l64Cache, (size_t)S * eng->l64Stride));
   if (c->dxcp) {
     if (c->cohDrift) return fail(eng, "DXCP-PhaT and CohDrift estimation are exclusive");
@@ -892,7 +897,7 @@ void danse_engine_destroy(danse_engine* eng) {
                   eng->dxEst, eng->resYB, eng->resYU, eng->resZall, eng->resZhat, eng->resRyyG, eng->resRnnG,
                   eng->resUFlag, eng->resZFlag, eng->resGateRound, eng->resDanseFni, eng->resErr, eng->resFams,
                   eng->resFrames, eng->resChanNode, eng->resTrace, eng->condHist, eng->dxRecFrames,
-                  eng->dxRecOut, eng->dFsEv, eng->rawStream, eng->vCache, eng->l64Cache};
+                  eng->dxRecOut, eng->dFsEv, eng->rawStream, eng->vCache, eng->l64Cache, eng->lzStats};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (eng->dx) danse_dxcp_destroy(eng->dx);
@@ -941,6 +946,7 @@ static UpdateArgs make_update(danse_engine* e, int r) {
   a.liCache = e->liCache; a.liStride = e->liStride;
   a.vCache = e->vCache; a.vStride = e->vStride;
   a.l64Cache = e->l64Cache; a.l64Stride = e->l64Stride;
+  a.lzStats = e->lzStats;
   a.cdPhase = e->cdPhase;
   a.Cspec = e->Cspec; a.chanNode = e->dChanNode; a.cPhase = e->dCPhase;
   a.nodeMask = ~0u;
@@ -994,10 +1000,10 @@ static void launch_update(danse_engine* e, int r, hipStream_t st, unsigned mask 
       (void)danse_dxcp_process(e->dx, e->dxFrames, e->dxOut, st);
       const int feed = (r + 1) / every - 1;
       if (e->dxRecFrames && feed < e->dxRecFeeds) {
-        (void)hipMemcpyAsync(e->dxRecFrames + (size_t)feed * P * 2 * kDxFrame, e->dxFrames,
-                             (size_t)P * 2 * kDxFrame * sizeof(float), hipMemcpyDeviceToDevice, st);
-        (void)hipMemcpyAsync(e->dxRecOut + (size_t)feed * P * 2, e->dxOut, (size_t)P * 2 * sizeof(double),
-                             hipMemcpyDeviceToDevice, st);
+        // (kernel copies: this runs inside the engine's captured graph)
+        (void)copy_async(e->dxRecFrames + (size_t)feed * P * 2 * kDxFrame, e->dxFrames,
+                         (size_t)P * 2 * kDxFrame * sizeof(float), st);
+        (void)copy_async(e->dxRecOut + (size_t)feed * P * 2, e->dxOut, (size_t)P * 2 * sizeof(double), st);
       }
     }
     hipLaunchKernelGGL(dxcp_round_kernel, dim3((P + 63) / 64), dim3(64), 0, st, e->S, e->K, e->k0, nOwn, r, e->R, fed,
@@ -1439,6 +1445,19 @@ int danse_engine_dxcp_recorded(danse_engine* eng, int32_t* nFeeds, int32_t* nPai
   return 0;
 }
 
+int danse_engine_lanczos_stats(danse_engine* eng, int32_t* dst, size_t n) {
+  if (!eng || !dst) return fail(eng, "null argument");
+  if (n < (size_t)2 * eng->R) return fail(eng, "buffer too small: 2 R entries");
+  HIPCHK(hipSetDevice(eng->dev));
+  HIPCHK(hipDeviceSynchronize());
+  if (!eng->lzStats) {
+    std::fill(dst, dst + 2 * (size_t)eng->R, 0);
+    return 0;
+  }
+  HIPCHK(hipMemcpy(dst, eng->lzStats, (size_t)2 * eng->R * sizeof(int), hipMemcpyDeviceToHost));
+  return 0;
+}
+
 int danse_mi355x_fill(void* ptr, int32_t value, size_t bytes, void* stream) {
   danse_engine* eng = nullptr;   // (HIPCHK's error slot)
   if (!ptr && bytes) return fail(eng, "null pointer");
@@ -1764,10 +1783,12 @@ int danse_filter_update(const double* Ryy, const double* Rnn, int32_t B, int32_t
     wa.RyyD = (const cd*)Ryy; wa.Rnn = (const cd*)Rnn; wa.srcScene = (long long)D * D; wa.srcBin = 0;
     wa.nOut = 1; wa.refs[0] = ref; wa.wOff[0] = 0; wa.w = (cf*)w; wa.wScene = D; wa.wBin = 0;
     wa.diag = diag;
-    const long long chunk = std::min<long long>(B, 1024);
+    const long long chunk = wide::chunk_for(D, B);
     HIPCHK(hipMallocAsync((void**)&wa.work, (size_t)chunk * wide::work_elems(D) * sizeof(cd), st));
-    HIPCHK(wide::launch_wide_filters(wa, chunk, st));
-    HIPCHK(hipFreeAsync(wa.work, st));
+    const hipError_t le = wide::launch_wide_filters(wa, chunk, st);
+    const hipError_t fe = hipFreeAsync(wa.work, st);   // (released on the error path too)
+    HIPCHK(le);
+    HIPCHK(fe);
     return 0;
   }
   int G, DM;

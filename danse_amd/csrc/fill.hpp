@@ -27,8 +27,34 @@ __global__ void __launch_bounds__(256) fill8_kernel(uint8_t* __restrict__ p, uin
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) p[i] = v;
 }
 
+__global__ void __launch_bounds__(256) copy32_kernel(uint32_t* __restrict__ d, const uint32_t* __restrict__ s, size_t n) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) d[i] = s[i];
+}
+
+__global__ void __launch_bounds__(256) copy8_kernel(uint8_t* __restrict__ d, const uint8_t* __restrict__ s, size_t n) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) d[i] = s[i];
+}
+
 }  // namespace fillk
 }  // namespace
+
+// Device-to-device copy as a kernel node (a captured hipMemcpyAsync becomes a
+// memcpy node: the same node type family as the memset nodes above, so the
+// copies on capturable paths -- the DXCP input recording -- go through this).
+static inline hipError_t copy_async(void* dst, const void* src, size_t bytes, hipStream_t st) {
+  if (bytes == 0) return hipSuccess;
+  if ((((uintptr_t)dst | (uintptr_t)src) & 3u) == 0 && (bytes & 3u) == 0) {
+    const size_t n = bytes / 4;
+    const unsigned blocks = (unsigned)(n < (size_t)256 * 4096 ? (n + 255) / 256 : 4096);
+    hipLaunchKernelGGL(fillk::copy32_kernel, dim3(blocks), dim3(256), 0, st, (uint32_t*)dst, (const uint32_t*)src, n);
+  } else {
+    const unsigned blocks = (unsigned)(bytes < (size_t)256 * 4096 ? (bytes + 255) / 256 : 4096);
+    hipLaunchKernelGGL(fillk::copy8_kernel, dim3(blocks), dim3(256), 0, st, (uint8_t*)dst, (const uint8_t*)src, bytes);
+  }
+  return hipGetLastError();
+}
 
 // hipMemsetAsync's signature: every byte of [p, p + bytes) set to (uint8_t)value.
 static inline hipError_t fill_async(void* p, int value, size_t bytes, hipStream_t st) {

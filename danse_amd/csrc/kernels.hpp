@@ -110,6 +110,9 @@ struct UpdateArgs {
   // after it updates it by rank one instead of refactoring; null = off
   cd* l64Cache;
   long long l64Stride;
+  // [R][2] or null: per round the bins whose warm Lanczos solve was accepted
+  // and those sent back to the Householder path (diagnostics)
+  int* lzStats;
 };
 
 DANSE_DEV bool node_in(unsigned mask, int k) { return ((mask >> k) & 1u) != 0u; }

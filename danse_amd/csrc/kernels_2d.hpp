@@ -210,7 +210,10 @@ update_kernel_2d(const UpdateArgs a) {
         A.v[sb][tb] = x;
       });
     });
-    if (solve) gevd2d_filter<NB, RMAX, G>(A, S, li, D, a.rank, w, vC, fvalid);
+    if (solve) {
+      const int path = gevd2d_filter<NB, RMAX, G>(A, S, li, D, a.rank, w, vC, fvalid);
+      if (path && a.lzStats && li == 0 && fvalid) atomicAdd(&a.lzStats[2 * r + path - 1], 1);
+    }
   }
 
   const long long wBase = (long long)s * a.wStride + d.wOff;

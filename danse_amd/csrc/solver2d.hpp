@@ -1042,12 +1042,13 @@ DANSE_DEV void eigen2d(LDS2<NB, G>& S, int li, int D, int R, cf (&w)[vpl<NB, G>(
 template <int DM>
 constexpr int kLz() { return (DM - 1) / 2 < 8 ? (DM - 1) / 2 : 8; }
 constexpr float kLzTol = 3.0e-6f;
+constexpr float kLzBreak = 1.0e-6f;   // first-step breakdown test (relative to theta)
 
 // true (wave-uniform) if every bin of the wave converged: then vv (lane
 // layout) is the unit eigenvector of C and lam1 its eigenvalue
 template <int NB, int G = 8>
 DANSE_DEV bool lanczos2d(const Blk<NB>& A, LDS2<NB, G>& S, int li, int D, const cf* vIn, cf (&vv)[vpl<NB, G>()],
-                         float& lam1) {
+                         float& lam1, bool& warm) {
   constexpr int DM = G * NB, L = bin_lanes<G>(), V = vpl<NB, G>(), M = kLz<DM>();
   static_assert(M * DM <= DM * (DM - 1) / 2, "the Lanczos basis lives in the reflector space");
   const int p = li / G, q = li % G;
@@ -1064,10 +1065,19 @@ DANSE_DEV bool lanczos2d(const Blk<NB>& A, LDS2<NB, G>& S, int li, int D, const 
   });
   n0 = sumq<G>(n0);
   bool ok = n0 > 1e-30f && n0 < 1e30f;
+  warm = __ballot(n0 > 1e-30f) != 0ull;   // (a bin's first solve has no start vector: a cold solve)
   const float s0 = ok ? frsq(n0) : 0.0f;
   sfor<0, NB>([&](auto tc) { vc[decltype(tc)::value] = s0 * vc[decltype(tc)::value]; });
   if (p == 0) sfor<0, NB>([&](auto tc) { Q[q + G * decltype(tc)::value] = vc[decltype(tc)::value]; });
-  float blast = 0.0f;
+  float blast = 0.0f, b0 = 0.0f;
+  // largest diagonal entry of C: a lower bound of lambda_1 (the Rayleigh
+  // quotient of a unit vector), checked against the Ritz value below
+  float dmax1 = -3.0e38f;
+  sfor<0, NB>([&](auto sc) {
+    constexpr int sb = decltype(sc)::value;
+    if (p == q && p + G * sb < D) dmax1 = fmaxf(dmax1, A.v[sb][sb].re);
+  });
+  const float dmax = gmax<L>(dmax1);
   // k = 0 .. M - 1, unrolled (the orthogonalisation's loops get static bounds)
   sfor<0, M>([&](auto kc) {
     constexpr int k = decltype(kc)::value;
@@ -1124,6 +1134,7 @@ DANSE_DEV bool lanczos2d(const Blk<NB>& A, LDS2<NB, G>& S, int li, int D, const 
     sfor<0, NB>([&](auto tc) { vc[decltype(tc)::value] = ib * wc[decltype(tc)::value]; });
     if (k + 1 < M && p == 0) sfor<0, NB>([&](auto tc) { Q[(k + 1) * DM + q + G * decltype(tc)::value] = vc[decltype(tc)::value]; });
     blast = b;
+    if constexpr (k == 0) b0 = b;
     wsync();
   });
   // top Ritz pair of the M x M tridiagonal (the full path's eigen routines)
@@ -1150,7 +1161,14 @@ DANSE_DEV bool lanczos2d(const Blk<NB>& A, LDS2<NB, G>& S, int li, int D, const 
   ny = sumq<G>(ny);
   const float theta = lam[0];
   const float res = blast * fabsf(sm);
+  // Accept on the Lanczos residual, and only when nothing says the Ritz pair
+  // may be a lower eigenpair (an eigenvalue crossing since the start vector
+  // was the top one): a first step that already breaks down (the start
+  // vector spans an invariant subspace on its own: exact, but not
+  // necessarily the top pair) and a Ritz value below a diagonal entry of C
+  // (a Rayleigh quotient: lambda_1 is at least that) send the bin back.
   ok = ok && ny > 0.5f && theta > 0.0f && theta < 3.0e38f && res <= kLzTol * theta;
+  ok = ok && b0 > kLzBreak * theta && theta >= dmax * (1.0f - 4.0e-6f);
   const float sy = frsq(fmaxf(ny, 1e-30f));
   // lane layout through LDS
   if (p == 0) sfor<0, NB>([&](auto tc) { S.vb[q + G * decltype(tc)::value] = sy * yc[decltype(tc)::value]; });
@@ -1221,17 +1239,22 @@ DANSE_DEV void rank1_w2d(LDS2<NB, G>& S, int li, int D, const cf (&vv)[vpl<NB, G
 // vCache (rank 1, or null): this bin's eigenvector of C from its previous
 // solve (the Lanczos start; zero = none), rewritten with this solve's (store:
 // the bin is real, not a padding copy)
+// Returns the path (wave-uniform): 0 the Householder path (no warm start
+// tried, or none to try from), 1 the warm Lanczos solve accepted, 2 the warm
+// solve tried and sent back to the Householder path.
 template <int NB, int RMAX, int G = 8>
-DANSE_DEV void gevd2d_filter(Blk<NB>& A, LDS2<NB, G>& S, int li, int D, int R, cf (&w)[vpl<NB, G>()],
-                             cf* vCache = nullptr, bool store = false) {
+DANSE_DEV int gevd2d_filter(Blk<NB>& A, LDS2<NB, G>& S, int li, int D, int R, cf (&w)[vpl<NB, G>()],
+                            cf* vCache = nullptr, bool store = false) {
   constexpr int V = vpl<NB, G>(), L = bin_lanes<G>(), DM = G * NB;
   congruence2d<NB, G>(A, S, li, D);
+  int path = 0;
   // (classes below 20: too few Lanczos steps fit, and the D-step Householder
   // path is short there -- measured slower with the warm start)
   if (G * NB >= 20 && vCache && R == 1) {
     cf vv[V];
     float lam1;
-    if (lanczos2d<NB, G>(A, S, li, D, vCache, vv, lam1)) {
+    bool warm;
+    if (lanczos2d<NB, G>(A, S, li, D, vCache, vv, lam1, warm)) {
       rank1_w2d<NB, G>(S, li, D, vv, lam1, w);
       if (store) {
         sfor<0, V>([&](auto vc) {
@@ -1239,11 +1262,13 @@ DANSE_DEV void gevd2d_filter(Blk<NB>& A, LDS2<NB, G>& S, int li, int D, int R, c
           if (i < DM) vCache[i] = vv[decltype(vc)::value];
         });
       }
-      return;
+      return 1;
     }
+    path = warm ? 2 : 0;
   }
   tridiag2d<NB, G>(A, S, li, D);
   eigen2d<NB, RMAX, G>(S, li, D, R, w, R == 1 ? vCache : nullptr, store);
+  return path;
 }
 
 }  // namespace t2d

@@ -33,6 +33,14 @@ struct WideArgs {   // (passed by value: the per-output tables ride in the kerne
 // launch (a.work holds chunk * work_elems(D) complex doubles).
 hipError_t launch_wide_filters(const WideArgs& a, long long chunk, hipStream_t st);
 inline size_t work_elems(int D) { return (size_t)2 * D * D; }
+// workgroups per launch for nItems items: at most 1024 and at most a 1 GiB
+// float64 workspace (512 at D = 256), at least one per CU (256)
+constexpr size_t kWorkBudget = (size_t)1 << 30;
+inline long long chunk_for(int D, long long nItems) {
+  long long c = (long long)(kWorkBudget / (work_elems(D) * sizeof(cd)));
+  c = c < 256 ? 256 : (c > 1024 ? 1024 : c);
+  return nItems < c ? (nItems > 0 ? nItems : 1) : c;
+}
 
 }  // namespace wide
 }  // namespace danse

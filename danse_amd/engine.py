@@ -884,6 +884,16 @@ class DanseEngine:
     def diagnostics(self):
         return self._get(L.OUT_DIAG, dtype=np.int32, shape=(self.S, self.K, 4))
 
+    def lanczos_stats(self):
+        """[R][2] int32 of the last run: per round, the bins whose warm-started
+        rank-1 Lanczos solve was accepted and the bins its acceptance test sent
+        back to the Householder path (lane-grid GEVD classes of DMAX >= 20;
+        zeros elsewhere)."""
+        out = np.zeros((self.R, 2), dtype=np.int32)
+        L.check(self.lib.danse_engine_lanczos_stats(
+            self.eng, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), out.size), self.eng)
+        return out
+
     def dxcp_record(self, on=True):
         """Record every DXCP-PhaT feed's gathered input frames and estimator
         outputs over the following runs (estimateSROs='DXCPPhaT')."""

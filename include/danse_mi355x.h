@@ -225,6 +225,12 @@ int danse_engine_dxcp_recorded(danse_engine* eng, int32_t* nFeeds, int32_t* nPai
  * the wait, at the publish); *bytes in: capacity of dst (may be NULL), out:
  * the size. */
 int danse_engine_resident_trace(danse_engine* eng, void* dst, size_t* bytes);
+/* Diagnostics of the warm-started rank-1 Lanczos path of the lane-grid GEVD
+ * classes (update_w_gevd, d_classes.py:3343-3387, solved by solver2d.hpp
+ * lanczos2d): per round of the last run, [R][2] int32 -- the bins whose warm
+ * solve was accepted, and the bins the acceptance test sent back to the
+ * Householder path.  n: capacity of dst in elements (>= 2 R). */
+int danse_engine_lanczos_stats(danse_engine* eng, int32_t* dst, size_t n);
 
 /* Condition numbers of Ryy (ConditionNumbers.get_new_cond_number,
  * d_classes.py:19-130,2126-2186; saveConditionNumber /

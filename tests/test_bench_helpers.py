@@ -11,14 +11,21 @@ from oracle import danse_ref_cpu as O
 def test_alg_bytes_flops():
     D = 11
     t = D * (D + 1)
-    # VAD frame with a solve: Ryy r+w (c64) + read Rnn (c128) + y, w, dhat
-    assert bench.alg_bytes_update(D, 1, 0, True) == 16 * D + 8 + 8 * t + 8 * t
-    # noise frame without a solve: Rnn r+w (c128)
-    assert bench.alg_bytes_update(D, 0, 1, False) == 16 * D + 8 + 16 * t
+    AVG, SET, KEEP = bench.OP_AVG, bench.OP_SET, bench.OP_KEEP
+    assert (KEEP, SET, AVG) == (0, 1, 2)
+    # SURVEY §8d (c64 packed): VAD frame with a solve = B_cov + the solve's
+    # read of Rnn and write of w: 1.15 KB + 0.62 KB at D = 11
+    assert bench.alg_bytes_update(D, AVG, KEEP, True) == 8 * t + 8 * D + 8 + 4 * t + 8 * D == 1768
+    # noise frame without a solve: Rnn read + write
+    assert bench.alg_bytes_update(D, KEEP, AVG, False) == 8 * D + 8 + 8 * t
     # first frame sets the SCM: write only
-    assert bench.alg_bytes_update(D, 2, 0, False) == 16 * D + 8 + 4 * t
-    b = bench.alg_bytes_update(D, np.array([1, 0]), np.array([0, 1]), np.array([True, False]))
+    assert bench.alg_bytes_update(D, SET, KEEP, False) == 8 * D + 8 + 4 * t
+    assert bench.alg_bytes_update(39, AVG, KEEP, True) == 8 * 39 * 40 + 8 * 39 + 8 + 4 * 39 * 40 + 8 * 39
+    b = bench.alg_bytes_update(D, np.array([AVG, KEEP]), np.array([KEEP, AVG]), np.array([True, False]))
     assert b.shape == (2,)
+    # engine storage: Ryy c64, Rnn c128 (twice the bytes), the w ring
+    assert bench.storage_bytes_update(D, KEEP, AVG, False) == 8 * D + 8 + 16 * t + 16 * D
+    assert bench.storage_bytes_update(D, AVG, KEEP, True) == 8 * D + 8 + 8 * t + 8 * t + 8 * D
     assert bench.alg_flops_update(D, 0, 0, False) == 8 * D
     assert np.isclose(bench.alg_flops_update(39, 1, 0, True), 8 * 39 + 5 * 39 * 40 + 32 / 3 * 39 ** 3 + 12 * 39 ** 2)
 

@@ -224,6 +224,71 @@ def test_headline_shape_K32x8_D39_vs_oracle():
     assert de <= 1e-4
 
 
+N2_LONG_POST_ROUNDS = 44
+
+
+def test_headline_shape_K32x8_D39_long_run_vs_oracle():
+    """The headline shape's steady-state solve path, pinned over many solves
+    per bin: K = 32 x 8 (D = 39), asy, with 0.9 s speech pauses so that every
+    node's gate opens at round 84 (`test_headline_shape_K32x8_D39_vs_oracle`'s
+    scene opens it at 153 and compares about two solves per bin).  The oracle
+    runs N2_LONG_POST_ROUNDS rounds past the gate: each bin's filter goes
+    through the warm-started Lanczos solve (solver2d.hpp lanczos2d) and the
+    rank-one moves of the float64 factor record (li_rank1_2d) dozens of times
+    in a row (update_w_gevd, d_classes.py:3343-3387; the recursion,
+    d_classes.py:2086-2090).  The per-round Lanczos acceptance counts
+    (danse_engine_lanczos_stats) are printed and must show the warm path
+    carrying the post-gate rounds."""
+    from danse_amd.engine import DanseEngine
+    from danse_amd.scene import make_scene
+    from oracle import danse_ref_cpu as O
+    import os
+    case = dict(name='online_N2_K32x8_long', M=[8] * 32, dur=4.5, seed=41, danse=dict(BATTERY, nodeUpdating='asy'))
+    dp, wp = make_case_params(case)
+    sc = make_scene(case['M'], sigDur=case['dur'], seed=case['seed'], pauseDuration=0.9)
+    sc.get_vad_per_frame(dp.DFTsize, dp.Ns, wp.vadMinProportionActive)
+    K, D = 32, 39
+    eng = DanseEngine([sc], dp)
+    try:
+        eng.run()
+        dv = eng.outputs()[0]
+        lz = eng.lanczos_stats()
+        diag = eng.diagnostics()
+    finally:
+        eng.close()
+    R0 = int(np.max(dv.startRound)) + N2_LONG_POST_ROUNDS
+    assert R0 + 2 <= eng.R, (R0, eng.R)
+    O.set_workers(min(16, max(2, len(os.sched_getaffinity(0)))))
+    try:
+        ov = O.OnlineDANSE(sc, dp, vadMinProp=wp.vadMinProportionActive, maxRounds=R0).run()
+    finally:
+        O.set_workers(0)
+    assert np.array_equal(dv.startRound, ov.startRound)
+    assert int(np.max(ov.startRound)) <= 90, ov.startRound
+    assert int(np.sum(diag)) == 0
+    errs, last = [], []
+    for k in range(K):
+        s0 = int(ov.startRound[k])
+        e = _bin_rel(dv.wTilde[k][:, s0 + 1:R0 + 1], ov.wTilde[k][:, s0 + 1:R0 + 1])   # [F][rounds]
+        errs.append(e.ravel())
+        last.append(e[:, -1])
+    st = _stats(np.concatenate(errs))
+    st_last = _stats(np.concatenate(last))
+    T1 = int(ov.idxEnd) - (dp.DFTsize - dp.Ns)
+    de = rel_err(dv.d[:T1], ov.d[:T1])
+    s0 = int(np.min(ov.startRound))
+    acc, back = lz[s0:R0, 0], lz[s0:R0, 1]
+    print(case['name'], 'rounds', R0, 'post-gate', R0 - s0, 'w', st, 'last round', st_last, 'd', de)
+    print('lanczos accepted per launch', acc.tolist())
+    print('lanczos sent back per launch', back.tolist())
+    # every post-gate round after the first solve: all K * F bins solve, and
+    # the warm path must carry them (the first solve of a bin is cold)
+    assert np.all(acc[2:] + back[2:] == K * 513), (acc, back)
+    assert acc[2:].sum() >= 0.9 * (R0 - s0 - 2) * K * 513, (acc.sum(), back.sum())
+    assert st['median'] <= 1e-5 and st['p99'] <= 1e-4 and st['max'] <= 1e-3, st
+    assert de <= 1e-4
+
+
 @pytest.mark.parametrize('name', ['online_C_sro_comp_asy', 'online_ragged_asy_r2', 'online_E_fs_L64_asy'])
 def test_dv_fields_on_device(name):
     """Every dv field the reference's post-processing reads is present; the
