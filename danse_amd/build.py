@@ -66,43 +66,60 @@ def _stale(obj: Path, src: Path) -> bool:
     return any(p.stat().st_mtime > t for p in [src, *_deps(src)])
 
 
-def up_to_date() -> bool:
-    if not OUT.exists():
+# A/B variants of the same library (compile-time switches; loaded with
+# DANSE_LIB=danse_amd/libdanse_<name>.so): objects in _obj/<name>/
+VARIANTS = {
+    'stamp': ['-DDANSE_STAMP=1'],   # per-wave phase clocks in update_kernel_2d (DANSE_UPDATE_TRACE)
+}
+
+
+def _paths(variant):
+    if variant is None:
+        return OBJ, OUT
+    return OBJ / variant, HERE / f'libdanse_{variant}.so'
+
+
+def up_to_date(variant: str | None = None) -> bool:
+    obj, out = _paths(variant)
+    if not out.exists():
         return False
-    t = OUT.stat().st_mtime
-    return all(not _stale(OBJ / o, s) and (OBJ / o).stat().st_mtime <= t for o, s, _ in _units())
+    t = out.stat().st_mtime
+    return all(not _stale(obj / o, s) and (obj / o).stat().st_mtime <= t for o, s, _ in _units())
 
 
-def build(force: bool = False, verbose: bool = True, jobs: int | None = None) -> Path:
-    if not force and up_to_date():
-        return OUT
+def build(force: bool = False, verbose: bool = True, jobs: int | None = None, variant: str | None = None) -> Path:
+    obj, out = _paths(variant)
+    if not force and up_to_date(variant):
+        return out
     hipcc = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
-    OBJ.mkdir(exist_ok=True)
-    todo = [(o, s, x) for o, s, x in _units() if force or _stale(OBJ / o, s)]
+    obj.mkdir(parents=True, exist_ok=True)
+    vflags = VARIANTS[variant] if variant else []
+    todo = [(o, s, x) for o, s, x in _units() if force or _stale(obj / o, s)]
 
     def compile_one(item):
         o, s, x = item
-        cmd = [hipcc, *FLAGS, f'-I{INC}', *x, '-c', str(s), '-o', str(OBJ / o) + '.tmp']
+        cmd = [hipcc, *FLAGS, f'-I{INC}', *vflags, *x, '-c', str(s), '-o', str(obj / o) + '.tmp']
         if verbose:
             print(' '.join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f'hipcc failed for {o}:\n{r.stderr}')
-        os.replace(str(OBJ / o) + '.tmp', OBJ / o)
+        os.replace(str(obj / o) + '.tmp', obj / o)
 
     n = jobs or min(16, os.cpu_count() or 4, max(1, len(todo)))
     # heaviest classes first so the pool drains evenly
     todo.sort(key=lambda it: -int(it[0][8:-2]) if it[0].startswith('update_d') else 0)
     with ThreadPoolExecutor(max_workers=n) as ex:
         list(ex.map(compile_one, todo))
-    cmd = [hipcc, '--offload-arch=gfx950', '-fPIC', '-shared', *[str(OBJ / o) for o, _, _ in _units()],
-           '-o', str(OUT) + '.tmp']
+    cmd = [hipcc, '--offload-arch=gfx950', '-fPIC', '-shared', *[str(obj / o) for o, _, _ in _units()],
+           '-o', str(out) + '.tmp']
     if verbose:
         print(' '.join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    os.replace(str(OUT) + '.tmp', OUT)
-    return OUT
+    os.replace(str(out) + '.tmp', out)
+    return out
 
 
 if __name__ == '__main__':
-    build(force='--force' in sys.argv)
+    _v = [a.split('=', 1)[1] for a in sys.argv[1:] if a.startswith('--variant=')]
+    build(force='--force' in sys.argv, variant=_v[0] if _v else None)

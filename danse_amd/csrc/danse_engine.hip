@@ -146,8 +146,9 @@ struct danse_engine {
   int *resGateRound = nullptr, *resDanseFni = nullptr, *resErr = nullptr, *resFams = nullptr;
   float* resFrames = nullptr;
   int* resChanNode = nullptr;        // [MT] node of each channel
-  unsigned long long* resTrace = nullptr;   // DANSE_RESIDENT_TRACE diagnostics
+  unsigned long long* resTrace = nullptr;   // DANSE_RESIDENT_TRACE / DANSE_UPDATE_TRACE diagnostics
   size_t resTraceBytes = 0;
+  int updTraceRound = -1;   // DANSE_UPDATE_TRACE=r: stamp build's per-wave marks of round r's update launch
   int resNFam = 0;
   // condition numbers of Ryy (cond.hpp), every condEvery-th iteration
   int condEvery = 0;
@@ -766,6 +767,13 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
   if (eng->liStride > 0) HIPCHK(dalloc(&eng->liCache, (size_t)S * eng->liStride));
   if (eng->vStride > 0) HIPCHK(dalloc(&eng->vCache, (size_t)S * eng->vStride));
   if (eng->vStride > 0) HIPCHK(dalloc(&eng->lzStats, (size_t)2 * R));
+  if (const char* tr = std::getenv("DANSE_UPDATE_TRACE")) {
+    // (upper bound: one wave per (scene, family-node, bin))
+    eng->updTraceRound = std::atoi(tr);
+    eng->resTraceBytes = (size_t)S * eng->fns.size() * F * (kStampN + 1) * sizeof(unsigned long long);
+    HIPCHK(hipMalloc((void**)&eng->resTrace, eng->resTraceBytes));
+    HIPCHK(hipMemset(eng->resTrace, 0, eng->resTraceBytes));
+  }
   if (eng->l64Stride > 0) HIPCHK(dalloc(&eng->l64Cache, (size_t)S * eng->l64Stride));
   if (c->dxcp) {
     if (c->cohDrift) return fail(eng, "DXCP-PhaT and CohDrift estimation are exclusive");
@@ -964,6 +972,7 @@ static void launch_update(danse_engine* e, int r, hipStream_t st, unsigned mask 
     a.famNodeId = cl.devIds;
     a.splitSolve = cl.split ? 1 : 0;
     a.noSolve = (!e->noRO && (int)cl.anySolve.size() > r && !cl.anySolve[r]) ? 1 : 0;
+    if (r == e->updTraceRound) a.stamps = e->resTrace;
     launch_update_class(cl.DMAX, a, st);   // D > kMaxDMax rejected at create time
     if (cl.split && cl.solveCount[r] > 0) {
       a.solveItems = cl.dSolveItems + (size_t)r * e->S * cl.host.size();

@@ -113,7 +113,12 @@ struct UpdateArgs {
   // [R][2] or null: per round the bins whose warm Lanczos solve was accepted
   // and those sent back to the Householder path (diagnostics)
   int* lzStats;
+  // DANSE_STAMP builds only (diagnostics): per launch wave, kStampN shader
+  // clock marks + a path code (update_kernel_2d), or null
+  unsigned long long* stamps;
 };
+
+constexpr int kStampN = 9;   // marks per wave; slot kStampN holds the path code
 
 DANSE_DEV bool node_in(unsigned mask, int k) { return ((mask >> k) & 1u) != 0u; }
 

@@ -16,6 +16,9 @@
 #ifndef DANSE_2D_WPE
 #define DANSE_2D_WPE 2
 #endif
+#ifndef DANSE_STAMP
+#define DANSE_STAMP 0   // diagnostics build (danse_amd.build variant 'stamp'): per-wave phase clocks
+#endif
 #include "solver2d.hpp"
 
 namespace danse {
@@ -47,6 +50,12 @@ update_kernel_2d(const UpdateArgs a) {
   LDS2<NB, G>& S = reinterpret_cast<LDS2<NB, G>*>(ldsRaw)[bw];   // (not touched when SM == 1)
   cf* const vb = (SM == 1) ? reinterpret_cast<cf*>(ldsRaw) + bw * L * V : S.vb;
   const int p = li / G, q = li % G;
+  unsigned long long tsv[kStampN];
+  int tcode = 0;
+  auto stamp = [&](int i) {
+    if constexpr (DANSE_STAMP) tsv[i] = __builtin_amdgcn_s_memtime();
+  };
+  stamp(0);
   const int F = a.F;
   const int FG = (F + W - 1) / W;
   const int fg = blockIdx.x % FG;
@@ -98,6 +107,7 @@ update_kernel_2d(const UpdateArgs a) {
     yc[sb] = vb[q + G * sb];
   });
   t2d::wsync();
+  stamp(1);
   const double beta = a.beta[s * a.K + d.k];
   // entry (i, c) of the SCM (both in range): the stored lower entry (hi, lo)
   // -- packed lower triangles, bin-major ([F][D(D+1)/2], FamNode.packed 2), or
@@ -159,16 +169,23 @@ update_kernel_2d(const UpdateArgs a) {
         M.v[sb][tb] = x;
       });
     });
+    stamp(2);
     if (solve && !reuse) {
       if (l64 && beta > 0.0 && li_updatable(a, d, s, opN)) {
         ok = li_rank1_2d<NB, G>(S, li, yc, beta, cy, l64, fvalid);
+        tcode |= 2;
       } else {
         ok = gevd2d_factor<NB, G>(M, S, li, D, d.ref, fvalid ? l64 : nullptr);
+        tcode |= 4;
       }
       if (liC && fvalid) li_store2d<NB, G>(S, liC, li);
     }
+  } else {
+    stamp(2);
   }
   if (reuse) li_load2d<NB, G>(S, liC, li);
+  tcode |= (opN ? 1 : 0) | (reuse ? 8 : 0) | (solve ? 16 : 0);
+  stamp(3);
 
   // ---- Ryy (float32): recursion, store, filter ---------------------------
   cf w[V];
@@ -210,11 +227,21 @@ update_kernel_2d(const UpdateArgs a) {
         A.v[sb][tb] = x;
       });
     });
+    stamp(4);
     if (solve) {
-      const int path = gevd2d_filter<NB, RMAX, G>(A, S, li, D, a.rank, w, vC, fvalid);
+      congruence2d<NB, G>(A, S, li, D);
+      stamp(5);
+      const int path = gevd2d_solve<NB, RMAX, G>(A, S, li, D, a.rank, w, vC, fvalid);
       if (path && a.lzStats && li == 0 && fvalid) atomicAdd(&a.lzStats[2 * r + path - 1], 1);
+      tcode |= path << 5;
+    } else {
+      stamp(5);
     }
+  } else {
+    stamp(4);
+    stamp(5);
   }
+  stamp(6);
 
   const long long wBase = (long long)s * a.wStride + d.wOff;
   const int slotPrev = a.wHistory ? r : (r & 1);
@@ -240,6 +267,17 @@ update_kernel_2d(const UpdateArgs a) {
     constexpr int v = decltype(vc)::value;
     node_bin_tail(a, d, s, f, li + L * v, fl, pregiven, fvalid, w[v], y[v], dh);
   });
+  if constexpr (DANSE_STAMP) {
+    stamp(7);
+    __builtin_amdgcn_s_waitcnt(0);   // (the stores drained: the last mark includes them)
+    stamp(8);
+    if (a.stamps && threadIdx.x <= kStampN) {
+      // lane i stores mark i (vector stores), lane kStampN the path code
+      unsigned long long v = (unsigned long long)tcode;
+      sfor<0, kStampN>([&](auto ic) { v = (threadIdx.x == decltype(ic)::value) ? tsv[decltype(ic)::value] : v; });
+      a.stamps[(long long)blockIdx.x * (kStampN + 1) + threadIdx.x] = v;
+    }
+  }
 }
 
 // Stand-alone GEVD filter update (danse_filter_update): float64 SCM pairs

@@ -1243,10 +1243,19 @@ DANSE_DEV void rank1_w2d(LDS2<NB, G>& S, int li, int D, const cf (&vv)[vpl<NB, G
 // tried, or none to try from), 1 the warm Lanczos solve accepted, 2 the warm
 // solve tried and sent back to the Householder path.
 template <int NB, int RMAX, int G = 8>
+DANSE_DEV int gevd2d_solve(Blk<NB>& A, LDS2<NB, G>& S, int li, int D, int R, cf (&w)[vpl<NB, G>()],
+                           cf* vCache = nullptr, bool store = false);
+template <int NB, int RMAX, int G = 8>
 DANSE_DEV int gevd2d_filter(Blk<NB>& A, LDS2<NB, G>& S, int li, int D, int R, cf (&w)[vpl<NB, G>()],
                             cf* vCache = nullptr, bool store = false) {
-  constexpr int V = vpl<NB, G>(), L = bin_lanes<G>(), DM = G * NB;
   congruence2d<NB, G>(A, S, li, D);
+  return gevd2d_solve<NB, RMAX, G>(A, S, li, D, R, w, vCache, store);
+}
+// the part after the congruence (C in A)
+template <int NB, int RMAX, int G>
+DANSE_DEV int gevd2d_solve(Blk<NB>& A, LDS2<NB, G>& S, int li, int D, int R, cf (&w)[vpl<NB, G>()], cf* vCache,
+                           bool store) {
+  constexpr int V = vpl<NB, G>(), L = bin_lanes<G>(), DM = G * NB;
   int path = 0;
   // (classes below 20: too few Lanczos steps fit, and the D-step Householder
   // path is short there -- measured slower with the warm start)
