@@ -55,6 +55,38 @@ def _work(args):
     return b1 - b0
 
 
+def gevd_w_chunk(Ryy, Rnn, S, X, ref, rank):
+    """w[:, :] of update_w_gevd (d_classes.py:3343-3387) for a stack of bins
+    whose eigenpairs (S ascending, X) are given: descending sort, Q = inv(X^H),
+    W = X D Q^H, column ref.  Every step is a per-matrix LAPACK / BLAS call, so
+    a bin's result does not depend on the stack it is computed in."""
+    nF, n = S.shape
+    Xmat = np.zeros((nF, n, n), dtype=complex)
+    sigma = np.zeros((nF, n))
+    for kappa in range(nF):
+        idx = np.flip(np.argsort(S[kappa]))
+        sigma[kappa, :] = S[kappa][idx]
+        Xmat[kappa] = X[kappa][:, idx]
+    Qmat = np.linalg.inv(np.transpose(Xmat.conj(), axes=[0, 2, 1]))
+    Dmat = np.zeros((nF, n, n))
+    for r in range(rank):
+        Dmat[:, r, r] = np.squeeze(1 - 1 / sigma[:, r])
+    Qh = np.transpose(Qmat.conj(), axes=[0, 2, 1])
+    fullW = np.matmul(np.matmul(Xmat, Dmat), Qh)
+    return fullW[:, :, ref]
+
+
+def _work_w(args):
+    import scipy.linalg as sla
+    F, n, b0, b1, ref, rank = args
+    A, B, X, S = _views(_W.buf, F, n)
+    for kappa in range(b0, b1):
+        S[kappa], X[kappa] = sla.eigh(A[kappa], B[kappa])
+    w = gevd_w_chunk(A[b0:b1], B[b0:b1], S[b0:b1], X[b0:b1], ref, rank)
+    X[b0:b1, 0, :] = w      # (the chunk's eigenvectors are no longer needed)
+    return b1 - b0
+
+
 class _Pool:
     def __init__(self, workers):
         self.workers = workers
@@ -79,6 +111,17 @@ class _Pool:
         done = sum(self.pool.map(_work, [(F, n, b, min(b + step, F)) for b in range(0, F, step)]))
         assert done == F
         return S.copy(), X.copy()
+
+    def gevd_w(self, Ryy, Rnn, ref, rank):
+        F, n, _ = Ryy.shape
+        self._ensure(F * n * (48 * n + 8))
+        A, B, X, S = _views(self.shm.buf, F, n)
+        A[:] = Ryy
+        B[:] = Rnn
+        step = -(-F // (4 * self.workers))
+        done = sum(self.pool.map(_work_w, [(F, n, b, min(b + step, F), ref, rank) for b in range(0, F, step)]))
+        assert done == F
+        return X[:, 0, :].copy()
 
     def close(self):
         if self.pool is not None:
@@ -115,6 +158,16 @@ def eigh_bins(Ryy, Rnn):
     for kappa in range(F):
         S[kappa], X[kappa] = sla.eigh(Ryy[kappa], Rnn[kappa])
     return S, X
+
+
+def gevd_w_bins(Ryy, Rnn, ref, rank):
+    """update_w_gevd's filters w [F][n]: with workers, each worker runs the
+    whole per-bin computation (eigh, sort, inverse, product) for its chunk of
+    bins; None without workers (the caller's serial path)."""
+    if _POOL is not None and Ryy.shape[0] >= 8:
+        return _POOL.gevd_w(np.ascontiguousarray(Ryy, dtype=np.complex128),
+                            np.ascontiguousarray(Rnn, dtype=np.complex128), ref, rank)
+    return None
 
 
 @atexit.register

@@ -28,7 +28,7 @@ import scipy.signal as sig
 
 from danse_amd.scheduler import initialize_events
 
-from ._gevd_pool import eigh_bins, set_workers  # noqa: F401
+from ._gevd_pool import eigh_bins, gevd_w_bins, set_workers  # noqa: F401
 
 
 # --------------------------------------------------------------------------- #
@@ -186,6 +186,11 @@ def update_w_gevd(Ryy, Rnn, refSensorIdx, rank=1):
     ``scipy.linalg.eigh(Ryy, Rnn)``, descending sort, W = X D X^{-1})."""
     n = Ryy.shape[-1]
     nFreqs = Ryy.shape[0]
+    # with worker processes (oracle/_gevd_pool.py) the whole per-bin
+    # computation below runs in them, chunked over bins (bit-identical)
+    wp = gevd_w_bins(Ryy, Rnn, refSensorIdx, rank)
+    if wp is not None:
+        return wp
     Xmat = np.zeros((nFreqs, n, n), dtype=complex)
     sigma = np.zeros((nFreqs, n))
     # the per-bin eigh calls (serial, or spread over worker processes with
@@ -487,6 +492,10 @@ class OnlineDANSE:
         nUp = 0
         import time as _time
         self.roundTimes = [(int(np.min(self.i)), _time.perf_counter())]
+        # (progressEvery: a progress line on stderr every that many rounds --
+        # long parity runs on the GPU box must keep writing)
+        pe = getattr(self, 'progressEvery', None)
+        lastRep = 0
         for ev in events:
             for ii in range(ev.nEvents):
                 k = ev.nodes[ii]
@@ -498,6 +507,11 @@ class OnlineDANSE:
                     self.update_and_estimate(ev.t, fs[k], k, ev.bypassUpdate[ii])
                     nUp += 1
             self.roundTimes.append((int(np.min(self.i)), _time.perf_counter()))
+            if pe and self.roundTimes[-1][0] >= lastRep + pe:
+                lastRep = self.roundTimes[-1][0]
+                import sys as _sys
+                print(f'# oracle round {lastRep} ({self.roundTimes[-1][1] - self.roundTimes[0][1]:.1f} s)',
+                      file=_sys.stderr, flush=True)
             if self.maxRounds is not None and np.all(self.i >= self.maxRounds):
                 break
         self.nUpdateEvents = nUp

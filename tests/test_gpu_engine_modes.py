@@ -224,7 +224,7 @@ def test_headline_shape_K32x8_D39_vs_oracle():
     assert de <= 1e-4
 
 
-N2_LONG_POST_ROUNDS = 44
+N2_LONG_POST_ROUNDS = 40
 
 
 def test_headline_shape_K32x8_D39_long_run_vs_oracle():
@@ -260,7 +260,9 @@ def test_headline_shape_K32x8_D39_long_run_vs_oracle():
     assert R0 + 2 <= eng.R, (R0, eng.R)
     O.set_workers(min(16, max(2, len(os.sched_getaffinity(0)))))
     try:
-        ov = O.OnlineDANSE(sc, dp, vadMinProp=wp.vadMinProportionActive, maxRounds=R0).run()
+        ov = O.OnlineDANSE(sc, dp, vadMinProp=wp.vadMinProportionActive, maxRounds=R0)
+        ov.progressEvery = 4
+        ov.run()
     finally:
         O.set_workers(0)
     assert np.array_equal(dv.startRound, ov.startRound)
