@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import atexit
 import multiprocessing as mp
+import os
 from multiprocessing import shared_memory
 
 import numpy as np
@@ -99,7 +100,22 @@ class _Pool:
         self.close()
         self.shm = shared_memory.SharedMemory(create=True, size=max(nbytes, 1 << 20))
         ctx = mp.get_context('spawn')
-        self.pool = ctx.Pool(self.workers, initializer=_attach, initargs=(self.shm.name,))
+        # single-threaded BLAS / LAPACK in the workers from their start (the
+        # environment a spawned interpreter inherits: threadpoolctl alone did
+        # not hold every BLAS the workers load to one thread, and 16 workers x
+        # 16 BLAS threads oversubscribed the GPU box's CPU share)
+        keys = ('OMP_NUM_THREADS', 'OPENBLAS_NUM_THREADS', 'MKL_NUM_THREADS', 'BLIS_NUM_THREADS')
+        old = {k: os.environ.get(k) for k in keys}
+        try:
+            for k in keys:
+                os.environ[k] = '1'
+            self.pool = ctx.Pool(self.workers, initializer=_attach, initargs=(self.shm.name,))
+        finally:
+            for k, v in old.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
 
     def eigh(self, Ryy, Rnn):
         F, n, _ = Ryy.shape
