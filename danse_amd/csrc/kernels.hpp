@@ -198,9 +198,17 @@ DANSE_DEV bool li_updatable(const UpdateArgs& a, const FamNode& d, int s, int op
 // bin f: a local spectrum, or the fused spectrum of sender q (the frame of
 // round r or r-1, zLag) with the SRO phase compensation
 // yhat *= exp(-j 2 pi f phi / N) of compensate_sros (d_classes.py:1936-2046).
+DANSE_DEV cf load_y_c(const UpdateArgs& a, const FamNode& d, int s, int f, int c, bool act);
+DANSE_DEV int chan_of(const UpdateArgs& a, const FamNode& d, int li, bool act) {
+  return a.chanList[d.chanOff + (act ? li : 0)];
+}
 DANSE_DEV cf load_y(const UpdateArgs& a, const FamNode& d, int s, int f, int li, bool act) {
+  return load_y_c(a, d, s, f, chan_of(a, d, li, act), act);
+}
+// (the same, from the channel id: callers that issue other loads between the
+// channel-id load and the spectrum load)
+DANSE_DEV cf load_y_c(const UpdateArgs& a, const FamNode& d, int s, int f, int c, bool act) {
   const int F = a.F, r = a.r;
-  const int c = a.chanList[d.chanOff + (act ? li : 0)];
   const int rawBase = a.MT + a.K;
   cf v;
   if (c < a.MT) {

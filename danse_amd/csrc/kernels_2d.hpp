@@ -92,12 +92,66 @@ update_kernel_2d(const UpdateArgs a) {
                ? a.vCache + (long long)s * a.vStride + d.vOff + (long long)f * (G * NB)
                : nullptr;
 
+  // Loads of the solve on a cached factor (the common solve: a VAD frame,
+  // Rnn unchanged since the last factorisation) issued with the observation's:
+  // the factor record (S.Ls + g) and the Ryy block, so that the record, the
+  // block and the spectra are one memory round trip instead of three.
+  constexpr int kRec = t2d::li_record<NB, G>(), kRecL = (kRec + L - 1) / L, kNL = G * NB * (G * NB + 1) / 2;
+  const long long triOff0 = PK ? (long long)s * a.scmStride + d.scmOff + f
+                               : (long long)s * a.scmStride + d.scmOff + (long long)f * (D * (D + 1) / 2);
+  auto entA = [&](int i, int c) -> long long {
+    const int hi = i >= c ? i : c, lo = i >= c ? c : i;
+    const long long t = hi * (hi + 1) / 2 + lo;
+    return PK ? triOff0 + t * F : triOff0 + t;
+  };
+  Blk<NB> A;
+  cf lrec[kRecL];
+  int ych[V];
+  sfor<0, V>([&](auto vc) {
+    constexpr int v = decltype(vc)::value;
+    const int i = li + L * v;
+    ych[v] = chan_of(a, d, i, i < D);
+  });
+  if constexpr (SM != 1) {
+    if (reuse) {
+      sfor<0, kRecL>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        const int e = li + L * j;
+        lrec[j] = liC[e < kRec ? e : 0];
+      });
+      sfor<0, NB>([&](auto sc) {
+        constexpr int sb = decltype(sc)::value;
+        sfor<0, NB>([&](auto tc) {
+          constexpr int tb = decltype(tc)::value;
+          const int i = p + G * sb, c = q + G * tb;
+          const bool in = i < D && c < D;
+          A.v[sb][tb] = a.Ryy[in ? entA(i, c) : triOff0];
+        });
+      });
+    }
+  }
   cf y[V];
   sfor<0, V>([&](auto vc) {
     constexpr int v = decltype(vc)::value;
     const int i = li + L * v;
-    y[v] = load_y(a, d, s, f, i, i < D);
-    vb[i] = y[v];
+    y[v] = load_y_c(a, d, s, f, ych[v], i < D);
+  });
+  if constexpr (SM != 1) {
+    if (reuse) {
+      hold(lrec);
+      sfor<0, NB>([&](auto sc) { hold(A.v[decltype(sc)::value]); });
+      // the record into LDS (li_load2d's layout: [0, kNL) S.Ls, then g)
+      sfor<0, kRecL>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        const int e = li + L * j;
+        if (e < kNL) S.Ls[e] = lrec[j];
+        else if (e < kRec) S.g[e - kNL] = lrec[j];
+      });
+    }
+  }
+  sfor<0, V>([&](auto vc) {
+    constexpr int v = decltype(vc)::value;
+    vb[li + L * v] = y[v];
   });
   t2d::wsync();
   cf yr[NB], yc[NB];
@@ -183,7 +237,6 @@ update_kernel_2d(const UpdateArgs a) {
   } else {
     stamp(2);
   }
-  if (reuse) li_load2d<NB, G>(S, liC, li);
   tcode |= (opN ? 1 : 0) | (reuse ? 8 : 0) | (solve ? 16 : 0);
   stamp(3);
 
@@ -191,7 +244,6 @@ update_kernel_2d(const UpdateArgs a) {
   cf w[V];
   sfor<0, V>([&](auto vc) { w[decltype(vc)::value] = cf{0.0f, 0.0f}; });
   if (opY || solve) {
-    Blk<NB> A;
     const float by = (float)beta, cy = (opY == DANSE_OP_SET) ? (float)(1.0 / D) : (float)((1.0 - beta) / D);
     auto ld_row_Ryy = [&](auto sc) {
       constexpr int sb = decltype(sc)::value;
@@ -203,8 +255,10 @@ update_kernel_2d(const UpdateArgs a) {
       });
     };
     if constexpr (SM != 1) {
-      sfor<0, NB>(ld_row_Ryy);
-      sfor<0, NB>([&](auto sc) { hold(A.v[decltype(sc)::value]); });
+      if (!reuse) {   // (reuse: loaded with the observation above)
+        sfor<0, NB>(ld_row_Ryy);
+        sfor<0, NB>([&](auto sc) { hold(A.v[decltype(sc)::value]); });
+      }
     }
     sfor<0, NB>([&](auto sc) {
       constexpr int sb = decltype(sc)::value;

@@ -570,9 +570,12 @@ DANSE_DEV void congruence2d(Blk<NB>& A, LDS2<NB, G>& S, int li, int D) {
       if (c < G * sk + p) S.cz[p][c] = conjg(A.v[sk][s]);    // (c, 8 sk + p) from (8 sk + p, c)
     });
     wsync();
-    for (int rk = 0; rk < G; ++rk) {
-      const int k = G * sk + rk;
-      if (k >= D) break;
+    // (pivots unrolled at compile time: k is a constant and the next
+    // pivot's LDS reads can go out under this one's multiply-adds; the
+    // padding pivots k >= D add exact zeros -- Li and A are zero there)
+    sfor<0, G>([&](auto rkc) {
+      constexpr int rk = decltype(rkc)::value;
+      constexpr int k = G * sk + rk;
       cf ak[NB], lc[NB];
       sfor<0, NB>([&](auto sc) {
         constexpr int s = decltype(sc)::value;
@@ -589,7 +592,7 @@ DANSE_DEV void congruence2d(Blk<NB>& A, LDS2<NB, G>& S, int li, int D) {
           pk_fma_cc(Z.v[s][t], ak[s], lc[t]);
         });
       });
-    }
+    });
   });
   // C = Li Z: C[i][c] = sum_k Li[i][k] Z[k][c], Li[i][k] = 0 for k > i  (into A);
   // block row sk of Z staged in S.cz the same way
@@ -605,9 +608,9 @@ DANSE_DEV void congruence2d(Blk<NB>& A, LDS2<NB, G>& S, int li, int D) {
       S.cz[p][q + G * t] = Z.v[sk][t];
     });
     wsync();
-    for (int rk = 0; rk < G; ++rk) {
-      const int k = G * sk + rk;
-      if (k >= D) break;
+    sfor<0, G>([&](auto rkc) {
+      constexpr int rk = decltype(rkc)::value;
+      constexpr int k = G * sk + rk;
       cf zk[NB], lr[NB];
       sfor<0, NB>([&](auto tc) {
         constexpr int t = decltype(tc)::value;
@@ -624,7 +627,7 @@ DANSE_DEV void congruence2d(Blk<NB>& A, LDS2<NB, G>& S, int li, int D) {
           pk_fma_c(A.v[s][t], lr[s], zk[t]);
         });
       });
-    }
+    });
   });
   sfor<0, NB>([&](auto sc) {
     constexpr int s = decltype(sc)::value;

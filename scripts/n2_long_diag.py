@@ -66,11 +66,20 @@ def main():
         print(f'{cfg}: median {np.median(flat):.3g} p99 {np.percentile(flat, 99):.3g} p99.9 '
               f'{np.percentile(flat, 99.9):.3g} max {flat.max():.3g}; >1e-4: {int((flat > 1e-4).sum())}, '
               f'>1e-3: {int((flat > 1e-3).sum())} of {flat.size}; lanczos sent back {int(lz[:, 1].sum())}')
+        # the same errors relative to the bin's median oracle filter norm over
+        # the window (a filter that passes near zero -- lambda_1 near 1 makes
+        # (1 - 1/lambda_1) cancel -- inflates the per-entry relative error)
+        Nrm = np.stack([np.linalg.norm(ov.wTilde[k][:, int(ov.startRound[k]) + 1:R0 + 1], axis=-1) for k in range(K)])
+        med = np.median(Nrm, axis=-1, keepdims=True)
+        En = E * Nrm / np.maximum(med, 1e-30)
+        fn = En.ravel()
+        print(f'{cfg} (normalised by the bin median norm): median {np.median(fn):.3g} p99 {np.percentile(fn, 99):.3g} '
+              f'max {fn.max():.3g}; >1e-3: {int((fn > 1e-3).sum())}')
         idx = np.argsort(flat)[::-1][:12]
         for i in idx:
             k, f, r = np.unravel_index(i, E.shape)
-            print(f'   k {k:2d} f {f:3d} post-gate round {r:2d}: {E[k, f, r]:.3g}  (same bin, rounds: '
-                  f'{" ".join(f"{x:.1e}" for x in E[k, f, max(0, r - 3):r + 4])})')
+            print(f'   k {k:2d} f {f:3d} post-gate round {r:2d}: {E[k, f, r]:.3g} norm/median {Nrm[k, f, r] / med[k, f, 0]:.3g} '
+                  f'(same bin, rounds: {" ".join(f"{x:.1e}" for x in E[k, f, max(0, r - 3):r + 4])})')
         sys.stdout.flush()
 
 
