@@ -268,26 +268,43 @@ def test_headline_shape_K32x8_D39_long_run_vs_oracle():
     assert np.array_equal(dv.startRound, ov.startRound)
     assert int(np.max(ov.startRound)) <= 90, ov.startRound
     assert int(np.sum(diag)) == 0
-    errs, last = [], []
+    errs, last, errn, small = [], [], [], []
     for k in range(K):
         s0 = int(ov.startRound[k])
-        e = _bin_rel(dv.wTilde[k][:, s0 + 1:R0 + 1], ov.wTilde[k][:, s0 + 1:R0 + 1])   # [F][rounds]
+        wo = ov.wTilde[k][:, s0 + 1:R0 + 1]
+        e = _bin_rel(dv.wTilde[k][:, s0 + 1:R0 + 1], wo)   # [F][rounds]
+        # the error against the bin's median filter norm over the window: at
+        # a frame where lambda_1 nears 1 the filter (1 - 1/lambda_1) x x^H Rnn
+        # e_ref nearly vanishes and its per-frame relative error is that of a
+        # near-zero vector (the float32 residue of the cancellation)
+        nrm = np.linalg.norm(wo, axis=-1)
+        rel = nrm / np.maximum(np.median(nrm, axis=-1, keepdims=True), 1e-30)
         errs.append(e.ravel())
+        errn.append((e * rel).ravel())
+        small.append(rel.ravel())
         last.append(e[:, -1])
     st = _stats(np.concatenate(errs))
+    stn = _stats(np.concatenate(errn))
     st_last = _stats(np.concatenate(last))
+    big = np.concatenate(errs) > 1e-3
     T1 = int(ov.idxEnd) - (dp.DFTsize - dp.Ns)
     de = rel_err(dv.d[:T1], ov.d[:T1])
     s0 = int(np.min(ov.startRound))
     acc, back = lz[s0:R0, 0], lz[s0:R0, 1]
-    print(case['name'], 'rounds', R0, 'post-gate', R0 - s0, 'w', st, 'last round', st_last, 'd', de)
+    print(case['name'], 'rounds', R0, 'post-gate', R0 - s0, 'w', st, 'normalised', stn, 'last round', st_last,
+          'd', de, 'entries > 1e-3:', int(big.sum()), 'their norm / median:', np.concatenate(small)[big].tolist())
     print('lanczos accepted per launch', acc.tolist())
     print('lanczos sent back per launch', back.tolist())
     # every post-gate round after the first solve: all K * F bins solve, and
     # the warm path must carry them (the first solve of a bin is cold)
     assert np.all(acc[2:] + back[2:] == K * 513), (acc, back)
     assert acc[2:].sum() >= 0.9 * (R0 - s0 - 2) * K * 513, (acc.sum(), back.sum())
-    assert st['median'] <= 1e-5 and st['p99'] <= 1e-4 and st['max'] <= 1e-3, st
+    assert st['median'] <= 1e-5 and st['p99'] <= 1e-4, st
+    # max: on the norm-normalised errors; the per-frame relative errors above
+    # 1e-3 must all be frames where the filter collapsed below 2 % of its
+    # median norm (measured on MI355X: 4 of 656,640, at 0.07 %-1.5 %)
+    assert stn['max'] <= 1e-3, stn
+    assert np.all(np.concatenate(small)[big] < 0.02)
     assert de <= 1e-4
 
 
