@@ -119,6 +119,9 @@ struct UpdateArgs {
 };
 
 constexpr int kStampN = 9;   // marks per wave; slot kStampN holds the path code
+#ifndef DANSE_STAMP
+#define DANSE_STAMP 0   // diagnostics build (danse_amd.build variant 'stamp'): per-wave phase clocks
+#endif
 
 DANSE_DEV bool node_in(unsigned mask, int k) { return ((mask >> k) & 1u) != 0u; }
 

@@ -16,9 +16,7 @@
 #ifndef DANSE_2D_WPE
 #define DANSE_2D_WPE 2
 #endif
-#ifndef DANSE_STAMP
-#define DANSE_STAMP 0   // diagnostics build (danse_amd.build variant 'stamp'): per-wave phase clocks
-#endif
+
 #include "solver2d.hpp"
 
 namespace danse {
@@ -283,9 +281,8 @@ update_kernel_2d(const UpdateArgs a) {
     });
     stamp(4);
     if (solve) {
-      congruence2d<NB, G>(A, S, li, D);
       stamp(5);
-      const int path = gevd2d_solve<NB, RMAX, G>(A, S, li, D, a.rank, w, vC, fvalid);
+      const int path = gevd2d_filter<NB, RMAX, G>(A, S, li, D, a.rank, w, vC, fvalid);
       if (path && a.lzStats && li == 0 && fvalid) atomicAdd(&a.lzStats[2 * r + path - 1], 1);
       tcode |= path << 5;
     } else {

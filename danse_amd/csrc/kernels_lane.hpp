@@ -48,6 +48,12 @@ template <int D, int RMAX, bool GEVD, bool RO = false>
 __global__ void __launch_bounds__(64) update_kernel_lane(const UpdateArgs a) {
   using namespace lane;
   constexpr int NT = tri_n(D);
+  // DANSE_STAMP builds (kernels_2d.hpp): per-wave phase clocks
+  unsigned long long tsv[kStampN];
+  auto stamp = [&](int i) {
+    if constexpr (DANSE_STAMP) tsv[i] = __builtin_amdgcn_s_memtime();
+  };
+  stamp(0);
   const LaneIdx ix = lane_index(a);
   const int F = a.F, f = ix.f, s = ix.s, r = a.r;
   const FamNode d = a.fn[ix.fni];
@@ -68,6 +74,7 @@ __global__ void __launch_bounds__(64) update_kernel_lane(const UpdateArgs a) {
   if (opY || opN) {
     load_y_all<D>(a, d, s, f, y);
   }
+  stamp(1);
   const double beta = a.beta[s * a.K + d.k];
   const long long base = (long long)s * a.scmStride + d.scmOff + f;
   // Ryy (float32) of this frame into A: load, the recursion when the VAD
@@ -161,6 +168,7 @@ __global__ void __launch_bounds__(64) update_kernel_lane(const UpdateArgs a) {
       sfor<0, NT>([&](auto ec) { a.Rnn[base + (long long)decltype(ec)::value * F] = N.a[decltype(ec)::value]; });
     }
   }
+  stamp(2);
   bool ok = true;
   if (solve) {
   if constexpr (GEVD) {
@@ -209,6 +217,7 @@ __global__ void __launch_bounds__(64) update_kernel_lane(const UpdateArgs a) {
   }
   if (!ok && valid) atomicOr(&a.diag[(s * a.K + d.k) * kMaxFam + d.fam], 1);
   }
+  stamp(3);
   if (!RO && !solve && opY) {   // (a solve updates Ryy where it uses it)
     PTri<D> A;
     ryy_update(A);
@@ -232,8 +241,11 @@ __global__ void __launch_bounds__(64) update_kernel_lane(const UpdateArgs a) {
       sfor<0, D>([&](auto ic) { g[decltype(ic)::value] = Gs[decltype(ic)::value][threadIdx.x]; });
       PTri<D> A;
       ryy_update(A);
+      stamp(4);
       congruence<D>(A, Li);
+      stamp(5);
       gevd_filter_mixed<D, RMAX>(A, Li, g, a.rank, w);
+      stamp(6);
     }
     if (valid) sfor<0, D>([&](auto ic) { wNext[decltype(ic)::value] = w[decltype(ic)::value]; });
   } else if (fl & DANSE_FLAG_INITSLOT) {
@@ -289,6 +301,20 @@ __global__ void __launch_bounds__(64) update_kernel_lane(const UpdateArgs a) {
   }
   if (f == 0 || f == F - 1) dh.im = 0.0f;
   if (valid) a.dhat[((((long long)d.fam * a.S + s) * a.K + d.k) * a.R + r) * F + f] = dh;
+  if constexpr (DANSE_STAMP) {
+    stamp(7);
+    __builtin_amdgcn_s_waitcnt(0);
+    stamp(8);
+    // path code over the wave's lanes: 1 any noise frame, 8 any cached
+    // factor, 16 any solve, 4 any factorisation
+    const unsigned long long code = (__ballot(opN != 0) ? 1ull : 0ull) | (__ballot(reuse) ? 8ull : 0ull) |
+                                    (__ballot(solve) ? 16ull : 0ull) | (__ballot(solve && !reuse) ? 4ull : 0ull);
+    if (a.stamps && threadIdx.x <= kStampN) {
+      unsigned long long v = code;
+      sfor<0, kStampN>([&](auto ic) { v = (threadIdx.x == decltype(ic)::value) ? tsv[decltype(ic)::value] : v; });
+      a.stamps[(long long)blockIdx.x * (kStampN + 1) + threadIdx.x] = v;
+    }
+  }
 }
 
 

@@ -28,6 +28,10 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 
 PHASES = ['y', 'Rnn', 'factor', 'Ryy', 'congr', 'solve', 'tail', 'drain']
+# update_kernel_lane (D <= 12): 1 observation loaded, 2 Rnn recursion (noise
+# frames), 3 factor (float64 Cholesky + inverse, or the cached factor into
+# LDS), 4 Ryy recursion, 5 congruence, 6 eigen part + filter, 7 / 8 as above
+PHASES_LANE = ['y', 'Rnn', 'factor', 'Ryy', 'congr', 'eigen', 'tail', 'drain']
 
 
 def main():
@@ -58,7 +62,8 @@ def main():
     eng.lib.danse_engine_resident_trace(eng.eng, buf.ctypes.data_as(ctypes.c_void_p), ctypes.byref(n))
     eng.close()
     t = buf.reshape(-1, 10)
-    t = t[t[:, 0] != 0]
+    t = t[(t[:, 0] != 0) & np.all(t[:, :9] != 0, axis=1)]
+    phases = PHASES_LANE if max(wl['M']) + len(wl['M']) - 1 <= 12 else PHASES
     marks, code = t[:, :9].astype(np.int64), t[:, 9]
     dt = np.diff(marks, axis=1)
     life = marks[:, 8] - marks[:, 0]
@@ -69,11 +74,11 @@ def main():
         sel = code == c
         bits = [nm for b, nm in ((1, 'noise'), (2, 'rank1'), (4, 'fullfactor'), (8, 'reuse'), (16, 'solve'),
                                  (32, 'lz-ok'), (64, 'lz-back')) if c & b]
-        row = ' '.join(f'{nm} {np.mean(dt[sel, i]):7.0f}' for i, nm in enumerate(PHASES))
+        row = ' '.join(f'{nm} {np.mean(dt[sel, i]):7.0f}' for i, nm in enumerate(phases))
         print(f'code {c:3d} ({"+".join(bits) or "-"}): {sel.sum():6d} waves, life {np.mean(life[sel]):7.0f}: {row}')
     # concurrency: waves alive over the launch
     print('mean phase share of wave life:',
-          ' '.join(f'{nm} {np.sum(dt[:, i]) / np.sum(life):.3f}' for i, nm in enumerate(PHASES)))
+          ' '.join(f'{nm} {np.sum(dt[:, i]) / np.sum(life):.3f}' for i, nm in enumerate(phases)))
 
 
 if __name__ == '__main__':
