@@ -392,7 +392,7 @@ int danse_engine_reset(danse_engine* eng, void* stream) {
   HIPCHK(fill_async(eng->d, 0, (size_t)kMaxFam * S * K * eng->T * sizeof(float), st));
   HIPCHK(fill_async(eng->diag, 0, (size_t)S * K * kMaxFam * sizeof(int), st));
   if (eng->vCache) HIPCHK(fill_async(eng->vCache, 0, (size_t)S * eng->vStride * sizeof(cf), st));
-  if (eng->lzStats) HIPCHK(fill_async(eng->lzStats, 0, (size_t)2 * eng->R * sizeof(int), st));
+  if (eng->lzStats) HIPCHK(fill_async(eng->lzStats, 0, (size_t)2 * eng->R * kLzSlots * sizeof(int), st));
   const int nFN = (int)eng->fns.size();
   hipLaunchKernelGGL(reset_fam_kernel, dim3(64, S * nFN), dim3(256), 0, st, eng->dFnAll, nFN, eng->dInitW0Off,
                      eng->dInitScmOff, eng->dW0, eng->dScm0, eng->wHist, eng->wStride, eng->Ryy, eng->Rnn,
@@ -766,7 +766,7 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
   HIPCHK(dalloc(&eng->diag, (size_t)S * K * kMaxFam));
   if (eng->liStride > 0) HIPCHK(dalloc(&eng->liCache, (size_t)S * eng->liStride));
   if (eng->vStride > 0) HIPCHK(dalloc(&eng->vCache, (size_t)S * eng->vStride));
-  if (eng->vStride > 0) HIPCHK(dalloc(&eng->lzStats, (size_t)2 * R));
+  if (eng->vStride > 0) HIPCHK(dalloc(&eng->lzStats, (size_t)2 * R * kLzSlots));
   if (const char* tr = std::getenv("DANSE_UPDATE_TRACE")) {
     // (upper bound: one wave per (scene, family-node, bin))
     eng->updTraceRound = std::atoi(tr);
@@ -1463,7 +1463,13 @@ int danse_engine_lanczos_stats(danse_engine* eng, int32_t* dst, size_t n) {
     std::fill(dst, dst + 2 * (size_t)eng->R, 0);
     return 0;
   }
-  HIPCHK(hipMemcpy(dst, eng->lzStats, (size_t)2 * eng->R * sizeof(int), hipMemcpyDeviceToHost));
+  std::vector<int> h((size_t)2 * eng->R * kLzSlots);
+  HIPCHK(hipMemcpy(h.data(), eng->lzStats, h.size() * sizeof(int), hipMemcpyDeviceToHost));
+  for (size_t i = 0; i < (size_t)2 * eng->R; ++i) {
+    int acc = 0;
+    for (int j = 0; j < kLzSlots; ++j) acc += h[i * kLzSlots + j];
+    dst[i] = acc;
+  }
   return 0;
 }
 

@@ -110,14 +110,16 @@ struct UpdateArgs {
   // after it updates it by rank one instead of refactoring; null = off
   cd* l64Cache;
   long long l64Stride;
-  // [R][2] or null: per round the bins whose warm Lanczos solve was accepted
-  // and those sent back to the Householder path (diagnostics)
+  // [R][2][kLzSlots] or null: per round the bins whose warm Lanczos solve was
+  // accepted and those sent back to the Householder path (diagnostics; the
+  // host sums the slots)
   int* lzStats;
   // DANSE_STAMP builds only (diagnostics): per launch wave, kStampN shader
   // clock marks + a path code (update_kernel_2d), or null
   unsigned long long* stamps;
 };
 
+constexpr int kLzSlots = 64;
 constexpr int kStampN = 9;   // marks per wave; slot kStampN holds the path code
 #ifndef DANSE_STAMP
 #define DANSE_STAMP 0   // diagnostics build (danse_amd.build variant 'stamp'): per-wave phase clocks

@@ -95,6 +95,9 @@ update_kernel_2d(const UpdateArgs a) {
   // the factor record (S.Ls + g) and the Ryy block, so that the record, the
   // block and the spectra are one memory round trip instead of three.
   constexpr int kRec = t2d::li_record<NB, G>(), kRecL = (kRec + L - 1) / L, kNL = G * NB * (G * NB + 1) / 2;
+  // (G = 4 keeps the separate loads: its 16-entry record chunk next to the
+  // Ryy block spilled)
+  constexpr bool kPre = (SM != 1) && G == 8;
   const long long triOff0 = PK ? (long long)s * a.scmStride + d.scmOff + f
                                : (long long)s * a.scmStride + d.scmOff + (long long)f * (D * (D + 1) / 2);
   auto entA = [&](int i, int c) -> long long {
@@ -110,7 +113,7 @@ update_kernel_2d(const UpdateArgs a) {
     const int i = li + L * v;
     ych[v] = chan_of(a, d, i, i < D);
   });
-  if constexpr (SM != 1) {
+  if constexpr (kPre) {
     if (reuse) {
       sfor<0, kRecL>([&](auto jc) {
         constexpr int j = decltype(jc)::value;
@@ -134,7 +137,7 @@ update_kernel_2d(const UpdateArgs a) {
     const int i = li + L * v;
     y[v] = load_y_c(a, d, s, f, ych[v], i < D);
   });
-  if constexpr (SM != 1) {
+  if constexpr (kPre) {
     if (reuse) {
       hold(lrec);
       sfor<0, NB>([&](auto sc) { hold(A.v[decltype(sc)::value]); });
@@ -235,6 +238,7 @@ update_kernel_2d(const UpdateArgs a) {
   } else {
     stamp(2);
   }
+  if (!kPre && reuse) li_load2d<NB, G>(S, liC, li);
   tcode |= (opN ? 1 : 0) | (reuse ? 8 : 0) | (solve ? 16 : 0);
   stamp(3);
 
@@ -253,7 +257,7 @@ update_kernel_2d(const UpdateArgs a) {
       });
     };
     if constexpr (SM != 1) {
-      if (!reuse) {   // (reuse: loaded with the observation above)
+      if (!kPre || !reuse) {   // (kPre and reuse: loaded with the observation above)
         sfor<0, NB>(ld_row_Ryy);
         sfor<0, NB>([&](auto sc) { hold(A.v[decltype(sc)::value]); });
       }
@@ -281,9 +285,16 @@ update_kernel_2d(const UpdateArgs a) {
     });
     stamp(4);
     if (solve) {
+      congruence2d<NB, G>(A, S, li, D);
       stamp(5);
-      const int path = gevd2d_filter<NB, RMAX, G>(A, S, li, D, a.rank, w, vC, fvalid);
-      if (path && a.lzStats && li == 0 && fvalid) atomicAdd(&a.lzStats[2 * r + path - 1], 1);
+      const int path = gevd2d_solve<NB, RMAX, G>(A, S, li, D, a.rank, w, vC, fvalid);
+      // (one atomic per wave -- the path is wave-uniform -- into one of
+      // kLzSlots counters per round and path: a single counter took every
+      // wave's add and stalled config C's launches 2x)
+      if (path && a.lzStats && threadIdx.x == 0) {
+        const int nb = (W == 1) ? 1 : min(W, F - fg * W);
+        atomicAdd(&a.lzStats[((long long)(2 * r + path - 1)) * kLzSlots + (blockIdx.x & (kLzSlots - 1))], nb);
+      }
       tcode |= path << 5;
     } else {
       stamp(5);

@@ -1054,116 +1054,80 @@ constexpr float kLzTol = 3.0e-6f;
 constexpr float kLzBreak = 1.0e-6f;   // first-step breakdown test (relative to theta)
 
 // true (wave-uniform) if every bin of the wave converged: then vv (lane
-// layout) is the unit eigenvector of C = Li A Li^H and lam1 its eigenvalue.
-// C is never formed: every Lanczos step applies it as three matvecs with
-// the factor (S.Ls, this lane's blocks held in registers) and the Ryy block
-// A -- t = Li^H v (a sum over the row groups), u = A t (over the lanes of a
-// row group), u to the column layout through LDS, w = Li u -- 3 D^2 complex
-// multiply-adds per step instead of the D^3 of the congruence the
-// Householder path needs.  The Lanczos vectors live in
-// the row layout (entries p + G s); the basis in the reflector space S.U.
+// layout) is the unit eigenvector of C and lam1 its eigenvalue
 template <int NB, int G = 8>
 DANSE_DEV bool lanczos2d(const Blk<NB>& A, LDS2<NB, G>& S, int li, int D, const cf* vIn, cf (&vv)[vpl<NB, G>()],
                          float& lam1, bool& warm) {
   constexpr int DM = G * NB, L = bin_lanes<G>(), V = vpl<NB, G>(), M = kLz<DM>();
   static_assert(M * DM <= DM * (DM - 1) / 2, "the Lanczos basis lives in the reflector space");
-  // (the lane index laundered: otherwise this path's LDS address arithmetic
-  // is merged with the earlier phases' and held live across them -- the
-  // rank-one factor path then spilled)
-  asm volatile("" : "+v"(li));
   const int p = li / G, q = li % G;
-  cf* Q = S.U;   // [M][DM] basis vectors (row layout, stored by the q == 0 lanes)
-  wsync();
-  // this lane's blocks of Li (rows p + G s, columns q + G t, s >= t; zero
-  // above the diagonal inside the diagonal blocks), read from LDS where a
-  // matvec needs them (held in registers they spilled the kernel)
-  auto lb = [&](int sb, int t) { return ls_get<DM>(S.Ls, p + G * sb, q + G * t); };
-  // start vector, row layout, unit norm
-  cf vr[NB];
+  cf* Q = S.U;   // [M][DM] basis vectors (the Householder vectors' space: unused on this path)
+  wsync();       // the congruence's staging reads (S.cz aliases S.qb / S.a) before the writes below
+  // start vector, column layout (entries q + G t), unit norm
+  cf vc[NB];
   float n0 = 0.0f;
-  sfor<0, NB>([&](auto sc) {
-    constexpr int sb = decltype(sc)::value;
-    const int i = p + G * sb;
-    vr[sb] = (i < D) ? vIn[i] : cf{0.0f, 0.0f};
-    n0 += abs2(vr[sb]);
+  sfor<0, NB>([&](auto tc) {
+    constexpr int t = decltype(tc)::value;
+    const int i = q + G * t;
+    vc[t] = (i < D) ? vIn[i] : cf{0.0f, 0.0f};
+    n0 += abs2(vc[t]);
   });
-  n0 = sump<G>(n0);
+  n0 = sumq<G>(n0);
   bool ok = n0 > 1e-30f && n0 < 1e30f;
   warm = __ballot(n0 > 1e-30f) != 0ull;   // (a bin's first solve has no start vector: a cold solve)
   const float s0 = ok ? frsq(n0) : 0.0f;
-  sfor<0, NB>([&](auto sc) { vr[decltype(sc)::value] = s0 * vr[decltype(sc)::value]; });
-  if (q == 0) sfor<0, NB>([&](auto sc) { Q[p + G * decltype(sc)::value] = vr[decltype(sc)::value]; });
+  sfor<0, NB>([&](auto tc) { vc[decltype(tc)::value] = s0 * vc[decltype(tc)::value]; });
+  if (p == 0) sfor<0, NB>([&](auto tc) { Q[q + G * decltype(tc)::value] = vc[decltype(tc)::value]; });
   float blast = 0.0f, b0 = 0.0f;
+  // largest diagonal entry of C: a lower bound of lambda_1 (the Rayleigh
+  // quotient of a unit vector), checked against the Ritz value below
+  float dmax1 = -3.0e38f;
+  sfor<0, NB>([&](auto sc) {
+    constexpr int sb = decltype(sc)::value;
+    if (p == q && p + G * sb < D) dmax1 = fmaxf(dmax1, A.v[sb][sb].re);
+  });
+  const float dmax = gmax<L>(dmax1);
   // k = 0 .. M - 1, unrolled (the orthogonalisation's loops get static bounds)
   sfor<0, M>([&](auto kc) {
     constexpr int k = decltype(kc)::value;
-    asm volatile("" ::: "memory");   // (one step's LDS reads at a time)
-    // t = Li^H v: t_c = sum_i conj(Li[i][c]) v_i, column layout
-    cf tcv[NB];
-    sfor<0, NB>([&](auto tc) {
-      constexpr int t = decltype(tc)::value;
-      cf acc = cf{0.0f, 0.0f};
-      sfor<t, NB>([&](auto sc) {
-        constexpr int sb = decltype(sc)::value;
-        cmac<true, false, false>(acc, lb(sb, t), vr[sb]);
-      });
-      tcv[t] = acc;
-    });
-    sfor<0, NB>([&](auto tc) { tcv[decltype(tc)::value] = sump<G>(tcv[decltype(tc)::value]); });
-    // u = A t, row layout; then to the column layout through LDS
-    cf ur[NB];
+    // w = C v: row-layout partial sums over the row group, then the column
+    // layout through LDS
     sfor<0, NB>([&](auto sc) {
       constexpr int sb = decltype(sc)::value;
       cf acc = cf{0.0f, 0.0f};
-      sfor<0, NB>([&](auto tc) { pk_fma_c(acc, A.v[sb][decltype(tc)::value], tcv[decltype(tc)::value]); });
-      ur[sb] = acc;
+      sfor<0, NB>([&](auto tc) { pk_fma_c(acc, A.v[sb][decltype(tc)::value], vc[decltype(tc)::value]); });
+      acc = sumq<G>(acc);
+      if (q == 0) S.qb[k & 1][p + G * sb] = acc;
     });
-    sfor<0, NB>([&](auto sc) { ur[decltype(sc)::value] = sumq<G>(ur[decltype(sc)::value]); });
-    if (q == 0) sfor<0, NB>([&](auto sc) { S.qb[k & 1][p + G * decltype(sc)::value] = ur[decltype(sc)::value]; });
     wsync();
-    cf uc[NB];
-    sfor<0, NB>([&](auto tc) { uc[decltype(tc)::value] = S.qb[k & 1][q + G * decltype(tc)::value]; });
-    // w = Li u, row layout
-    cf wr[NB];
-    sfor<0, NB>([&](auto sc) {
-      constexpr int sb = decltype(sc)::value;
-      cf acc = cf{0.0f, 0.0f};
-      sfor<0, sb + 1>([&](auto tc) { pk_fma_c(acc, lb(sb, decltype(tc)::value), uc[decltype(tc)::value]); });
-      wr[sb] = acc;
-    });
-    sfor<0, NB>([&](auto sc) { wr[decltype(sc)::value] = sumq<G>(wr[decltype(sc)::value]); });
+    cf wc[NB];
+    sfor<0, NB>([&](auto tc) { wc[decltype(tc)::value] = S.qb[k & 1][q + G * decltype(tc)::value]; });
     // one classical Gram-Schmidt pass against the basis Q_0 .. Q_k: the
     // coefficients are independent (one reduction each, side by side);
     // h_k is the Lanczos alpha_k, h_(k-1) its beta_(k-1)
     cf h[k + 1];
     sfor<0, k + 1>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
-      // (the basis read two vectors at a time: all k NB reads issued at once
-      // spilled the kernel)
-      if constexpr (j % 2 == 0 && j > 0) asm volatile("" ::: "memory");
       cf acc = cf{0.0f, 0.0f};
-      sfor<0, NB>([&](auto sc) {
-        constexpr int sb = decltype(sc)::value;
-        const cf qj = (j == k) ? vr[sb] : Q[j * DM + p + G * sb];
-        acc = acc + cmul(qj, wr[sb]);
+      sfor<0, NB>([&](auto tc) {
+        constexpr int t = decltype(tc)::value;
+        const cf qj = (j == k) ? vc[t] : Q[j * DM + q + G * t];
+        acc = acc + cmul(qj, wc[t]);
       });
       h[j] = acc;
     });
-    sfor<0, k + 1>([&](auto jc) { h[decltype(jc)::value] = sump<G>(h[decltype(jc)::value]); });
-    // (the basis re-read from LDS for the update, two vectors at a time)
-    asm volatile("" ::: "memory");
+    sfor<0, k + 1>([&](auto jc) { h[decltype(jc)::value] = sumq<G>(h[decltype(jc)::value]); });
     sfor<0, k + 1>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
-      if constexpr (j % 2 == 0 && j > 0) asm volatile("" ::: "memory");
-      sfor<0, NB>([&](auto sc) {
-        constexpr int sb = decltype(sc)::value;
-        const cf qj = (j == k) ? vr[sb] : Q[j * DM + p + G * sb];
-        fms_c(wr[sb], h[j], qj);
+      sfor<0, NB>([&](auto tc) {
+        constexpr int t = decltype(tc)::value;
+        const cf qj = (j == k) ? vc[t] : Q[j * DM + q + G * t];
+        fms_c(wc[t], h[j], qj);
       });
     });
     float nb = 0.0f;
-    sfor<0, NB>([&](auto sc) { nb += abs2(wr[decltype(sc)::value]); });
-    nb = sump<G>(nb);
+    sfor<0, NB>([&](auto tc) { nb += abs2(wc[decltype(tc)::value]); });
+    nb = sumq<G>(nb);
     const float b = fsqrt(nb);
     if (li == 0) {
       S.a[k] = h[k].re;
@@ -1174,10 +1138,10 @@ DANSE_DEV bool lanczos2d(const Blk<NB>& A, LDS2<NB, G>& S, int li, int D, const 
     }
     // (a breakdown -- an invariant subspace, b ~ 0 -- leaves the remaining
     // basis vectors zero: the small tridiagonal splits and its top Ritz pair
-    // is exact for that subspace)
+    // is exact)
     const float ib = (b > 1e-20f) ? frcp(b) : 0.0f;
-    sfor<0, NB>([&](auto sc) { vr[decltype(sc)::value] = ib * wr[decltype(sc)::value]; });
-    if (k + 1 < M && q == 0) sfor<0, NB>([&](auto sc) { Q[(k + 1) * DM + p + G * decltype(sc)::value] = vr[decltype(sc)::value]; });
+    sfor<0, NB>([&](auto tc) { vc[decltype(tc)::value] = ib * wc[decltype(tc)::value]; });
+    if (k + 1 < M && p == 0) sfor<0, NB>([&](auto tc) { Q[(k + 1) * DM + q + G * decltype(tc)::value] = vc[decltype(tc)::value]; });
     blast = b;
     if constexpr (k == 0) b0 = b;
     wsync();
@@ -1191,31 +1155,32 @@ DANSE_DEV bool lanczos2d(const Blk<NB>& A, LDS2<NB, G>& S, int li, int D, const 
   if (li < M) S.x[0][li] = x[0];
   wsync();
   const float sm = S.x[0][M - 1];
-  // Ritz vector y = sum_k s_k Q_k (row layout), unit norm
-  cf yr[NB];
-  sfor<0, NB>([&](auto sc) { yr[decltype(sc)::value] = cf{0.0f, 0.0f}; });
+  // Ritz vector y = sum_k s_k Q_k (column layout), unit norm
+  cf yc[NB];
+  sfor<0, NB>([&](auto tc) { yc[decltype(tc)::value] = cf{0.0f, 0.0f}; });
   for (int k = 0; k < M; ++k) {
     const float sk = S.x[0][k];
-    sfor<0, NB>([&](auto sc) {
-      constexpr int sb = decltype(sc)::value;
-      yr[sb] = yr[sb] + sk * Q[k * DM + p + G * sb];
+    sfor<0, NB>([&](auto tc) {
+      constexpr int t = decltype(tc)::value;
+      yc[t] = yc[t] + sk * Q[k * DM + q + G * t];
     });
   }
   float ny = 0.0f;
-  sfor<0, NB>([&](auto sc) { ny += abs2(yr[decltype(sc)::value]); });
-  ny = sump<G>(ny);
+  sfor<0, NB>([&](auto tc) { ny += abs2(yc[decltype(tc)::value]); });
+  ny = sumq<G>(ny);
   const float theta = lam[0];
   const float res = blast * fabsf(sm);
-  // Accept on the Lanczos residual, unless the first step already broke
-  // down: then the start vector spans an invariant subspace on its own, and
-  // its eigenpair, exact, need not be the top one (an eigenvalue crossing
-  // since the start vector was the top eigenvector) -- the bin goes back to
-  // the Householder path.
+  // Accept on the Lanczos residual, and only when nothing says the Ritz pair
+  // may be a lower eigenpair (an eigenvalue crossing since the start vector
+  // was the top one): a first step that already breaks down (the start
+  // vector spans an invariant subspace on its own: exact, but not
+  // necessarily the top pair) and a Ritz value below a diagonal entry of C
+  // (a Rayleigh quotient: lambda_1 is at least that) send the bin back.
   ok = ok && ny > 0.5f && theta > 0.0f && theta < 3.0e38f && res <= kLzTol * theta;
-  ok = ok && b0 > kLzBreak * theta;
+  ok = ok && b0 > kLzBreak * theta && theta >= dmax * (1.0f - 4.0e-6f);
   const float sy = frsq(fmaxf(ny, 1e-30f));
   // lane layout through LDS
-  if (q == 0) sfor<0, NB>([&](auto sc) { S.vb[p + G * decltype(sc)::value] = sy * yr[decltype(sc)::value]; });
+  if (p == 0) sfor<0, NB>([&](auto tc) { S.vb[q + G * decltype(tc)::value] = sy * yc[decltype(tc)::value]; });
   wsync();
   sfor<0, V>([&](auto vc2) {
     constexpr int v = decltype(vc2)::value;
@@ -1287,8 +1252,18 @@ DANSE_DEV void rank1_w2d(LDS2<NB, G>& S, int li, int D, const cf (&vv)[vpl<NB, G
 // tried, or none to try from), 1 the warm Lanczos solve accepted, 2 the warm
 // solve tried and sent back to the Householder path.
 template <int NB, int RMAX, int G = 8>
+DANSE_DEV int gevd2d_solve(Blk<NB>& A, LDS2<NB, G>& S, int li, int D, int R, cf (&w)[vpl<NB, G>()],
+                           cf* vCache = nullptr, bool store = false);
+template <int NB, int RMAX, int G = 8>
 DANSE_DEV int gevd2d_filter(Blk<NB>& A, LDS2<NB, G>& S, int li, int D, int R, cf (&w)[vpl<NB, G>()],
                             cf* vCache = nullptr, bool store = false) {
+  congruence2d<NB, G>(A, S, li, D);
+  return gevd2d_solve<NB, RMAX, G>(A, S, li, D, R, w, vCache, store);
+}
+// the part after the congruence (C in A)
+template <int NB, int RMAX, int G>
+DANSE_DEV int gevd2d_solve(Blk<NB>& A, LDS2<NB, G>& S, int li, int D, int R, cf (&w)[vpl<NB, G>()], cf* vCache,
+                           bool store) {
   constexpr int V = vpl<NB, G>(), L = bin_lanes<G>(), DM = G * NB;
   int path = 0;
   // (classes below 20: too few Lanczos steps fit, and the D-step Householder
@@ -1309,8 +1284,6 @@ DANSE_DEV int gevd2d_filter(Blk<NB>& A, LDS2<NB, G>& S, int li, int D, int R, cf
     }
     path = warm ? 2 : 0;
   }
-  // the Householder path on the explicit C
-  congruence2d<NB, G>(A, S, li, D);
   tridiag2d<NB, G>(A, S, li, D);
   eigen2d<NB, RMAX, G>(S, li, D, R, w, R == 1 ? vCache : nullptr, store);
   return path;
