@@ -20,6 +20,7 @@
 #include "resident.hpp"
 #include "resident_api.hpp"
 #include "cond.hpp"
+#include "wide_online.hpp"
 
 using namespace danse;
 
@@ -107,6 +108,12 @@ struct danse_engine {
   cd* l64Cache = nullptr;    // lane-grid GEVD classes: float64 factor record per bin (rank-one updates)
   long long l64Stride = 0;
   int* lzStats = nullptr;    // [R][2] warm Lanczos solves accepted / sent back (danse_engine_lanczos_stats)
+  // the online centralised family above 64 channels (wide_online.hpp)
+  std::vector<int> wideIds;          // family-node indices
+  std::vector<uint8_t> wideSolve;    // [R][wideIds]: some scene solves
+  int* dWideIds = nullptr;
+  cd* wideWork = nullptr;
+  long long wideChunk = 0;
   int scmPerBin = 0;   // dScm0 holds [F][D][D] per family-node (else [D][D])
   FamNode* dFnAll = nullptr;
   long long *dInitW0Off = nullptr, *dInitScmOff = nullptr, *dExtSrcOff = nullptr, *dTgtOff = nullptr;
@@ -412,6 +419,21 @@ const char* danse_last_error(const danse_engine* eng) {
 }
 
 // The split classes' per-round lists of solving (scene, family-node) items.
+// per round and wide family-node: does some scene solve (the wide filter
+// launch is skipped otherwise)
+static void build_wide_lists(danse_engine* eng, const uint8_t* flags) {
+  const int nW = (int)eng->wideIds.size(), R = eng->R, S = eng->S, K = eng->K;
+  eng->wideSolve.assign((size_t)R * nW, 0);
+  for (int r = 0; r < R; ++r)
+    for (int w = 0; w < nW; ++w) {
+      const FamNode& fn = eng->fns[eng->wideIds[w]];
+      for (int s = 0; s < S; ++s) {
+        const uint8_t fl = flags[(((size_t)r * S + s) * kMaxFam + fn.fam) * K + fn.k];
+        if ((fl & DANSE_FLAG_SOLVE) && !(fl & DANSE_FLAG_PREGIVEN)) eng->wideSolve[(size_t)r * nW + w] = 1;
+      }
+    }
+}
+
 static int build_split_lists(danse_engine* eng, const uint8_t* flags) {
   const int S = eng->S, K = eng->K, R = eng->R;
   for (auto& cl : eng->classes) {
@@ -569,7 +591,15 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
         fn.D = mt;
         fn.ref = eng->base[k] + c->ref;
       }
-      if (fn.D > kMaxDMax) return fail(eng, "filter dimension > 64 not supported");
+      if (fn.D > kMaxDMax) {
+        // (only the centralised family reaches past 64 channels: the wide
+        // classes of wide_online.hpp, synchronous wholeChunk runs, the gate's
+        // matrix in LDS up to kGateMaxD)
+        if (fam != DANSE_FAM_CENTR || fn.D > kGateMaxD)
+          return fail(eng, "filter dimension > 64 outside the centralised family, or a centralised family above 96 channels");
+        if (c->cEnd || c->fsTab || c->cPhase)
+          return fail(eng, "centralised family above 64 channels: synchronous wholeChunk runs only");
+      }
       if (c->gevd && c->rank > fn.D) return fail(eng, "GEVD rank larger than a filter dimension");
       fn.scmOff = scmOff;
       // smallDGrid: GEVD of D <= 12 on the 4 x 4 grid class 16; the grid and
@@ -580,8 +610,11 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
       fn.wOff = wOff;
       wOff += histW * F * fn.D;
       fn.liOff = liOff;
+      const bool wideFn = fn.D > kMaxDMax;
       // (a split class's grid solves keep their own per-bin record in the region)
-      if (c->gevd && fn.packed == 1)
+      if (wideFn) {
+        // (no factor caches: the wide solve factors every time)
+      } else if (c->gevd && fn.packed == 1)
         liOff += (long long)F * std::max<long long>(fn.D * (fn.D + 1) / 2 + fn.D,
                                                     class_split(class_dmax(fn.D)) ? class_split_li_record() : 0);
       else if (c->gevd && gridSmall) liOff += (long long)F * class_li_record(16);
@@ -591,14 +624,14 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
       // float64 factor records (li_rank1_2d) of the one-bin-per-wave grid
       // classes (DMAX 24-48; at G = 4, DMAX <= 20, the O(D^3) factor is short
       // and the update measured slower: C 360 -> 372 us, N2 263 -> 255 us)
-      if (c->gevd && fn.packed == 2 && !gridSmall && class_grid(class_dmax(fn.D)) > 0 &&
+      if (!wideFn && c->gevd && fn.packed == 2 && !gridSmall && class_grid(class_dmax(fn.D)) > 0 &&
           class_dmax(fn.D) >= 24 && !std::getenv("DANSE_NO_R1")) {
         const int DMr = class_dmax(fn.D);
         fn.l64Off = l64Off;
         l64Off += (long long)F * (DMr * (DMr + 1) / 2 + DMr);
       }
       // (grid classes of 20 and more: solver2d.hpp gevd2d_filter)
-      if (warm && fn.packed == 2 && !gridSmall && class_grid(class_dmax(fn.D)) > 0 && class_dmax(fn.D) >= 20) {
+      if (!wideFn && warm && fn.packed == 2 && !gridSmall && class_grid(class_dmax(fn.D)) > 0 && class_dmax(fn.D) >= 20) {
         fn.vOff = vOff;
         vOff += (long long)F * class_dmax(fn.D);
       }
@@ -624,6 +657,10 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
     if (fn.fam == DANSE_FAM_DANSE) { fn.wExtOff = eng->wExtNodeOff[fn.k]; fn.tgtOff = tgtOff[fn.k]; }
   }
   for (size_t i = 0; i < eng->fns.size(); ++i) {
+    if (eng->fns[i].D > kMaxDMax) {
+      eng->wideIds.push_back((int)i);
+      continue;
+    }
     int G, DM;
     pick_class(eng->fns[i].D, G, DM);
     if (eng->fns[i].packed == 2 && DM <= kLaneMaxD) {   // smallDGrid (above)
@@ -711,6 +748,23 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
     const bool on = c->gevd && (sp && std::atoi(sp) != 0);
     for (auto& cl : eng->classes) cl.split = on && class_split(cl.DMAX) && (cl.G == 1 || cl.DMAX > kLaneMaxD);
     if (int rc = build_split_lists(eng, c->flags)) return rc;
+  }
+  if (!eng->wideIds.empty()) {
+    int dw = 0;
+    for (int id : eng->wideIds) dw = std::max(dw, eng->fns[id].D);
+    eng->wideChunk = wide::chunk_for(dw, (long long)S * F);
+    HIPCHK(dalloc(&eng->wideWork, (size_t)eng->wideChunk * wide::work_elems(dw)));
+    HIPCHK(dalloc(&eng->dWideIds, eng->wideIds.size()));
+    HIPCHK(hipMemcpy(eng->dWideIds, eng->wideIds.data(), eng->wideIds.size() * sizeof(int), hipMemcpyHostToDevice));
+    build_wide_lists(eng, c->flags);
+  }
+  {
+    // the gate's [D][D + 1] complex-double matrix in dynamic LDS above 64 KiB
+    int dmax = 0;
+    for (const auto& x : eng->fns) dmax = std::max(dmax, x.D);
+    const size_t lds = (size_t)dmax * (dmax + 1) * sizeof(cd);
+    if (lds > 65536)
+      HIPCHK(hipFuncSetAttribute((const void*)gate_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   }
   const size_t MT = (size_t)eng->MT;
   HIPCHK(dalloc(&eng->Yspec, 2 * S * MT * F));
@@ -905,7 +959,8 @@ void danse_engine_destroy(danse_engine* eng) {
                   eng->dxEst, eng->resYB, eng->resYU, eng->resZall, eng->resZhat, eng->resRyyG, eng->resRnnG,
                   eng->resUFlag, eng->resZFlag, eng->resGateRound, eng->resDanseFni, eng->resErr, eng->resFams,
                   eng->resFrames, eng->resChanNode, eng->resTrace, eng->condHist, eng->dxRecFrames,
-                  eng->dxRecOut, eng->dFsEv, eng->rawStream, eng->vCache, eng->l64Cache, eng->lzStats};
+                  eng->dxRecOut, eng->dFsEv, eng->rawStream, eng->vCache, eng->l64Cache, eng->lzStats,
+                  eng->dWideIds, eng->wideWork};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (eng->dx) danse_dxcp_destroy(eng->dx);
@@ -963,7 +1018,33 @@ static UpdateArgs make_update(danse_engine* e, int r) {
 
 // mask: the nodes updated by this launch; full: the round's last update
 // launch (its per-round extras run)
+static void launch_wide(danse_engine* e, int r, hipStream_t st, unsigned mask) {
+  const int nW = (int)e->wideIds.size();
+  UpdateArgs a = make_update(e, r);
+  a.nodeMask = mask;
+  const int S = e->S, F = e->F, K = e->K;
+  hipLaunchKernelGGL(wide_rec_kernel, dim3(F, S * nW), dim3(kWideRecThr), 0, st, a, e->dFnAll, e->dWideIds, nW);
+  for (int w = 0; w < nW; ++w) {
+    const FamNode& fn = e->fns[e->wideIds[w]];
+    if (!((mask >> fn.k) & 1u) || !e->wideSolve[(size_t)r * nW + w]) continue;
+    const int D = fn.D;
+    const int slotNext = e->keepHistory ? r + 1 : ((r + 1) & 1);
+    wide::WideArgs wa{};
+    wa.D = D; wa.rank = e->rank; wa.gevd = e->gevd; wa.F = F; wa.nItems = (long long)S * F; wa.layout = 1;
+    wa.RyyF = e->Ryy + fn.scmOff; wa.Rnn = e->Rnn + fn.scmOff;
+    wa.srcScene = e->scmStride; wa.srcBin = (long long)D * (D + 1) / 2;
+    wa.nOut = 1; wa.refs[0] = fn.ref; wa.wOff[0] = fn.wOff + (long long)slotNext * F * D;
+    wa.w = e->wHist; wa.wScene = e->wStride; wa.wBin = D;
+    wa.work = e->wideWork;
+    wa.flags = e->dFlags + ((size_t)r * S * kMaxFam + fn.fam) * K + fn.k;
+    wa.flagStride = (long long)kMaxFam * K;
+    (void)wide::launch_wide_filters(wa, e->wideChunk, st);
+  }
+  hipLaunchKernelGGL(wide_tail_kernel, dim3(F, S * nW), dim3(64), 0, st, a, e->dFnAll, e->dWideIds, nW);
+}
+
 static void launch_update(danse_engine* e, int r, hipStream_t st, unsigned mask = ~0u, bool full = true) {
+  if (!e->wideIds.empty()) launch_wide(e, r, st, mask);
   for (auto& cl : e->classes) {
     UpdateArgs a = make_update(e, r);
     a.nodeMask = mask;
@@ -1354,6 +1435,7 @@ int danse_engine_run_resident(danse_engine* eng, void* stream) {
 
 int danse_engine_set_cond(danse_engine* eng, int32_t every) {
   if (!eng || every < 0) return fail(eng, "bad condition-number interval");
+  if (every > 0 && !eng->wideIds.empty()) return fail(eng, "condition numbers above 64 channels are not supported");
   HIPCHK(hipSetDevice(eng->dev));
   if (eng->graphExec) {   // the captured run changes
     (void)hipGraphExecDestroy(eng->graphExec);
@@ -1646,6 +1728,7 @@ int danse_engine_set_flags(danse_engine* eng, const uint8_t* flags, void* stream
     (void)hipGraphExecDestroy(eng->graphExec);
     eng->graphExec = nullptr;
   }
+  if (!eng->wideIds.empty()) build_wide_lists(eng, flags);
   return build_split_lists(eng, flags);
 }
 

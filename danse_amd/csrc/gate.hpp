@@ -44,6 +44,9 @@ DANSE_DEV void tri_ij(int e, int& i, int& j) {
 // All 64 lanes share every step: the loads, the recursion and the Hermitian
 // test go over the packed lower triangle in storage order (coalesced), the
 // Cholesky's trailing updates over the trailing triangle's entries.
+// (filter dimensions up to kGateMaxD: the online centralised family above
+// 64 channels -- [D][D + 1] complex doubles of dynamic LDS, 147 KiB at 96)
+constexpr int kGateMaxD = 96;
 __global__ void __launch_bounds__(64) gate_kernel(const UpdateArgs a, const FamNode* fns, const GateCand* cand,
                                                  const long long* initOff, const cd* scm0, int perBin, int* verdict) {
   extern __shared__ cd gX[];   // [D][D + 1]
@@ -56,9 +59,9 @@ __global__ void __launch_bounds__(64) gate_kernel(const UpdateArgs a, const FamN
   const int P = D + 1;
   const int T = D * (D + 1) / 2;
   const uint8_t fl = a.flags[(((long long)a.r * a.S + s) * kMaxFam + d.fam) * a.K + d.k];
-  __shared__ cf gy[64];
-  __shared__ double gd[64];   // diagonal entries (the trace)
-  gy[li] = load_y(a, d, s, f, li, li < D);
+  __shared__ cf gy[kGateMaxD];
+  __shared__ double gd[kGateMaxD];   // diagonal entries (the trace)
+  for (int i = li; i < D; i += 64) gy[i] = load_y(a, d, s, f, i, true);
   __syncthreads();
   const double beta = a.beta[s * a.K + d.k];
   const cd* R0 = scm0 + initOff[c.fni] + (perBin ? (long long)f * D * D : 0ll);
@@ -69,7 +72,7 @@ __global__ void __launch_bounds__(64) gate_kernel(const UpdateArgs a, const FamN
     const double cy = (op == DANSE_OP_SET) ? 1.0 / D : (1.0 - beta) / D;
     const double cx = (op == DANSE_OP_SET) ? 0.0 : beta;
     bool herm = true;
-    if (li < D) gd[li] = 0.0;
+    for (int i = li; i < D; i += 64) gd[i] = 0.0;
     __syncthreads();
     for (int e = li; e < T; e += 64) {
       int i, j;
@@ -103,7 +106,8 @@ __global__ void __launch_bounds__(64) gate_kernel(const UpdateArgs a, const FamN
     if (a.gevd && __ballot(!herm) != 0ull) pass = false;
     __syncthreads();
     // full rank (+ positive definite): float64 Cholesky of the lower triangle
-    double tr = (li < D) ? gd[li] : 0.0;
+    double tr = 0.0;
+    for (int i = li; i < D; i += 64) tr += gd[i];
     for (int o = 32; o >= 1; o >>= 1) tr += __shfl_xor(tr, o);
     const double tol = (double)D * 2.220446049250313e-16 * fabs(tr);
     // GEVD (eigvalsh >= 0 and full rank): every pivot above tol.  MWF (rank
@@ -116,7 +120,8 @@ __global__ void __launch_bounds__(64) gate_kernel(const UpdateArgs a, const FamN
         break;
       }
       const double inv = 1.0 / sqrt(fabs(pj));
-      if (li > j && li < D) gX[li * P + j] = inv * gX[li * P + j];
+      for (int row = li; row < D; row += 64)
+        if (row > j) gX[row * P + j] = inv * gX[row * P + j];
       __syncthreads();
       // trailing lower triangle (rows and columns j + 1 .. D - 1), entry by entry
       const int n = D - 1 - j;

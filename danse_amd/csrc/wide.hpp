@@ -24,6 +24,7 @@
 #pragma once
 #include "solver.hpp"
 #include "wide_api.hpp"
+#include "../../include/danse_mi355x_defs.h"
 
 namespace danse {
 namespace wide {
@@ -145,6 +146,10 @@ __global__ void __launch_bounds__(kThr) wide_filter_kernel(const WideArgs a) {
   const int t = threadIdx.x;
   const int D = a.D;
   const int s = (int)(b / a.F), f = (int)(b % a.F);
+  if (a.flags) {   // workgroup-uniform
+    const unsigned char fl = a.flags[(long long)s * a.flagStride];
+    if (!(fl & DANSE_FLAG_SOLVE) || (fl & DANSE_FLAG_PREGIVEN)) return;
+  }
   const long long base = (long long)s * a.srcScene + (long long)f * a.srcBin;
   cd* Lc = a.work + (long long)blockIdx.x * 2 * D * D;   // Lc[k * D + i] = L[i][k]
   cd* Cw = Lc + (long long)D * D;

@@ -27,6 +27,11 @@ struct WideArgs {   // (passed by value: the per-output tables ride in the kerne
   long long wScene, wBin;
   int* diag;                    // [nItems] or null: 1 = factor / eigen failure, 0 ok
   cd* work;                     // [gridDim.x][2][D][D]
+  // online engine (scene items): item (s, f) solves only when the flag byte
+  // flags[s * flagStride] has DANSE_FLAG_SOLVE and not DANSE_FLAG_PREGIVEN;
+  // null = every item solves
+  const unsigned char* flags;
+  long long flagStride;
 };
 
 // Launch wide_filter_kernel over a.nItems items, `chunk` workgroups per

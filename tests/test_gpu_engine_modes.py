@@ -308,6 +308,63 @@ def test_headline_shape_K32x8_D39_long_run_vs_oracle():
     assert de <= 1e-4
 
 
+def test_online_centralised_wide_vs_oracle():
+    """The online centralised family above 64 channels (wide_online.hpp):
+    K = 3 nodes x 32 mics, sum(M) = 96, asy, with the DANSE family (D = 34)
+    alongside.  The centralised SCMs (96 x 96 per bin and node) are updated
+    per round on the device and solved by the float64 wide classes once the
+    reference gate (counters > 96, Hermitian / PSD / rank checks on the
+    device) lets them (d_classes.py:1542-1585,2139-2201,3343-3387).  The
+    float64 oracle runs until a few rounds past the centralised start."""
+    from danse_amd.core import danse_multi
+    from danse_amd.scene import make_scene
+    from oracle import danse_ref_cpu as O
+    import os
+    case = dict(name='online_centr_wide_K3x32', M=[32] * 3, dur=7.2, seed=43,
+                danse=dict(BATTERY, nodeUpdating='asy', computeCentralised=True))
+    dp, wp = make_case_params(case)
+    sc = make_scene(case['M'], sigDur=case['dur'], seed=case['seed'], pauseDuration=0.9)
+    sc.get_vad_per_frame(dp.DFTsize, dp.Ns, wp.vadMinProportionActive)
+    dv = danse_multi([sc], dp)[0]
+    K, MT = 3, 96
+    assert dv.wCentr[0].shape[-1] == MT
+    # the centralised start: the counters of the node-averaged VAD pass 96
+    vad = np.stack([nd.vadPerFrame for nd in sc.wasn])
+    cv = vad.sum(axis=0) / K > 0
+    ny = np.cumsum(cv)
+    nn = np.arange(1, len(cv) + 1) - ny
+    c0 = int(np.argmax((ny > MT) & (nn > MT)))
+    R0 = c0 + 6
+    assert R0 + 2 <= dv.nRounds, (c0, dv.nRounds)
+    O.set_workers(min(16, max(2, len(os.sched_getaffinity(0)))))
+    try:
+        ov = O.OnlineDANSE(sc, dp, vadMinProp=wp.vadMinProportionActive, maxRounds=R0)
+        ov.progressEvery = 20
+        ov.run()
+    finally:
+        O.set_workers(0)
+    assert np.array_equal(dv.startRound, ov.startRound)
+    assert int(np.sum(dv.diag)) == 0
+    errs, errc = [], []
+    for k in range(K):
+        s0 = int(ov.startRound[k])
+        errs.append(_bin_rel(dv.wTilde[k][:, s0 + 1:R0 + 1], ov.wTilde[k][:, s0 + 1:R0 + 1]).ravel())
+        # centralised filters over every round (the init ones before its start)
+        ec = _bin_rel(dv.wCentr[k][:, 1:R0 + 1], ov.wCentr[k][:, 1:R0 + 1])
+        errc.append(ec.ravel())
+    st, stc = _stats(np.concatenate(errs)), _stats(np.concatenate(errc))
+    T1 = int(ov.idxEnd) - (dp.DFTsize - dp.Ns)
+    de, dc = rel_err(dv.d[:T1], ov.d[:T1]), rel_err(dv.dCentr[:T1], ov.dCentr[:T1])
+    # the centralised filters did change after the start (solved, not carried)
+    moved = np.linalg.norm(dv.wCentr[0][:, R0] - dv.wCentr[0][:, c0], axis=-1)
+    print(case['name'], 'centralised start', c0, 'rounds', R0, 'w', st, 'wCentr', stc, 'd', de, 'dCentr', dc,
+          'wCentr moved (median over bins)', float(np.median(moved)))
+    assert float(np.median(moved)) > 0.0
+    assert st['median'] <= 1e-5 and st['p99'] <= 1e-4, st
+    assert stc['median'] <= 1e-5 and stc['p99'] <= 1e-4, stc
+    assert de <= 1e-4 and dc <= 1e-4, (de, dc)
+
+
 @pytest.mark.parametrize('name', ['online_C_sro_comp_asy', 'online_ragged_asy_r2', 'online_E_fs_L64_asy'])
 def test_dv_fields_on_device(name):
     """Every dv field the reference's post-processing reads is present; the
