@@ -128,6 +128,11 @@ struct danse_engine {
   float* rawStream = nullptr;      // [S][MT][zLen] (cfg.rawStreams)
   float* zChunk = nullptr;         // node-sharded DXCP: [K][S][Ns] exchange buffer (borrowed)
   float *wIR = nullptr, *dSn = nullptr;
+  // desSigProcessingType 'conv' (danse_cfg.desSigConv): per-family-node T(z)
+  // IRs of the new filter's first M_k columns [S][nFN][Mmax][2N - 1] and the
+  // window cross-correlation table of dist_fct_approx(w, win_s, win_s, Ns)
+  int desConv = 0;
+  float *convIR = nullptr, *dSnConv = nullptr;
   // DXCP-PhaT SRO estimation in the loop (cfg.dxcp, an extension: the
   // reference's integration raises, quirk Q12): one estimator per (scene,
   // receiver, sender), fed every kDxEvery rounds
@@ -821,6 +826,23 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
   if (eng->liStride > 0) HIPCHK(dalloc(&eng->liCache, (size_t)S * eng->liStride));
   if (eng->vStride > 0) HIPCHK(dalloc(&eng->vCache, (size_t)S * eng->vStride));
   if (eng->vStride > 0) HIPCHK(dalloc(&eng->lzStats, (size_t)2 * R * kLzSlots));
+  if (c->desSigConv) {
+    // (the centralised / SSBC vectors' first M_k channels under SRO clocks
+    // come from the receivers' raw buffers: not on this path)
+    if (c->cEnd) return fail(eng, "desSigProcessingType conv with centralised / SSBC estimates under SRO clocks");
+    eng->desConv = 1;
+    HIPCHK(dalloc(&eng->convIR, (size_t)S * eng->fns.size() * eng->Mmax * tzc::kA));
+    std::vector<float> sn(tzc::kA);
+    for (int i = 0; i < tzc::kA; ++i) {
+      const int tau = i - (c->N - 1);
+      double acc = 0.0;
+      for (int n = std::max(0, -tau); n < std::min(c->N, c->N - tau); ++n)
+        acc += (double)c->winSynthesis[n] * (double)c->winSynthesis[n + tau];
+      sn[i] = (float)(acc / ((double)c->N * (double)c->Ns));
+    }
+    HIPCHK(dalloc(&eng->dSnConv, (size_t)tzc::kA));
+    HIPCHK(hipMemcpy(eng->dSnConv, sn.data(), sn.size() * sizeof(float), hipMemcpyHostToDevice));
+  }
   if (const char* tr = std::getenv("DANSE_UPDATE_TRACE")) {
     // (upper bound: one wave per (scene, family-node, bin))
     eng->updTraceRound = std::atoi(tr);
@@ -960,7 +982,7 @@ void danse_engine_destroy(danse_engine* eng) {
                   eng->resUFlag, eng->resZFlag, eng->resGateRound, eng->resDanseFni, eng->resErr, eng->resFams,
                   eng->resFrames, eng->resChanNode, eng->resTrace, eng->condHist, eng->dxRecFrames,
                   eng->dxRecOut, eng->dFsEv, eng->rawStream, eng->vCache, eng->l64Cache, eng->lzStats,
-                  eng->dWideIds, eng->wideWork};
+                  eng->dWideIds, eng->wideWork, eng->convIR, eng->dSnConv};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (eng->dx) danse_dxcp_destroy(eng->dx);
@@ -1018,6 +1040,70 @@ static UpdateArgs make_update(danse_engine* e, int r) {
 
 // mask: the nodes updated by this launch; full: the round's last update
 // launch (its per-round extras run)
+// ---- desSigProcessingType 'conv' (get_desired_sig_chunk, d_base.py:
+// 2085-2100; get_desired_signal, d_classes.py:2623-2709): for every
+// family-node, the IRs dist_fct_approx(w[r + 1][:, m], win_s, win_s, Ns) of
+// the first M_k filter columns (one wave each, tzconv.hpp ir_wave), then the
+// last Ns samples of their convolutions with the first M_k channels of the
+// family's update frame (yTD = yTilde[k][:, i, :nLocalMic[k]]), idDesired =
+// 2N - 1 - Ns .. 2N - 2 (one below the broadcast chunks' indices), summed
+// over m into d[end - Ns, end); dhat is NaN (dhatCurr = None).
+__global__ void __launch_bounds__(256) conv_ir_kernel(const UpdateArgs a, const FamNode* fns, int nFN, int Mmax,
+                                                      const cf* tw, const float* snc, float* irOut) {
+  __shared__ cf lds[4][wfft::kLdsElems];
+  const int wv = threadIdx.x >> 6;
+  const int item = blockIdx.x * 4 + wv;
+  if (item >= a.S * nFN * Mmax) return;
+  const int m = item % Mmax;
+  const int fni = (item / Mmax) % nFN;
+  const int s = item / (nFN * Mmax);
+  const FamNode d = fns[fni];
+  if (m >= d.M || !node_in(a.nodeMask, d.k)) return;
+  const int slotNext = a.wHistory ? a.r + 1 : ((a.r + 1) & 1);
+  const cf* w = a.wHist + (long long)s * a.wStride + d.wOff + (long long)slotNext * a.F * d.D + m;
+  float* o = irOut + (((long long)s * nFN + fni) * Mmax + m) * tzc::kA;
+  tzc::ir_wave(lds[wv], tw, snc, [&](int f) { return w[(long long)f * d.D]; }, [&](int t, float v) { o[t] = v; });
+}
+
+__global__ void __launch_bounds__(tzc::kThr) conv_d_kernel(const UpdateArgs a, const FamNode* fns, int nFN, int Mmax,
+                                                           const int* upEnd, const float* y, int T, int N, int Ns,
+                                                           const float* ir, float* d) {
+  __shared__ tzc::ConvLds sm;
+  const int fni = blockIdx.x % nFN;
+  const int s = blockIdx.x / nFN;
+  const FamNode fn = fns[fni];
+  if (!node_in(a.nodeMask, fn.k)) return;
+  const int r = a.r, K = a.K, F = a.F;
+  const int end = upEnd[r * K + fn.k];
+  const float* irb = ir + ((long long)s * nFN + fni) * Mmax * tzc::kA;
+  float* dd = d + (((long long)fn.fam * a.S + s) * K + fn.k) * T;
+  const int* ch = a.chanList + fn.chanOff;   // the family vector's first M_k channels (all < MT here)
+  tzc::conv_block(
+      sm, fn.M, Ns,
+      [&](int q, int m) { return y[((long long)s * a.MT + ch[m]) * T + min(max(end - N + q, 0), T - 1)]; },
+      [&](int q, int) { return end - N + q >= 0 && end - N + q < T; },
+      [&](int i, int m) { return irb[(long long)m * tzc::kA + i]; },
+      [&](int e, float v) {
+        const int idx = end - Ns + e;
+        if (idx >= 0 && idx < T) dd[idx] = v;
+      },
+      -1);
+  const float qn = __builtin_nanf("");
+  for (int f = threadIdx.x; f < F; f += blockDim.x)
+    a.dhat[((((long long)fn.fam * a.S + s) * K + fn.k) * a.R + r) * F + f] = cf{qn, qn};
+}
+
+static void launch_conv(danse_engine* e, int r, hipStream_t st, unsigned mask) {
+  UpdateArgs a = make_update(e, r);
+  a.nodeMask = mask;
+  const int nFN = (int)e->fns.size();
+  const int items = e->S * nFN * e->Mmax;
+  hipLaunchKernelGGL(conv_ir_kernel, dim3((items + 3) / 4), dim3(256), 0, st, a, e->dFnAll, nFN, e->Mmax,
+                     e->dTw + e->N, e->dSnConv, e->convIR);
+  hipLaunchKernelGGL(conv_d_kernel, dim3(e->S * nFN), dim3(tzc::kThr), 0, st, a, e->dFnAll, nFN, e->Mmax, e->dUpEnd,
+                     e->y, e->T, e->N, e->Ns, e->convIR, e->d);
+}
+
 static void launch_wide(danse_engine* e, int r, hipStream_t st, unsigned mask) {
   const int nW = (int)e->wideIds.size();
   UpdateArgs a = make_update(e, r);
@@ -1060,6 +1146,7 @@ static void launch_update(danse_engine* e, int r, hipStream_t st, unsigned mask 
       launch_split_solve_class(cl.DMAX, a, cl.solveCount[r], st);
     }
   }
+  if (e->desConv) launch_conv(e, r, st, mask);
   if (!full) return;
   if (e->condEvery > 0 && (r + 1) % e->condEvery == 0) {
     // (saved when i - last >= every, last starting at -1: d_classes.py:2128-2130)
@@ -1127,6 +1214,8 @@ static void launch_fs(danse_engine* e, int row, hipStream_t st) {
 // analysis alone (no local-frame analyses, no estimate synthesis)
 static void launch_bcast(danse_engine* e, int r, int synth, int bc, hipStream_t st, unsigned zMask = ~0u,
                          int zOnly = 0) {
+  if (e->desConv) synth = 0;   // ('conv': conv_d_kernel writes the estimates after each update)
+  if (!synth && !bc) return;
   BcastArgs a = make_bcast(e, r, synth, bc);
   a.zMask = zMask;
   a.zOnly = zOnly;
@@ -1351,6 +1440,7 @@ static UpdateArgs make_update_resident(danse_engine* e, int r) {
 
 int danse_engine_run_resident(danse_engine* eng, void* stream) {
   if (!eng || !eng->y) return fail(eng, "inputs not set");
+  if (eng->desConv) return fail(eng, "resident run: WOLA estimates only (desSigProcessingType wola)");
   HIPCHK(hipSetDevice(eng->dev));
   int NB = 0;
   if (int rc = resident_prepare(eng, NB)) return rc;

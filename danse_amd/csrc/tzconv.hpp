@@ -91,8 +91,11 @@ DANSE_DEV void ir_wave(cf* lds, const cf* __restrict__ tw, const float* __restri
 // read value discarded -- the read stays unconditional); aAt(i, m): IR tap
 // i < kA of sensor m; out(e, v): output e in [0, L).
 // nTiles = ceil(L / kR) output tiles, G = kThr / nTiles q ranges (G >= 1).
+// off: 0 for the broadcast chunks (idDesired = kA - L + 1 .. kA,
+// d_base.py:1924-1927), -1 for the 'conv' desired-signal chunk (kA - Ns ..
+// kA - 1, d_base.py:2092).
 template <class YF, class YK, class AF, class OF>
-DANSE_DEV void conv_block(ConvLds& sm, int M, int L, YF yAt, YK yKeep, AF aAt, OF out) {
+DANSE_DEV void conv_block(ConvLds& sm, int M, int L, YF yAt, YK yKeep, AF aAt, OF out, int off = 0) {
   const int t = threadIdx.x;
   const int nTiles = (L + kR - 1) / kR;
   const int G = kThr / nTiles;
@@ -100,7 +103,7 @@ DANSE_DEV void conv_block(ConvLds& sm, int M, int L, YF yAt, YK yKeep, AF aAt, O
   const bool active = g < G;
   const int qc = (kN + G - 1) / G;
   const int q0 = min(kN, g * qc), q1 = min(kN, q0 + qc);
-  const int d0 = kA - L + 1 + tile * kR;   // convolution index of this thread's first output
+  const int d0 = kA - L + 1 + off + tile * kR;   // convolution index of this thread's first output
   float acc[kR];
 #pragma unroll
   for (int r = 0; r < kR; ++r) acc[r] = 0.f;

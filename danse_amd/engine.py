@@ -142,8 +142,8 @@ class DanseEngine:
                 raise ValueError('all scenes of one engine must share the node clocks')
         if p.simType != 'online':
             raise ValueError('DanseEngine runs the online engine (simType online)')
-        if p.desSigProcessingType != 'wola':
-            raise NotImplementedError('desSigProcessingType conv (T(z) estimate) on the device path')
+        if p.desSigProcessingType not in ('wola', 'conv'):
+            raise ValueError(f'desSigProcessingType {p.desSigProcessingType!r}')
         self.device = device
         self.keepHistory = keepHistory
         # latency layout: GEVD filter dimensions <= 12 on the 4 x 4 lane-grid
@@ -566,6 +566,8 @@ class DanseEngine:
             c.cdCompensate = int(bool(p.compensateSROs))
         c.cEnd = _ptr(self._cEnd, ctypes.c_int32)
         c.rawStreams = int(self._rawStreams)
+        # 'conv': T(z) time-domain estimates (get_desired_sig_chunk, d_base.py:2085-2100)
+        c.desSigConv = int(p.desSigProcessingType == 'conv')
         c.cPhase = _ptr(self._cPhase, ctypes.c_double)
         c.zStreamLen = int(self.rt.zStreamLen) if self.fewSamples else 0
         self.zLen = c.zStreamLen if self.fewSamples else self.R * self.Ns

@@ -149,6 +149,13 @@ typedef struct danse_cfg {
    * frame ends floor(t fs) of consecutive chunks may overlap or skip a
    * sample, so the stream is not a slice of y.                           */
   int32_t rawStreams;
+  /* desSigProcessingType 'conv' (get_desired_sig_chunk, d_base.py:2085-2100,
+   * d_classes.py:2623-2709): 1 = every family's time-domain estimate is the
+   * last Ns samples of the T(z) convolution of the first M_k channels of its
+   * observation vector's update frame with the IRs dist_fct_approx(w[r + 1],
+   * win_s, win_s, Ns) of the same filter columns, written to d[end - Ns,
+   * end) (no overlap-add); dhat is NaN (the reference stores None).      */
+  int32_t desSigConv;
 } danse_cfg;
 
 typedef struct danse_engine danse_engine;

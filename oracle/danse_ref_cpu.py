@@ -780,7 +780,13 @@ class OnlineDANSE:
             sroOut = (self.SROsppm[self.neighbors[k]] - self.SROsppm[k]) * 1e-6
             self.SROsResiduals[k][i, :] = sroOut
         elif p.estimateSROs == 'CohDrift':
-            self._cohdrift(k, i)
+            if self.extEst is not None:
+                # replay: the residual estimates of another run (the device's)
+                # drive the same closed-loop accumulation (a test of the loop
+                # against the estimator, tests/test_gpu_engine_modes.py)
+                self.SROsResiduals[k][i, :] = self.extEst[k][i, :]
+            else:
+                self._cohdrift(k, i)
         elif p.estimateSROs == 'DXCPPhaT':
             self.SROsResiduals[k][i, :] = self.extEst[k][i, :]
         if p.compensateSROs:
@@ -803,6 +809,11 @@ class OnlineDANSE:
                     e = int(np.sum(self.M[:q + 1]))
                     self.phaseShiftFactorsCentr[k][b:e] -= est * self.Ns
         # get_desired_signal (2623-2709)
+        if p.desSigProcessingType == 'conv':
+            self._conv_estimates(k, i, yT, yC if p.computeCentralised else None, yLoc,
+                                 yS if p.computeSingleSensorBroadcast else None)
+            self.i[k] += 1
+            return
         nf = np.sqrt(self.Ns)
         sl = slice(self.idxBeg, self.idxEnd)
         _, dh = desired_sig_chunk(self.danse[k].w[:, i + 1, :], yTHat, self.f, nf, self.d[sl, k])
@@ -817,6 +828,38 @@ class OnlineDANSE:
             _, dh = desired_sig_chunk(self.ssbc[k].w[:, i + 1, :], ySHat, self.f, nf, self.dSSBC[sl, k])
             self.dHatSSBC[:, i, k] = dh
         self.i[k] += 1
+
+    # ---- get_desired_signal with desSigProcessingType 'conv'
+    # (get_desired_sig_chunk, d_base.py:2085-2100; d_classes.py:2623-2709):
+    # per family, wIR = dist_fct_approx(w[:, i+1, :], win_s, win_s, Ns) (the
+    # closed form, oracle/tz_ref.py, equal to the reference's diagonal sums to
+    # ~1e-16), the last Ns samples (idDesired = len - Ns .. len - 1) of the
+    # convolutions of its first M_k columns with the first M_k channels of
+    # the family's time-domain update frame, summed, into d[idxEnd - Ns,
+    # idxEnd); dhat is None (NaN in the complex array) ----
+    def _conv_estimates(self, k, i, yT, yC, yLoc, yS):
+        from . import tz_ref
+        p, Ns, Mk = self.p, self.Ns, self.M[k]
+        sl = slice(self.idxEnd - Ns, self.idxEnd)
+
+        def chunk(w, yTD):
+            wIR = tz_ref.dist_fct_approx_closed(w, self.f, self.f, Ns)
+            idD = np.arange(start=len(wIR) - Ns, stop=len(wIR))
+            out = np.zeros((Ns, Mk))
+            for m in range(Mk):
+                out[:, m] = tz_ref.extract_few_samples_from_convolution(idD, wIR[:, m], yTD[:, m])
+            return np.sum(out, axis=1)
+        self.d[sl, k] = chunk(self.danse[k].w[:, i + 1, :], yT)
+        self.dhat[:, i, k] = np.nan
+        if p.computeCentralised:
+            self.dCentr[sl, k] = chunk(self.centr[k].w[:, i + 1, :], yC)
+            self.dHatCentr[:, i, k] = np.nan
+        if p.computeLocal:
+            self.dLocal[sl, k] = chunk(self.local[k].w[:, i + 1, :], yLoc)
+            self.dHatLocal[:, i, k] = np.nan
+        if p.computeSingleSensorBroadcast:
+            self.dSSBC[sl, k] = chunk(self.ssbc[k].w[:, i + 1, :], yS)
+            self.dHatSSBC[:, i, k] = np.nan
 
     # ---- condition numbers (d_classes.py:2126-2186, ConditionNumbers
     # .get_new_cond_number / compute_condition_numbers, d_classes.py:19-130):

@@ -21,6 +21,7 @@ TAG=$1
 shift
 O=gpurun_out/$TAG
 mkdir -p "$O"
+NT=0
 summary() {
   python - "$1" "$2" <<'PY'
 import json, sys
@@ -42,9 +43,10 @@ for step in "$@"; do
         > "$O/pytest_gpu.log" 2>&1 || { echo "suite failed"; tail -40 "$O/pytest_gpu.log"; exit 1; }
       grep -E "passed|failed" "$O/pytest_gpu.log" | tail -2 ;;
     tests)
+      NT=$((NT + 1))
       timeout -k 10 900 python -u -m pytest -x -v -s --timeout 600 --timeout-method thread -m gpu tests -k "$a1" \
-        > "$O/pytest_k.log" 2>&1 || { echo "tests failed"; tail -40 "$O/pytest_k.log"; exit 1; }
-      grep -E "passed|failed" "$O/pytest_k.log" | tail -2 ;;
+        > "$O/pytest_k$NT.log" 2>&1 || { echo "tests failed"; tail -40 "$O/pytest_k$NT.log"; exit 1; }
+      grep -E "passed|failed" "$O/pytest_k$NT.log" | tail -2 ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 \
         || { echo "smoke failed"; tail -5 "$O/smoke.log"; exit 1; }

@@ -118,6 +118,11 @@ ONLINE_CASES = [
                     computeCentralised=True, computeSingleSensorBroadcast=not comp))
       for L, dur, seed in ((1, 2.5, 20), (16, 6.0, 21), (512, 2.5, 22))
       for tag, comp in (('nocomp', False), ('comp', True))],
+    # desSigProcessingType 'conv': T(z) time-domain estimates of every family
+    # (get_desired_sig_chunk, d_base.py:2085-2100), ragged nodes, asy
+    dict(name='online_conv_ragged_asy', M=[2, 3, 2], dur=2.0, seed=7,
+         danse=_d(SANDBOX, nodeUpdating='asy', computeLocal=True, computeCentralised=True,
+                  computeSingleSensorBroadcast=True, desSigProcessingType='conv')),
 ]
 
 BATCH_CASES = [

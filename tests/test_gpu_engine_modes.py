@@ -464,6 +464,28 @@ def test_config_C_shape_K16_sro_vs_oracle(est):
             ce = float(np.max(np.abs(ed - eo))) / max(float(np.max(np.abs(eo))), 1e-12)
             print('  node', k, 'cumulative SRO estimate rel err', ce)
             assert ce <= 5e-2, ce
+    if est == 'CohDrift':
+        # the same loop driven by the device's own residual estimates: the
+        # float64 oracle's filters then match the device's at the tolerance
+        # of every other case -- the p99 above 1e-4 of the free-running
+        # comparison is the estimator loop (float32 spectra -> coherence
+        # phase -> estimate -> compensation of every later frame), not the
+        # filter path
+        O.set_workers(min(16, max(2, len(__import__('os').sched_getaffinity(0)))))
+        try:
+            orp = O.danse(sc, dp, vadMinProp=wp.vadMinProportionActive,
+                          sroEstimates=[np.asarray(dv.SROsResiduals[k]) for k in range(16)])
+        finally:
+            O.set_workers(0)
+        errs = []
+        for k in range(16):
+            s0 = int(orp.startRound[k])
+            errs.append(_bin_rel(dv.wTilde[k][:, s0 + 1:dv.nRounds + 1], orp.wTilde[k][:, s0 + 1:dv.nRounds + 1]).ravel())
+        sr = _stats(np.concatenate(errs))
+        dr = rel_err(dv.d, orp.d)
+        print(case['name'], 'replayed device estimates: w', sr, 'd', dr)
+        assert sr['median'] <= 1e-5 and sr['p99'] <= 1e-4, sr
+        assert dr <= 1e-4
 
 
 def test_cohdrift_sro_estimates_vs_oracle():

@@ -87,7 +87,8 @@ def test_scene_conv_vad_vs_reference(golden_dir):
     _, v32 = convolve_vad(wet[ref].astype(np.float32), np.ones((len(ref), 1), np.float32), **kw)
     print('wet rel err', err, 'VAD mismatch (device wet)', mism, 'active', float(g['vad'].mean()))
     # (float32 accumulation over the 3200-tap IRs: ~sqrt(nIR) 2^-24 = 3.4e-6
-    # of the peak; measured 2.8e-6 on MI355X)
-    assert err <= 1e-5, err
+    # of the peak; measured 2.76e-6 on MI355X, deterministic for these fixed
+    # inputs)
+    assert err <= 4e-6, err
     assert np.array_equal(v32, g['vad32'])
     assert mism <= 1e-3, mism

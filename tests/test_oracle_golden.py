@@ -26,7 +26,10 @@ def test_online_oracle_matches_reference(case, golden_dir):
     dv = O.danse(sc, dp, vadMinProp=wp.vadMinProportionActive)
     every = 16
     assert rel_err(dv.d, g['d']) < TOL
-    assert rel_err(dv.dhat[:, ::every, :], g['dhat']) < TOL
+    if np.all(np.isnan(g['dhat'])):   # desSigProcessingType 'conv': dhatCurr = None
+        assert np.all(np.isnan(dv.dhat[:, ::every, :]))
+    else:
+        assert rel_err(dv.dhat[:, ::every, :], g['dhat']) < TOL
     for k in range(len(case['M'])):
         assert rel_err(dv.wTilde[k][:, ::every, :], g[f'w_{k}']) < TOL
         if f'wExt_{k}' in g:
