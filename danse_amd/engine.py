@@ -73,7 +73,12 @@ def init_scm_slices(p, Mtot, K, F):
     nodes or one per node (drawn node by node from the same generator), each
     ``(Mtot, Mtot)`` or per bin ``(F, Mtot, Mtot)``.  Returns the K slices."""
     if p.covMatInitType == 'batch_estimates':
-        raise NotImplementedError('covMatInitType batch_estimates (batch-mode SCM estimates as the online init)')
+        # the reference's own error: init_covmats_from_batch calls
+        # get_y_tilde_batch(k, False), whose useThisFilter=False is then
+        # indexed (d_classes.py:1002-1005 -> d_base.py:2526-2528); the run
+        # never starts (tests/golden/ref_modes.npz records it)
+        raise TypeError("'bool' object is not subscriptable (covMatInitType 'batch_estimates': "
+                        "init_covmats_from_batch, d_classes.py:1002-1005)")
     rng = np.random.default_rng(p.seed)
     dims = (Mtot, Mtot) if p.covMatSameInitForAllFreqs else (F, Mtot, Mtot)
 

@@ -393,7 +393,8 @@ class OnlineDANSE:
         rng = np.random.default_rng(p.seed)
         args = (p.covMatInitType, p.covMatRandomInitScaling, p.covMatEyeInitScaling)
         if p.covMatInitType == 'batch_estimates':
-            raise NotImplementedError('covMatInitType batch_estimates')
+            # (the reference raises here: d_classes.py:1002-1005, see danse_amd.engine.init_scm_slices)
+            raise TypeError("'bool' object is not subscriptable")
         if p.covMatSameInitForAllNodes:
             dims = (self.Mtot, self.Mtot) if p.covMatSameInitForAllFreqs else (F, self.Mtot, self.Mtot)
             fullSlice = init_covmats(dims, rng, *args)

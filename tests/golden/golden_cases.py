@@ -386,3 +386,10 @@ def scene_inputs(case):
 COND_CASES = [dict(name='cond_k4m3', M=[3, 3, 3, 3], dur=2.0, seed=41,
                    danse=_d(BATTERY, nodeUpdating='asy', computeLocal=True, saveConditionNumber=True,
                             saveConditionNumberEvery=3))]
+
+
+# online modes whose error behaviour is pinned (make_golden._run_modes):
+# covMatInitType 'batch_estimates' raises inside the reference itself
+# (init_covmats_from_batch, d_classes.py:1002-1005)
+REF_MODES_CASE = dict(name='ref_modes', base=BATTERY,
+                      modes={'batch_estimates': dict(covMatInitType='batch_estimates')})

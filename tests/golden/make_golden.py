@@ -26,7 +26,7 @@ from golden_cases import ONLINE_CASES, BATCH_CASES, SRO_EVENT_CASES, KAT_CASES, 
 from golden_cases import DXCP_CASES, dxcp_inputs, TZ_CASES, tz_inputs, CLDXCP_CASES, cldxcp_acs  # noqa: E402
 from golden_cases import METRIC_CASES, metric_inputs, GETMETRICS_CASE, get_metrics_inputs  # noqa: E402
 from golden_cases import FIELD_CASES, FIELD_STFT_BIN_STEP, STOI_CASES, stoi_inputs, E2E_METRICS_CASE  # noqa: E402
-from golden_cases import SCENE_CASES, scene_inputs, COND_CASES  # noqa: E402
+from golden_cases import SCENE_CASES, scene_inputs, COND_CASES, REF_MODES_CASE  # noqa: E402
 
 
 def _run_online(ns, case):
@@ -318,6 +318,24 @@ def _run_cond(ns, case):
     return out
 
 
+def _run_modes(ns, case):
+    """The reference's outcome (ran / the exception it raised) for the online
+    modes whose error behaviour the device path mirrors."""
+    out = {}
+    for key, extra in case['modes'].items():
+        sc = make_scene([2, 3], sigDur=2.0, seed=5)
+        p = H.make_params(ns, [2, 3], **dict(case['base'], nodeUpdating='asy', **extra))
+        w = H.to_ref_wasn(ns, sc)
+        p, w = H.prep(ns, p, w)
+        assert all(getattr(p.danseParams, a) == v for a, v in extra.items()), 'parameter not applied'
+        try:
+            ns.core.danse(w, p.danseParams)
+            out[key] = np.array('ran')
+        except Exception as e:   # noqa: BLE001 -- the outcome is what is recorded
+            out[key] = np.array(f'{type(e).__name__}: {e}')
+    return out
+
+
 def main():
     ns = H.load()
     only = sys.argv[1:]
@@ -335,7 +353,8 @@ def main():
            [('metrics', E2E_METRICS_CASE, _run_e2e_metrics)] + \
            [('scene', c, _run_scene) for c in SCENE_CASES] + \
            [('cond', c, _run_cond) for c in COND_CASES] + \
-           [('fields', dict(name=f'fields_{c}', src=c), lambda ns, c: _run_fields(ns, c['src'])) for c in FIELD_CASES]
+           [('fields', dict(name=f'fields_{c}', src=c), lambda ns, c: _run_fields(ns, c['src'])) for c in FIELD_CASES] + \
+           [('modes', REF_MODES_CASE, _run_modes)]
     for kind, case, fn in jobs:
         name = case['name']
         if only and name not in only:
