@@ -533,6 +533,8 @@ def bench_batch(args, wl, S, rank, world, local, dist):
     """The batch workload (config D) as the bench line: run_batch + the CPU
     leg of rank 0."""
     res = run_batch(args, wl, S, rank, world, local, dist)
+    if res is None:   # (--pmc-child)
+        return
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
         cpu = cpu_child(args.workload, args.cpu_seconds, None)
@@ -582,6 +584,11 @@ def run_batch(args, wl, S, rank, world, local, dist):
     else:
         eng = BatchEngine(scenes, dp, device=local)
         step = eng.run
+    if args.pmc_child:
+        # one run for the PMC collector (every kernel its own dispatch)
+        step()
+        torch.cuda.synchronize()
+        return None
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()

@@ -82,6 +82,11 @@ struct BcastArgs {
   // every owned node also go to zChunk [K][S][Ns] (node-major: a rank's block
   // is one all-gather chunk), for the other ranks' estimators
   float* zChunk;
+  // node-sharded engines with centralised / SSBC families (the vectors of
+  // the owned nodes read every node's raw spectra): the grid covers every
+  // node, and the blocks of the nodes this engine does not own run the
+  // analyses of phase 1 alone (no fused spectrum, no z, no estimates)
+  int foreign;
 };
 
 // y[(frame end - N) .. frame end) * win, zero before sample 0 -> buf (complex, imag 0)
@@ -125,9 +130,10 @@ __global__ void __launch_bounds__(NW * 64) bcast_kernel(const BcastArgs a) {
   __shared__ float zq[1024];
   const int wv = threadIdx.x >> 6;
   const int N = a.N, Ns = a.Ns, F = a.F;
-  const int nOwn = a.k1 - a.k0;
-  const int s = blockIdx.x / nOwn;
-  const int k = a.k0 + blockIdx.x % nOwn;
+  const int nGrid = a.foreign ? a.K : a.k1 - a.k0;
+  const int s = blockIdx.x / nGrid;
+  const int k = (a.foreign ? 0 : a.k0) + blockIdx.x % nGrid;
+  const bool owned = k >= a.k0 && k < a.k1;
   const float sqNs = sqrtf((float)Ns);
   const float invSqNs = 1.0f / sqNs;
   const float sc = sqNs / (float)N;
@@ -173,7 +179,7 @@ __global__ void __launch_bounds__(NW * 64) bcast_kernel(const BcastArgs a) {
       cf* dst = (kind == 2) ? a.Cspec + (((long long)(r & 1) * a.S + s) * a.MT + ch) * F
                             : a.Yspec + (((long long)((up ? r + 1 : r) & 1) * a.S + s) * a.MT + ch) * F;
       // (fewSamples: z comes from the T(z) chunk, no fused spectrum here)
-      const bool zk0 = kind == 0 && !a.fsTab;
+      const bool zk0 = kind == 0 && !a.fsTab && owned;
       if (zk0) {
         cf w[16];   // the weights first, at clamped bins (hold())
 #pragma unroll
@@ -203,6 +209,7 @@ __global__ void __launch_bounds__(NW * 64) bcast_kernel(const BcastArgs a) {
     }
   }
   __syncthreads();
+  if (!owned) return;   // (block-uniform)
 
   if (a.doBcast && wv == 0 && a.fsTab) {
     // (a sender outside zMask: its z frame is analysed by a later step)

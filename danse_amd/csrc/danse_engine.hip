@@ -83,6 +83,7 @@ struct danse_engine {
   int graphR0 = -1, graphR1 = -1;
   void* graphStream = nullptr;
   bool ownZspec = true;
+  int foreign = 0;   // BcastArgs.foreign
   bool noRO = false;     // DANSE_NO_RO: never the recursion-only update variants (A/B timing)
   int bcastAblate = 0;   // DANSE_BCAST_ABLATE (diagnostics only; results are wrong when set)
   // initial-state copies for danse_engine_reset
@@ -253,6 +254,8 @@ struct FsArgs {
   float* wIR;                // [S][K][Mmax][2N-1]
   float* zStream;            // [S][K][zLen]
   float* rawStream;          // [S][MT][zLen] raw-sample streams of the centralised buffers, or null
+  int foreign;               // (BcastArgs.foreign) the chunk grid covers every node; the blocks of the
+                             // nodes not owned append the raw samples only
 };
 
 DANSE_DEV const int* fs_entry(const FsArgs& a, int k) { return a.fsTab + ((long long)a.r * a.K + k) * DANSE_FS_FIELDS; }
@@ -283,9 +286,10 @@ __global__ void __launch_bounds__(256) fs_ir_kernel(const FsArgs a) {
 // d_classes.py:1185-1224): one workgroup per (scene, owned node).
 __global__ void __launch_bounds__(tzc::kThr) fs_chunk_kernel(const FsArgs a) {
   __shared__ tzc::ConvLds sm;
-  const int nOwn = a.k1 - a.k0;
-  const int s = blockIdx.x / nOwn;
-  const int k = a.k0 + blockIdx.x % nOwn;
+  const int nGrid = a.foreign ? a.K : a.k1 - a.k0;
+  const int s = blockIdx.x / nGrid;
+  const int k = (a.foreign ? 0 : a.k0) + blockIdx.x % nGrid;
+  const bool owned = k >= a.k0 && k < a.k1;
   const int* e = fs_entry(a, k);
   const int L = e[DANSE_FS_LEN];
   if (L <= 0) return;   // uniform per workgroup
@@ -295,6 +299,7 @@ __global__ void __launch_bounds__(tzc::kThr) fs_chunk_kernel(const FsArgs a) {
   const float* ir = a.wIR + ((long long)s * a.K + k) * a.Mmax * tzc::kA;
   float* z = a.zStream + ((long long)s * a.K + k) * a.zLen + e[DANSE_FS_POS];
   const int T = a.T, N = a.N;
+  if (owned)   // (block-uniform)
   tzc::conv_block(
       sm, Mk, L,
       [&](int q, int m) {   // local_chunk_for_broadcast: y[end - N + q] (clamped read), zero before sample 0
@@ -481,6 +486,8 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
   eng->S = c->S; eng->K = c->K; eng->N = c->N; eng->Ns = c->Ns; eng->F = c->N / 2 + 1; eng->T = c->T;
   eng->R = c->R; eng->k0 = c->k0; eng->k1 = c->k1; eng->gevd = c->gevd; eng->rank = c->rank; eng->ref = c->ref;
   eng->families = c->families | 1; eng->keepHistory = c->keepHistory; eng->alphaExt = c->alphaExt;
+  eng->foreign = (c->k0 != 0 || c->k1 != c->K) &&
+                 (eng->families & ((1 << DANSE_FAM_CENTR) | (1 << DANSE_FAM_SSBC))) ? 1 : 0;
   const int K = c->K, S = c->S, F = eng->F, R = c->R;
   eng->M.assign(c->M, c->M + K);
   for (int k = 0; k < K; ++k) eng->Mmax = std::max(eng->Mmax, eng->M[k]);
@@ -1015,6 +1022,7 @@ static BcastArgs make_bcast(danse_engine* e, int r, int synth, int bc) {
   a.cEnd = e->dCEnd; a.Cspec = e->Cspec; a.rawStream = e->rawStream; a.zChunk = e->zChunk;
   a.zMask = ~0u;
   a.zOnly = 0;
+  a.foreign = e->foreign;
   return a;
 }
 
@@ -1197,17 +1205,19 @@ static void launch_fs(danse_engine* e, int row, hipStream_t st) {
   a.wExtHist = e->wExtHist; a.wExtNodeOff = e->dWExtNodeOff; a.wExtStride = e->wExtStride;
   a.tw = e->dTw + e->N; a.sn = e->dSn; a.wIR = e->wIR; a.zStream = e->zStream; a.rawStream = e->rawStream;
   const int nOwn = e->k1 - e->k0;
+  a.foreign = (e->foreign && e->rawStream) ? 1 : 0;
   bool refresh = false, chunk = false;
-  for (int k = e->k0; k < e->k1; ++k) {
+  for (int k = 0; k < e->K; ++k) {
     const int* t = &e->fsEv[((size_t)row * e->K + k) * DANSE_FS_FIELDS];
-    refresh = refresh || t[DANSE_FS_IRSRC] >= 0;
-    chunk = chunk || t[DANSE_FS_LEN] > 0;
+    const bool own = k >= e->k0 && k < e->k1;
+    refresh = refresh || (own && t[DANSE_FS_IRSRC] >= 0);
+    chunk = chunk || ((own || a.foreign) && t[DANSE_FS_LEN] > 0);
   }
   if (refresh) {
     const unsigned items = (unsigned)(e->S * nOwn * e->Mmax);
     hipLaunchKernelGGL(fs_ir_kernel, dim3((items + 3) / 4), dim3(256), 0, st, a);
   }
-  if (chunk) hipLaunchKernelGGL(fs_chunk_kernel, dim3(e->S * nOwn), dim3(tzc::kThr), 0, st, a);
+  if (chunk) hipLaunchKernelGGL(fs_chunk_kernel, dim3(e->S * (a.foreign ? e->K : nOwn)), dim3(tzc::kThr), 0, st, a);
 }
 
 // zMask: fewSamples senders whose z frame this launch analyses; zOnly: that
@@ -1219,7 +1229,7 @@ static void launch_bcast(danse_engine* e, int r, int synth, int bc, hipStream_t 
   BcastArgs a = make_bcast(e, r, synth, bc);
   a.zMask = zMask;
   a.zOnly = zOnly;
-  const unsigned grid = (unsigned)(e->S * (e->k1 - e->k0));
+  const unsigned grid = (unsigned)(e->S * (e->foreign ? e->K : e->k1 - e->k0));
   if (bcast_waves(e->S, e->K) == 8) hipLaunchKernelGGL(bcast_kernel<8>, dim3(grid), dim3(512), 0, st, a);
   else hipLaunchKernelGGL(bcast_kernel<4>, dim3(grid), dim3(256), 0, st, a);
 }

@@ -48,7 +48,9 @@ class ShardedRun:
 
     Per round r: ``bcast(r)`` for the owned nodes, the in-place all-gather of
     the fused spectra, the start gate of round r for the owned nodes, then
-    ``update(r)``.
+    ``update(r)`` -- or, for a fewSamples round whose updates run as several
+    node-subset steps (``update_segments(r)`` > 1), ``update(r, j)`` per
+    segment with one more all-gather before each segment after the first.
 
     The reference's start gate (``check_covariance_matrices``,
     ``d_classes.py:1430-1540``) decides when each node starts updating from
@@ -139,8 +141,33 @@ class ShardedRun:
             self.exchange(r)
             if gate:
                 e.gate_launch(r)
-            e.update(r)
+            self._update(r)
         e.finish()
+
+    def _nseg(self, r):
+        f = getattr(self.eng, 'update_segments', None)
+        return 1 if f is None else f(r)
+
+    def _update(self, r, pending=None):
+        """The update phase of round r: one call, or (a fewSamples round
+        whose updates run as several node-subset steps) one segment per
+        update step with an exchange before every segment after the first
+        (its senders' late z frames were analysed in the previous one); the
+        exact gate decides each segment's nodes right before it."""
+        e = self.eng
+        n = self._nseg(r)
+        for j in range(n):
+            if j:
+                self.exchange(r)
+            if pending is not None and pending and min(pending.values()) == r:
+                if n == 1:
+                    e.gate_decide(r, pending)
+                else:
+                    e.gate_decide(r, pending, nodes=e.segment_nodes(r, j))
+            if n == 1:
+                e.update(r)
+            else:
+                e.update(r, j)
 
     def _sequence(self, reset, gate):
         """The round sequence, eagerly or as a replayed CUDA graph (captured
@@ -208,9 +235,7 @@ class ShardedRun:
         for r in range(e.R):
             e.bcast(r)
             self.exchange(r)
-            if pending and min(pending.values()) == r:
-                e.gate_decide(r, pending)
-            e.update(r)
+            self._update(r, pending)
         e.finish()
         return self
 
@@ -255,8 +280,14 @@ class ShardedEngine:
     def bcast(self, r):
         self.e.bcast(r)
 
-    def update(self, r):
-        self.e.update(r)
+    def update(self, r, seg=None):
+        self.e.update(r, seg)
+
+    def update_segments(self, r):
+        return self.e.update_segments(r)
+
+    def segment_nodes(self, r, seg):
+        return self.e.segment_nodes(r, seg)
 
     def finish(self):
         self.e.finish()
@@ -289,5 +320,5 @@ class ShardedEngine:
     def gate_pending(self):
         return self.e.gate_pending()
 
-    def gate_decide(self, r, pending):
-        self.e.gate_decide(r, pending)
+    def gate_decide(self, r, pending, nodes=None):
+        self.e.gate_decide(r, pending, nodes=nodes)

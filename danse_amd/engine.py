@@ -178,16 +178,12 @@ class DanseEngine:
         else:
             self.rt = compile_rounds(events, fs, p, K)
         self.R = R = self.rt.nRounds
-        if self.fewSamples and (self.k0, self.k1) != (0, K) and any(self._split_round(r) for r in range(R)):
-            # a node-subset update step inside a round would need its own
-            # exchange of the late chunk's z frame between the ranks
-            raise NotImplementedError('node-sharded fewSamples engines: rounds whose updates run in several steps '
-                                      '(SRO clocks with L < Ns drift)')
-        if (self.k0, self.k1) != (0, K) and (p.computeCentralised or p.computeSingleSensorBroadcast):
-            # the centralised / SSBC observation vectors read every node's raw
-            # local spectra and the centralised VAD averages every node's VAD;
-            # a node-sharded engine only analyses (and only has) its own nodes
-            raise NotImplementedError('centralised / single-sensor-broadcast estimates on a node-sharded engine')
+        # (node-sharded engines: a fewSamples round whose updates run as
+        # several node-subset steps is driven segment by segment, one exchange
+        # of the late z frames before each (update_segments / update(r, seg));
+        # with centralised / SSBC families the broadcast phase also analyses
+        # the raw local frames of the nodes the engine does not own, which
+        # their observation vectors read (BcastArgs.foreign))
         if p.computeSingleSensorBroadcast and p.compensateSROs:
             # compensate_sros raises here too (d_classes.py:2042-2044)
             raise NotImplementedError('SRO compensation for single-sensor broadcast not implemented yet.')
@@ -862,14 +858,42 @@ class DanseEngine:
     def gate_pending(self):
         return self._gate_pending()
 
-    def gate_decide(self, r, pending, stream=None):
-        self._gate_decide(r, pending, self.stream_ptr(stream))
+    def gate_decide(self, r, pending, stream=None, nodes=None):
+        self._gate_decide(r, pending, self.stream_ptr(stream), nodes=nodes)
 
     def bcast(self, r, stream=None):
         L.check(self.lib.danse_engine_bcast(self.eng, r, self.stream_ptr(stream)), self.eng)
 
-    def update(self, r, stream=None):
-        L.check(self.lib.danse_engine_update(self.eng, r, self.stream_ptr(stream)), self.eng)
+    def update(self, r, seg=None, stream=None):
+        """The update phase of round r, or its segment ``seg`` (see
+        ``update_segments``)."""
+        if seg is None:
+            L.check(self.lib.danse_engine_update(self.eng, r, self.stream_ptr(stream)), self.eng)
+            return
+        s0, s1, _ = self._segments(r)[seg]
+        L.check(self.lib.danse_engine_run_steps(self.eng, s0, s1, self.stream_ptr(stream)), self.eng)
+
+    def _segments(self, r):
+        """fewSamples: the update phase of round r cut before each UPDATE
+        step, [(first step, end step, node set)]."""
+        rs = self.rt.fsRoundStep
+        ups = [i for i in range(int(rs[r]), int(rs[r + 1])) if int(self.rt.fsSteps[i, 0]) == FS_STEP_UPDATE]
+        ends = ups[1:] + [int(rs[r + 1])]
+        return [(u, e, {k for k in range(self.K) if (int(self.rt.fsSteps[u, 2]) >> k) & 1})
+                for u, e in zip(ups, ends)]
+
+    def update_segments(self, r):
+        """Number of update segments of round r: 1, or (a fewSamples round
+        whose updates run as several node-subset steps) one per UPDATE step,
+        each needing the z frames analysed after the previous one -- a
+        node-sharded run exchanges the fused spectra before each segment."""
+        return len(self._segments(r)) if self._split_round(r) else 1
+
+    def segment_nodes(self, r, seg):
+        """The nodes updated by segment ``seg`` of round r."""
+        if not self._split_round(r):
+            return set(range(self.K))
+        return self._segments(r)[seg][2]
 
     def finish(self, stream=None):
         L.check(self.lib.danse_engine_finish(self.eng, self.stream_ptr(stream)), self.eng)

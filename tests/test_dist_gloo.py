@@ -149,3 +149,83 @@ def test_subgroup_runs_and_control_groups():
             for s in range(ref.S):
                 for k in range(ref.K):
                     assert np.array_equal(np.load(Path(td) / f'd_{g}_{s}_{k}.npy'), ref.st[s][k]['d']), (g, s, k)
+
+
+class _SegEngine:
+    """Protocol stand-in for fewSamples rounds whose updates run as several
+    node-subset steps (DanseEngine.update_segments): on odd rounds the first
+    half of the nodes updates first and each of them then writes a late z
+    value (the late chunk's z frame), which the second half's update must
+    read -- on another rank only if ShardedRun exchanges before segment 1."""
+    R, K = 6, 4
+
+    def __init__(self, k0, k1):
+        self.k0, self.k1 = k0, k1
+        self.zspec_slots = 1
+        self.torch_device = 'cpu'
+
+    def zspec_numel(self):
+        return self.K
+
+    def set_zspec(self, t):
+        self.z = t
+
+    def reset(self):
+        self.seen = {}
+
+    def bcast(self, r):
+        for k in range(self.k0, self.k1):
+            self.z[k] = 100.0 * r + k
+
+    def update_segments(self, r):
+        return 2 if r % 2 else 1
+
+    def segment_nodes(self, r, j):
+        h = self.K // 2
+        return set(range(h)) if j == 0 else set(range(h, self.K))
+
+    def update(self, r, seg=None):
+        nodes = set(range(self.K)) if seg is None else self.segment_nodes(r, seg)
+        for k in sorted(nodes & set(range(self.k0, self.k1))):
+            self.seen[(r, k)] = self.z.clone().numpy()
+        if seg == 0:
+            for k in sorted(nodes & set(range(self.k0, self.k1))):
+                self.z[k] = 100.0 * r + k + 0.5
+
+    def finish(self):
+        pass
+
+
+def _worker_segments(rank, world, port, outdir):
+    sys.path.insert(0, str(ROOT))
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from danse_amd.dist import ShardedRun, node_range
+    k0, k1 = node_range(_SegEngine.K, world, rank)
+    eng = _SegEngine(k0, k1)
+    ShardedRun(eng).run()
+    for (r, k), v in eng.seen.items():
+        np.save(Path(outdir) / f'seen_{r}_{k}.npy', v)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_split_round_segments_exchange_late_z():
+    """Node-sharded split rounds (fewSamples, SRO clocks with L < Ns): the
+    nodes of a later update segment see the late z values the earlier
+    segment's nodes wrote on the other rank, as in the single-process run."""
+    ref = _SegEngine(0, _SegEngine.K)
+    ref.set_zspec(torch.zeros(ref.zspec_numel()))
+    ref.reset()
+    for r in range(ref.R):
+        ref.bcast(r)
+        n = ref.update_segments(r)
+        for j in range(n):
+            ref.update(r, j if n > 1 else None)
+    assert np.array_equal(ref.seen[(1, 3)], [100.5, 101.5, 102, 103])
+    with tempfile.TemporaryDirectory() as td:
+        port = 29500 + (os.getpid() % 1000) + 43
+        mp.spawn(_worker_segments, args=(2, port, td), nprocs=2, join=True)
+        for (r, k), v in ref.seen.items():
+            assert np.array_equal(np.load(Path(td) / f'seen_{r}_{k}.npy'), v), (r, k)

@@ -9,6 +9,8 @@
     verdicts are all-reduced and every rank repeats the run exactly;
   - CohDrift SRO estimation on a sharded engine (each rank estimates for its
     own receivers from the all-gathered fused spectra);
+  - fewSamples rounds split into node-subset update steps (one more
+    all-gather per extra step) with centralised / SSBC estimates;
 * world size 1 over RCCL: the round sequence (bcast, the in-place RCCL
   all-gather of the fused spectra -- an identity at one rank, but a real
   collective in the graph --, gate, update) captured into a CUDA graph and
@@ -44,6 +46,13 @@ CASES = {
     'dxcp_k4': dict(name='dxcp_k4', M=[2, 2, 2, 2], dur=7.0, seed=16, sros=[0, 60, 120, 180],
                     danse=_d(BATTERY, nodeUpdating='asy', compensateSROs=True, includeFSDflags=True,
                              estimateSROs='DXCPPhaT')),
+    # fewSamples with split rounds (L = 8 at 200 ppm: round 94's updates run
+    # as two node-subset steps, one more all-gather between them) and the
+    # centralised / SSBC families (each rank analyses the other's raw frames)
+    'fs_split_centr_k2': dict(name='fs_split_centr_k2', M=[2, 3], dur=4.0, seed=0, sros=[0.0, 200.0],
+                              danse=_d(BATTERY, nodeUpdating='asy', broadcastType='fewSamples', broadcastLength=8,
+                                       computeCentralised=True, computeSingleSensorBroadcast=True,
+                                       compensateSROs=False)),
 }
 
 
@@ -61,6 +70,9 @@ def _save(dv, k0, k1, outdir, tag):
         np.save(Path(outdir) / f'{tag}_w_{k}.npy', dv.wTilde[k])
         np.save(Path(outdir) / f'{tag}_e_{k}.npy', dv.wTildeExt[k])
         np.save(Path(outdir) / f'{tag}_s_{k}.npy', np.asarray(dv.startRound[k]))
+        for nm in ('dCentr', 'dSSBC'):
+            if getattr(dv, nm, None) is not None:
+                np.save(Path(outdir) / f'{tag}_{nm}_{k}.npy', getattr(dv, nm)[:, k])
         if getattr(dv, 'SROsEstimates', None) is not None:
             np.save(Path(outdir) / f'{tag}_sro_{k}.npy', np.asarray(dv.SROsEstimates[k]))
 
@@ -124,12 +136,16 @@ def _compare(ref, td, K, passes):
             assert np.array_equal(np.load(td / f'p{i}_w_{k}.npy'), ref.wTilde[k]), (i, k)
             assert np.array_equal(np.load(td / f'p{i}_e_{k}.npy'), ref.wTildeExt[k]), (i, k)
             assert int(np.load(td / f'p{i}_s_{k}.npy')) == int(ref.startRound[k]), (i, k)
+            for nm in ('dCentr', 'dSSBC'):
+                f = td / f'p{i}_{nm}_{k}.npy'
+                if getattr(ref, nm, None) is not None:
+                    assert np.array_equal(np.load(f), getattr(ref, nm)[:, k]), (i, nm, k)
             f = td / f'p{i}_sro_{k}.npy'
             if f.exists() and getattr(ref, 'SROsEstimates', None) is not None:
                 assert np.array_equal(np.load(f), np.asarray(ref.SROsEstimates[k])), (i, k)
 
 
-@pytest.mark.parametrize('name', ['gate_delay_k4', 'cohdrift_k4', 'dxcp_k4'])
+@pytest.mark.parametrize('name', ['gate_delay_k4', 'cohdrift_k4', 'dxcp_k4', 'fs_split_centr_k2'])
 def test_sharded_processes_match_single_engine(name):
     ref, td = _spawn(name, 2, 'gloo', 2)
     K = len(CASES[name]['M'])

@@ -146,15 +146,29 @@ def test_keep_history_false_matches(name):
             assert np.array_equal(getattr(full, nm), getattr(ring, nm)), nm
 
 
-@pytest.mark.parametrize('name', ['online_B_k4m3_asy', 'online_C_sro_noflags_seq', 'online_E_fs_L128_sro_comp'])
+# a fewSamples run with split rounds (L = 8 < 32 at 200 ppm: round 94's
+# updates run as two node-subset steps), centralised and SSBC families on
+SPLIT_FS_CASE = dict(name='online_E_fs_L8_split_centr', M=[2, 3], dur=4.0, seed=0, sros=[0.0, 200.0],
+                     danse=dict(BATTERY, nodeUpdating='asy', broadcastType='fewSamples', broadcastLength=8,
+                                computeCentralised=True, computeSingleSensorBroadcast=True, compensateSROs=False))
+SHARDED_CASES = ['online_B_k4m3_asy', 'online_C_sro_noflags_seq', 'online_E_fs_L128_sro_comp',
+                 # centralised / SSBC on node-sharded engines (the foreign analyses):
+                 # synchronous, asynchronous raw frames (cEnd), fewSamples raw streams
+                 'online_ragged_asy_r2', 'online_C_sro_ssbc_nocomp_asy', 'online_C_sro_centr_asy',
+                 'online_E_fs_L64_sro_nocomp', SPLIT_FS_CASE]
+
+
+@pytest.mark.parametrize('name', SHARDED_CASES, ids=lambda c: c if isinstance(c, str) else c['name'])
 def test_sharded_engines_match_unsharded(name):
     """Two engines with nodeRange halves on one device, one shared fused
     spectra buffer (the all-gather's destination), bcast of both before the
-    update of both each round, as ``danse_amd.dist.ShardedRun`` does."""
+    update of both each round (per update segment in split fewSamples
+    rounds), as ``danse_amd.dist.ShardedRun`` does."""
     from danse_amd.core import danse_multi
     from danse_amd.engine import DanseEngine
     from danse_amd.dist import ShardedEngine
-    case = _case(name)
+    case = name if isinstance(name, dict) else _case(name)
+    name = case['name']
     sc, dp, wp = _scene_params(case)
     ref = danse_multi([sc], dp)[0]
     K = len(case['M'])
@@ -166,22 +180,29 @@ def test_sharded_engines_match_unsharded(name):
         a.set_zspec(zbuf)
         a.reset()
     R = engs[0].R
+    nSplit = 0
     for r in range(R):
         for a in ad:
             a.bcast(r)
-        for a in ad:
-            a.update(r)
+        n = ad[0].update_segments(r)
+        nSplit += n > 1
+        for j in range(n):
+            for a in ad:
+                a.update(r, j if n > 1 else None)
     for a in ad:
         a.finish()
     torch.cuda.synchronize()
+    if name == SPLIT_FS_CASE['name']:
+        assert nSplit >= 1
     outs = [e.outputs()[0] for e in engs]
     for i, (e, o) in enumerate(zip(engs, outs)):
         for k in range(e.k0, e.k1):
             assert np.array_equal(o.d[:, k], ref.d[:, k]), (name, k)
             assert np.array_equal(o.wTilde[k], ref.wTilde[k]), (name, k)
             assert np.array_equal(o.wTildeExt[k], ref.wTildeExt[k]), (name, k)
-            if hasattr(ref, 'dLocal'):
-                assert np.array_equal(o.dLocal[:, k], ref.dLocal[:, k]), (name, k)
+            for nm in ('dLocal', 'dCentr', 'dSSBC'):
+                if hasattr(ref, nm):
+                    assert np.array_equal(getattr(o, nm)[:, k], getattr(ref, nm)[:, k]), (name, nm, k)
         e.close()
 
 
