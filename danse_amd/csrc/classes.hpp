@@ -36,6 +36,7 @@ constexpr bool class_packed(int D) { return D <= kLaneMaxD; }
 #define DANSE_DECLARE_CLASS(N)                                                                      \
   void launch_update_d##N(const UpdateArgs& a, hipStream_t st);                                     \
   bool launch_split_solve_d##N(const UpdateArgs& a, int nItems, hipStream_t st);                    \
+  bool launch_lean_solve_d##N(const UpdateArgs& a, int nItems, int fbGrid, hipStream_t st);         \
   void launch_filter_update_d##N(const cd* Ryy, const cd* Rnn, int B, int D, int gevd, int rank,   \
                                  int ref, cf* w, int* diag, hipStream_t st);
 DANSE_FOR_EACH_CLASS(DANSE_DECLARE_CLASS)
@@ -55,6 +56,18 @@ inline bool launch_split_solve_class(int DMAX, const UpdateArgs& a, int nItems, 
   switch (DMAX) {
 #define DANSE_CASE(N) \
   case N: return launch_split_solve_d##N(a, nItems, st);
+    DANSE_FOR_EACH_CLASS(DANSE_CASE)
+#undef DANSE_CASE
+    default: return false;
+  }
+}
+// the solves on the cached factor and C of an 8 x 8 grid class
+// (kernels_2dc.hpp): update_kernel_2dc over nItems items, then
+// fallback_kernel_2d (fbGrid workgroups) over the bins it sent back
+inline bool launch_lean_solve_class(int DMAX, const UpdateArgs& a, int nItems, int fbGrid, hipStream_t st) {
+  switch (DMAX) {
+#define DANSE_CASE(N) \
+  case N: return launch_lean_solve_d##N(a, nItems, fbGrid, st);
     DANSE_FOR_EACH_CLASS(DANSE_CASE)
 #undef DANSE_CASE
     default: return false;

@@ -41,7 +41,14 @@ struct Class {
   std::vector<int> solveCount;
   // per round: does any item of the class solve (else the recursion-only
   // kernel variant runs)
-  std::vector<uint8_t> anySolve;
+  std::vector<uint8_t> anySolve;  // solves on the cached factor and C (kernels_2dc.hpp): per round the
+  // items for update_kernel_2dc, [R][S * nFN] (the first creCount[r] of a row
+  // used), and the fallback list / per-round counters
+  bool lean = false;
+  int* dCreItems = nullptr;
+  std::vector<int> creCount;
+  int* dFbList = nullptr;
+  int* dFbCount = nullptr;
 };
 
 template <typename T>
@@ -108,6 +115,8 @@ struct danse_engine {
   long long vStride = 0;
   cd* l64Cache = nullptr;    // lane-grid GEVD classes: float64 factor record per bin (rank-one updates)
   long long l64Stride = 0;
+  cf* cCache = nullptr;      // 8 x 8 grid GEVD classes: C = Li Ryy Li^H per bin (UpdateArgs.cCache)
+  long long cStride = 0;
   int* lzStats = nullptr;    // [R][2] warm Lanczos solves accepted / sent back (danse_engine_lanczos_stats)
   // the online centralised family above 64 channels (wide_online.hpp)
   std::vector<int> wideIds;          // family-node indices
@@ -455,6 +464,32 @@ static int build_split_lists(danse_engine* eng, const uint8_t* flags) {
         const uint8_t fl = flags[(((size_t)r * S + t / nn) * kMaxFam + d.fam) * K + d.k];
         if ((fl & DANSE_FLAG_SOLVE) && !(fl & DANSE_FLAG_PREGIVEN)) cl.anySolve[r] = 1;
       }
+    if (cl.lean) {
+      // (the host mirror of the kernels' reuse tests: kernels.hpp li_reusable
+      // and c_reusable -- a solve, no Rnn update this round, and a solve of
+      // this item since the last SCM update within kLiScan rounds)
+      auto flag = [&](int r, int t) {
+        const FamNode& d = cl.host[t % nn];
+        return flags[(((size_t)r * S + t / nn) * kMaxFam + d.fam) * K + d.k];
+      };
+      std::vector<int> items((size_t)R * S * nn, 0);
+      cl.creCount.assign(R, 0);
+      for (int r = 0; r < R; ++r)
+        for (int t = 0; t < S * nn; ++t) {
+          const uint8_t fl = flag(r, t);
+          if (!(fl & DANSE_FLAG_SOLVE) || (fl & DANSE_FLAG_PREGIVEN) || ((fl >> 2) & 3) != DANSE_OP_KEEP) continue;
+          if (cl.host[t % nn].cOff < 0) continue;
+          bool ok = false;
+          for (int rr = r - 1; rr >= 0 && rr >= r - kLiScan; --rr) {
+            const uint8_t f2 = flag(rr, t);
+            if ((f2 & DANSE_FLAG_SOLVE) && !(f2 & DANSE_FLAG_PREGIVEN)) { ok = true; break; }
+            if (f2 & 15) break;
+          }
+          if (ok) items[(size_t)r * S * nn + cl.creCount[r]++] = t;
+        }
+      if (!cl.dCreItems) HIPCHK(dalloc(&cl.dCreItems, items.size()));
+      HIPCHK(hipMemcpy(cl.dCreItems, items.data(), items.size() * sizeof(int), hipMemcpyHostToDevice));
+    }
     if (!cl.split) continue;
     const int n = (int)cl.host.size();
     std::vector<int> items((size_t)R * S * n, 0);
@@ -574,7 +609,7 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
   // ---- family-node table (owned nodes), channel lists; with cEnd the other
   // nodes' channels of the centralised / SSBC vectors are raw-frame codes
   // (MT + K + channel, kernels.hpp load_y)
-  long long scmOff = 0, wOff = 0, liOff = 0, vOff = 0, l64Off = 0;
+  long long scmOff = 0, wOff = 0, liOff = 0, vOff = 0, l64Off = 0, cOff = 0;
   // warm-started rank-1 Lanczos on the lane-grid classes (DANSE_NO_WARM=1: off)
   const bool warm = c->gevd && c->rank == 1 && !std::getenv("DANSE_NO_WARM");
   const int rawBase = mt + K;
@@ -647,6 +682,14 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
         fn.vOff = vOff;
         vOff += (long long)F * class_dmax(fn.D);
       }
+      // C = Li Ryy Li^H per bin (kernels_2d.hpp): the 8 x 8 grid classes with
+      // the warm start and the float64 factor record (DANSE_NO_CCACHE=1: off)
+      fn.cOff = -1;
+      if (fn.vOff >= 0 && fn.l64Off >= 0 && class_grid(class_dmax(fn.D)) == 8 && !std::getenv("DANSE_NO_CCACHE")) {
+        const long long nb = class_dmax(fn.D) / 8;
+        fn.cOff = cOff;
+        cOff += (long long)F * nb * nb * 64;
+      }
       eng->fns.push_back(fn);
     }
   }
@@ -655,6 +698,7 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
   eng->liStride = liOff;
   eng->vStride = vOff;
   eng->l64Stride = l64Off;
+  eng->cStride = cOff;
   eng->wExtNodeOff.assign(K, 0);
   long long eo = 0, to = 0;
   for (int k = 0; k < K; ++k) {
@@ -759,6 +803,21 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
     const char* sp = std::getenv("DANSE_LANE_SPLIT");
     const bool on = c->gevd && (sp && std::atoi(sp) != 0);
     for (auto& cl : eng->classes) cl.split = on && class_split(cl.DMAX) && (cl.G == 1 || cl.DMAX > kLaneMaxD);
+    // the lean solves of the 8 x 8 grid classes with the C cache (not with
+    // split solves, whose solving items run on the SM = 2 variant)
+    for (auto& cl : eng->classes) {
+      cl.lean = !cl.split && eng->cStride > 0 && eng->liStride > 0 && class_grid(cl.DMAX) == 8 && !std::getenv("DANSE_NO_LEAN");
+      if (cl.lean) {
+        bool any = false;
+        for (const auto& fn : cl.host) any = any || fn.cOff >= 0;
+        cl.lean = any;
+      }
+      if (cl.lean) {
+        HIPCHK(dalloc(&cl.dFbList, (size_t)S * cl.host.size() * F));
+        HIPCHK(dalloc(&cl.dFbCount, (size_t)R));
+        HIPCHK(hipMemset(cl.dFbCount, 0, (size_t)R * sizeof(int)));
+      }
+    }
     if (int rc = build_split_lists(eng, c->flags)) return rc;
   }
   if (!eng->wideIds.empty()) {
@@ -858,6 +917,7 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
     HIPCHK(hipMemset(eng->resTrace, 0, eng->resTraceBytes));
   }
   if (eng->l64Stride > 0) HIPCHK(dalloc(&eng->l64Cache, (size_t)S * eng->l64Stride));
+  if (eng->cStride > 0) HIPCHK(dalloc(&eng->cCache, (size_t)S * eng->cStride));
   if (c->dxcp) {
     if (c->cohDrift) return fail(eng, "DXCP-PhaT and CohDrift estimation are exclusive");
     if (c->fsTab) return fail(eng, "DXCP-PhaT estimation runs on wholeChunk broadcasts");
@@ -989,7 +1049,7 @@ void danse_engine_destroy(danse_engine* eng) {
                   eng->resUFlag, eng->resZFlag, eng->resGateRound, eng->resDanseFni, eng->resErr, eng->resFams,
                   eng->resFrames, eng->resChanNode, eng->resTrace, eng->condHist, eng->dxRecFrames,
                   eng->dxRecOut, eng->dFsEv, eng->rawStream, eng->vCache, eng->l64Cache, eng->lzStats,
-                  eng->dWideIds, eng->wideWork, eng->convIR, eng->dSnConv};
+                  eng->dWideIds, eng->wideWork, eng->convIR, eng->dSnConv, eng->cCache};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (eng->dx) danse_dxcp_destroy(eng->dx);
@@ -997,6 +1057,9 @@ void danse_engine_destroy(danse_engine* eng) {
     if (cl.dev) (void)hipFree(cl.dev);
     if (cl.devIds) (void)hipFree(cl.devIds);
     if (cl.dSolveItems) (void)hipFree(cl.dSolveItems);
+    if (cl.dCreItems) (void)hipFree(cl.dCreItems);
+    if (cl.dFbList) (void)hipFree(cl.dFbList);
+    if (cl.dFbCount) (void)hipFree(cl.dFbCount);
   }
   delete eng;
 }
@@ -1039,6 +1102,7 @@ static UpdateArgs make_update(danse_engine* e, int r) {
   a.liCache = e->liCache; a.liStride = e->liStride;
   a.vCache = e->vCache; a.vStride = e->vStride;
   a.l64Cache = e->l64Cache; a.l64Stride = e->l64Stride;
+  a.cCache = e->cCache; a.cStride = e->cStride;
   a.lzStats = e->lzStats;
   a.cdPhase = e->cdPhase;
   a.Cspec = e->Cspec; a.chanNode = e->dChanNode; a.cPhase = e->dCPhase;
@@ -1148,7 +1212,21 @@ static void launch_update(danse_engine* e, int r, hipStream_t st, unsigned mask 
     a.splitSolve = cl.split ? 1 : 0;
     a.noSolve = (!e->noRO && (int)cl.anySolve.size() > r && !cl.anySolve[r]) ? 1 : 0;
     if (r == e->updTraceRound) a.stamps = e->resTrace;
-    launch_update_class(cl.DMAX, a, st);   // D > kMaxDMax rejected at create time
+    // the solves on the cached factor and C: update_kernel_2dc (whole-round
+    // launches only; the fewSamples node-subset steps keep one kernel)
+    const int nItems = e->S * (int)cl.host.size();
+    const int nCre = (cl.lean && mask == ~0u && (int)cl.creCount.size() > r) ? cl.creCount[r] : 0;
+    if (nCre > 0) {
+      a.leanOn = 1;
+      a.creItems = cl.dCreItems + (size_t)r * nItems;
+      a.fbList = cl.dFbList;
+      a.fbCount = cl.dFbCount;
+    }
+    if (nCre < nItems) launch_update_class(cl.DMAX, a, st);   // D > kMaxDMax rejected at create time
+    if (nCre > 0) {
+      (void)fill_async(cl.dFbCount + r, 0, sizeof(int), st);
+      launch_lean_solve_class(cl.DMAX, a, nCre, std::min(nCre * e->F, 256), st);
+    }
     if (cl.split && cl.solveCount[r] > 0) {
       a.solveItems = cl.dSolveItems + (size_t)r * e->S * cl.host.size();
       launch_split_solve_class(cl.DMAX, a, cl.solveCount[r], st);

@@ -41,6 +41,7 @@ struct FamNode {
   long long liOff;    // lane classes, GEVD: offset of the factor cache (Li, g) within one scene's block
   long long vOff;     // lane-grid classes, GEVD: offset of the eigenvector cache (solver2d.hpp lanczos2d), -1 none
   long long l64Off;   // lane-grid classes, GEVD: offset of the float64 factor record (solver2d.hpp li_rank1_2d), -1 none
+  long long cOff;     // one-bin-per-wave grid classes, GEVD: offset of the C = Li Ryy Li^H cache (kernels_2d.hpp), -1 none
 };
 
 struct UpdateArgs {
@@ -114,6 +115,20 @@ struct UpdateArgs {
   // accepted and those sent back to the Householder path (diagnostics; the
   // host sums the slots)
   int* lzStats;
+  // one-bin-per-wave lane-grid GEVD classes: per bin C = Li Ryy Li^H of the
+  // last solve in the lane-grid block layout ([F][NB * NB][64] per
+  // family-node at FamNode.cOff, per scene stride cStride): a solve on the
+  // cached factor updates it by rank one (c_reusable) instead of the O(D^3)
+  // congruence; null = off
+  cf* cCache;
+  long long cStride;
+  // the solves on the cached factor and C run on update_kernel_2dc this round
+  // (items listed in creItems, their failed warm solves in fbList / fbCount
+  // for fallback_kernel_2d): update_kernel_2d skips them
+  int leanOn;
+  const int* creItems;     // this round's items (s * nFN + fni) for update_kernel_2dc
+  int* fbList;             // failed warm solves (item * F + f)
+  int* fbCount;            // their count (one counter per round)
   // DANSE_STAMP builds only (diagnostics): per launch wave, kStampN shader
   // clock marks + a path code (update_kernel_2d), or null
   unsigned long long* stamps;
@@ -195,6 +210,19 @@ DANSE_DEV bool li_updatable(const UpdateArgs& a, const FamNode& d, int s, int op
     const uint8_t f2 = a.flags[(((long long)rr * a.S + s) * kMaxFam + d.fam) * a.K + d.k];
     if ((f2 & DANSE_FLAG_SOLVE) && !(f2 & DANSE_FLAG_PREGIVEN)) return true;
     if (((f2 >> 2) & 3) != DANSE_OP_KEEP) return false;
+  }
+  return false;
+}
+
+// The C = Li Ryy Li^H cached by the last solve of this family-node is C of
+// the current factor and of Ryy before this round's update: the factor is
+// reused (li_reusable) and no round since that solve updated either SCM.
+// This round's Ryy update then moves C by the same rank one, through Li y.
+DANSE_DEV bool c_reusable(const UpdateArgs& a, const FamNode& d, int s) {
+  for (int rr = a.r - 1; rr >= 0 && rr >= a.r - kLiScan; --rr) {
+    const uint8_t f2 = a.flags[(((long long)rr * a.S + s) * kMaxFam + d.fam) * a.K + d.k];
+    if ((f2 & DANSE_FLAG_SOLVE) && !(f2 & DANSE_FLAG_PREGIVEN)) return true;
+    if ((f2 & 15) != 0) return false;   // (opY | opN << 2: an SCM update without a solve)
   }
   return false;
 }

@@ -89,6 +89,11 @@ update_kernel_2d(const UpdateArgs a) {
   cf* vC = (!PK && SM == 0 && a.vCache && d.vOff >= 0)
                ? a.vCache + (long long)s * a.vStride + d.vOff + (long long)f * (G * NB)
                : nullptr;
+  // C = Li Ryy Li^H per bin ([NB * NB][64], this lane layout), stored after
+  // every congruence: the solves on the cached factor and C (kernels.hpp
+  // c_reusable) run on update_kernel_2dc (kernels_2dc.hpp) and skip this one
+  const bool hasC = G == 8 && !PK && SM == 0 && a.cCache && d.cOff >= 0;
+  if (hasC && a.leanOn && reuse && c_reusable(a, d, s)) return;   // wave-uniform
 
   // Loads of the solve on a cached factor (the common solve: a VAD frame,
   // Rnn unchanged since the last factorisation) issued with the observation's:
@@ -286,6 +291,13 @@ update_kernel_2d(const UpdateArgs a) {
     stamp(4);
     if (solve) {
       congruence2d<NB, G>(A, S, li, D);
+      if (hasC && fvalid) {
+        cf* cC = a.cCache + (long long)s * a.cStride + a.fn[fni].cOff + (long long)f * (NB * NB * 64) + li;
+        sfor<0, NB>([&](auto sc) {
+          constexpr int sb = decltype(sc)::value;
+          sfor<0, NB>([&](auto tc) { cC[(sb * NB + decltype(tc)::value) * 64] = A.v[sb][decltype(tc)::value]; });
+        });
+      }
       stamp(5);
       const int path = gevd2d_solve<NB, RMAX, G>(A, S, li, D, a.rank, w, vC, fvalid);
       // (one atomic per wave -- the path is wave-uniform -- into one of

@@ -1,0 +1,283 @@
+// Lean solve kernel of the 8 x 8 lane-grid GEVD classes (rank 1, warm
+// Lanczos): the solves on the cached factor Li and the cached
+// C = Li Ryy Li^H (kernels.hpp c_reusable -- the common solve of a run, a
+// VAD-active frame after a solve on the same factor).  Same arithmetic as the
+// solve path of update_kernel_2d (update_w_gevd, d_classes.py:3343-3387;
+// SCM update d_classes.py:2048-2267; dhat = w^H yhat, d_base.py:2075), but
+// C moves by this round's rank one instead of being recomputed:
+//   Ryy' = by Ryy + cy y y^H  =>  C' = by C + cy (Li y)(Li y)^H,
+// an O(D^2) step in place of the O(D^3) congruence (update_kernel_2d stores C
+// after each of its congruences, so the cache is the exact congruence of the
+// last factorisation, moved by at most the VAD-active frames since).
+//
+// Registers and LDS: no float64 state (the factor is cached), no Householder
+// reflectors (LDS2 allocated up to the Lanczos basis, solver2d.hpp), so the
+// kernel runs at 3 waves per SIMD instead of 2.  A bin whose warm solve the
+// Lanczos acceptance test sends back is listed (fbList) for
+// fallback_kernel_2d, which runs the Householder path on the cached C and
+// writes that bin's filter and estimate: this kernel writes neither for it.
+#pragma once
+#include "kernels_2d.hpp"
+
+#ifndef DANSE_LEAN_RECOMP
+#define DANSE_LEAN_RECOMP 0   // (diagnostics) C by the full congruence
+#endif
+#ifndef DANSE_LEAN_NOUPD
+#define DANSE_LEAN_NOUPD 0    // (diagnostics) no rank-one move of C
+#endif
+#ifndef DANSE_LEAN_DMA
+#define DANSE_LEAN_DMA 1   // the factor record by LDS-DMA (0: through VGPRs, diagnostics)
+#endif
+
+namespace danse {
+
+template <int NB>
+constexpr int lean_lds_bytes() {
+  return (int)__builtin_offsetof(t2d::LDS2<NB>, U) + t2d::kLz<8 * NB>() * 8 * NB * (int)sizeof(cf);
+}
+
+// w[r + 1], its history slot, and the per-bin tail (external filters, dhat)
+template <int NB>
+DANSE_DEV void lean_tail(const UpdateArgs& a, const FamNode& d, int s, int f, int li, uint8_t fl, cf w, cf y) {
+  const int F = a.F, D = d.D, r = a.r;
+  const long long wBase = (long long)s * a.wStride + d.wOff;
+  const int slotNext = a.wHistory ? r + 1 : ((r + 1) & 1);
+  cf* wNext = a.wHist + wBase + ((long long)slotNext * F + f) * D;
+  const bool act = li < D;
+  if (act) wNext[li] = w;
+  const cf dh = gsum<64>(act ? cmul(w, y) : cf{0.0f, 0.0f});
+  node_bin_tail(a, d, s, f, li, fl, false, true, w, y, dh);
+}
+
+template <int NB>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) update_kernel_2dc(const UpdateArgs a) {
+  using namespace t2d;
+  constexpr int G = 8, DM = G * NB;
+  static_assert(vpl<NB, G>() == 1, "one lane-layout entry per lane");
+  __shared__ __attribute__((aligned(16))) char ldsRaw[lean_lds_bytes<NB>()];
+  LDS2<NB, G>& S = *reinterpret_cast<LDS2<NB, G>*>(ldsRaw);   // (members up to the Lanczos basis)
+  const int li = threadIdx.x, p = li / G, q = li % G;
+  const int F = a.F;
+  const int f = blockIdx.x % F;
+  const int tt = a.creItems[blockIdx.x / F];
+  const int fni = tt % a.nFN, s = tt / a.nFN;
+  const FamNode d = a.fn[fni];
+  const int D = d.D, r = a.r;
+  const uint8_t fl = a.flags[(((long long)r * a.S + s) * kMaxFam + d.fam) * a.K + d.k];
+  const int opY = fl & 3;
+  constexpr int kRec = li_record<NB, G>();
+  const cf* liC = a.liCache + (long long)s * a.liStride + d.liOff + (long long)f * kRec;
+  cf* cC = a.cCache + (long long)s * a.cStride + d.cOff + (long long)f * (NB * NB * 64) + li;
+  const long long tri = (long long)s * a.scmStride + d.scmOff + (long long)f * (D * (D + 1) / 2);
+  auto ent = [&](int i, int c) -> long long {
+    const int hi = i >= c ? i : c, lo = i >= c ? c : i;
+    return tri + hi * (hi + 1) / 2 + lo;
+  };
+
+  // the factor record straight into LDS (LDS-DMA, [S.Ls | S.g] is the
+  // record's layout; no VGPR staging), the C block and y
+#if DANSE_LEAN_DMA
+  {
+    constexpr int kChunks = (kRec * (int)sizeof(cf) + 1023) / 1024;   // 16 B per lane per instruction
+    static_assert(kChunks * 1024 <= lean_lds_bytes<NB>() - (int)__builtin_offsetof(LDS2<NB>, Ls),
+                  "the record's last chunk stays inside the lean LDS");
+    sfor<0, kChunks>([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      const int e = 2 * (64 * j + li);   // first record entry of this lane's 16 bytes
+      const cf* src = liC + (e + 1 < kRec ? e : kRec - 2);
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(reinterpret_cast<char*>(S.Ls) + 1024 * j),
+                                       16, 0, 0);
+    });
+  }
+#else
+  {
+    constexpr int kRecL = (kRec + 63) / 64, kNL = DM * (DM + 1) / 2;
+    cf lrec[kRecL];
+    sfor<0, kRecL>([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      const int e = li + 64 * j;
+      lrec[j] = liC[e < kRec ? e : 0];
+    });
+    hold(lrec);
+    sfor<0, kRecL>([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      const int e = li + 64 * j;
+      if (e < kNL) S.Ls[e] = lrec[j];
+      else if (e < kRec) S.g[e - kNL] = lrec[j];
+    });
+  }
+#endif
+  const int ych = chan_of(a, d, li, li < D);
+  Blk<NB> A;
+  sfor<0, NB>([&](auto sc) {
+    constexpr int sb = decltype(sc)::value;
+    sfor<0, NB>([&](auto tc) { A.v[sb][decltype(tc)::value] = cC[(sb * NB + decltype(tc)::value) * 64]; });
+  });
+  const cf y = load_y_c(a, d, s, f, ych, li < D);
+  S.vb[li] = y;
+  __builtin_amdgcn_s_waitcnt(0);   // (the record's LDS-DMA landed)
+  wsync();
+  cf yc[NB];
+  sfor<0, NB>([&](auto sc) { yc[decltype(sc)::value] = S.vb[q + G * decltype(sc)::value]; });
+  wsync();
+
+#if DANSE_LEAN_RECOMP
+  // (diagnostics: C by the full congruence of this round's Ryy)
+  if (true) {
+    const double beta = a.beta[s * a.K + d.k];
+    const float by = (float)beta, cy = (opY == DANSE_OP_SET) ? (float)(1.0 / D) : (float)((1.0 - beta) / D);
+    cf yr2[NB];
+    sfor<0, NB>([&](auto sc) { yr2[decltype(sc)::value] = S.vb[p + G * decltype(sc)::value]; });
+    sfor<0, NB>([&](auto sc) {
+      constexpr int sb = decltype(sc)::value;
+      sfor<0, NB>([&](auto tc) {
+        constexpr int tb = decltype(tc)::value;
+        const int i = p + G * sb, c = q + G * tb;
+        const bool in = i < D && c < D;
+        cf x = in ? a.Ryy[ent(i, c)] : cf{0.0f, 0.0f};
+        if (i < c) x = conjg(x);
+        if (opY) {
+          const cf yy = cy * mulc(yr2[sb], yc[tb]);
+          x = csel(opY == DANSE_OP_SET, yy, by * x + yy);
+          if (i == c) x.im = 0.0f;
+        }
+        A.v[sb][tb] = x;
+      });
+    });
+    wsync();
+    congruence2d<NB, G>(A, S, li, D);
+  }
+  if (false) {
+#else
+  if (opY) {
+#endif
+    const double beta = a.beta[s * a.K + d.k];
+    const float by = (float)beta, cy = (opY == DANSE_OP_SET) ? (float)(1.0 / D) : (float)((1.0 - beta) / D);
+    // u = Li y: partial sums over the row group (row layout: every lane of
+    // row group p holds u[p + G sb]), the column layout through LDS
+    cf ur[NB], uc[NB];
+    sfor<0, NB>([&](auto sc) {
+      constexpr int sb = decltype(sc)::value;
+      cf acc = cf{0.0f, 0.0f};
+      sfor<0, sb + 1>([&](auto tc) {
+        constexpr int tb = decltype(tc)::value;
+        acc = acc + ls_get<DM>(S.Ls, p + G * sb, q + G * tb) * yc[tb];   // (cmul would conjugate Li)
+      });
+      ur[sb] = sumq<G>(acc);
+      if (q == 0) S.vb[p + G * sb] = ur[sb];
+    });
+    wsync();
+    sfor<0, NB>([&](auto tc) { uc[decltype(tc)::value] = S.vb[q + G * decltype(tc)::value]; });
+    wsync();
+    if (!DANSE_LEAN_NOUPD)
+    sfor<0, NB>([&](auto sc) {
+      constexpr int sb = decltype(sc)::value;
+      sfor<0, NB>([&](auto tc) {
+        constexpr int tb = decltype(tc)::value;
+        const cf uu = cy * mulc(ur[sb], uc[tb]);
+        cf x = csel(opY == DANSE_OP_SET, uu, by * A.v[sb][tb] + uu);
+        if (sb == tb && p == q) x.im = 0.0f;
+        A.v[sb][tb] = x;
+        cC[(sb * NB + tb) * 64] = x;
+      });
+    });
+  }
+
+  cf* vC = a.vCache + (long long)s * a.vStride + d.vOff + (long long)f * DM;
+  cf vv[1];
+  float lam1;
+  bool warm;
+  // this round's Ryy recursion (as update_kernel_2d), after the solve: no
+  // register of it is live across the Lanczos phase
+  auto ryy_recursion = [&]() {
+    if (!opY) return;
+    constexpr int kLo = NB * (NB + 1) / 2;
+    cf rlo[kLo];
+    sfor<0, NB>([&](auto sc) {
+      constexpr int sb = decltype(sc)::value;
+      sfor<0, sb + 1>([&](auto tc) {
+        constexpr int tb = decltype(tc)::value;
+        const int i = p + G * sb, c = q + G * tb;
+        const bool lo = i < D && c < D && i >= c;
+        rlo[sb * (sb + 1) / 2 + tb] = a.Ryy[lo ? ent(i, c) : tri];
+      });
+    });
+    wsync();   // (the solve's LDS reads before the staging write)
+    S.vb[li] = y;
+    wsync();
+    cf yr[NB], yq[NB];
+    sfor<0, NB>([&](auto sc) {
+      constexpr int sb = decltype(sc)::value;
+      yr[sb] = S.vb[p + G * sb];
+      yq[sb] = S.vb[q + G * sb];
+    });
+    const double beta = a.beta[s * a.K + d.k];
+    const float by = (float)beta, cy = (opY == DANSE_OP_SET) ? (float)(1.0 / D) : (float)((1.0 - beta) / D);
+    sfor<0, NB>([&](auto sc) {
+      constexpr int sb = decltype(sc)::value;
+      sfor<0, sb + 1>([&](auto tc) {
+        constexpr int tb = decltype(tc)::value;
+        const int i = p + G * sb, c = q + G * tb;
+        const cf yy = cy * mulc(yr[sb], yq[tb]);
+        cf x = csel(opY == DANSE_OP_SET, yy, by * rlo[sb * (sb + 1) / 2 + tb] + yy);
+        if (i == c) x.im = 0.0f;
+        if (i < D && c < D && i >= c) a.Ryy[ent(i, c)] = x;
+      });
+    });
+  };
+  if (!lanczos2d<NB, G>(A, S, li, D, vC, vv, lam1, warm)) {
+    ryy_recursion();
+    // (wave-uniform) the Householder path of fallback_kernel_2d writes this bin
+    if (li == 0) {
+      const int e = atomicAdd(&a.fbCount[r], 1);
+      a.fbList[e] = tt * F + f;
+    }
+    return;
+  }
+  cf w[1];
+  rank1_w2d<NB, G>(S, li, D, vv, lam1, w);
+  if (li < DM) vC[li] = vv[0];
+  if (a.lzStats && li == 0) atomicAdd(&a.lzStats[((long long)(2 * r)) * kLzSlots + (blockIdx.x & (kLzSlots - 1))], 1);
+  lean_tail<NB>(a, d, s, f, li, fl, w[0], y);
+  ryy_recursion();
+}
+
+// The warm solves update_kernel_2dc sent back: the Householder path
+// (tridiagonalisation, eigen part, back-transform; gevd2d_solve path 2) on
+// the C and factor it cached, then the filter and the tail.  A fixed grid
+// strides over this round's list.
+template <int NB>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) fallback_kernel_2d(const UpdateArgs a) {
+  using namespace t2d;
+  constexpr int G = 8, DM = G * NB;
+  __shared__ LDS2<NB, G> S;
+  const int li = threadIdx.x;
+  const int F = a.F, r = a.r;
+  const int n = a.fbCount[r];
+  for (int e = blockIdx.x; e < n; e += gridDim.x) {
+    const int code = a.fbList[e];
+    const int tt = code / F, f = code % F;
+    const int fni = tt % a.nFN, s = tt / a.nFN;
+    const FamNode d = a.fn[fni];
+    const int D = d.D;
+    const uint8_t fl = a.flags[(((long long)r * a.S + s) * kMaxFam + d.fam) * a.K + d.k];
+    const cf* cC = a.cCache + (long long)s * a.cStride + d.cOff + (long long)f * (NB * NB * 64) + li;
+    Blk<NB> A;
+    sfor<0, NB>([&](auto sc) {
+      constexpr int sb = decltype(sc)::value;
+      sfor<0, NB>([&](auto tc) { A.v[sb][decltype(tc)::value] = cC[(sb * NB + decltype(tc)::value) * 64]; });
+    });
+    const cf y = load_y(a, d, s, f, li, li < D);
+    wsync();   // the previous item's LDS reads before this item's writes
+    li_load2d<NB, G>(S, a.liCache + (long long)s * a.liStride + d.liOff + (long long)f * li_record<NB, G>(), li);
+    tridiag2d<NB, G>(A, S, li, D);
+    cf w[1];
+    eigen2d<NB, 1, G>(S, li, D, 1, w, a.vCache + (long long)s * a.vStride + d.vOff + (long long)f * DM, true);
+    if (a.lzStats && li == 0)
+      atomicAdd(&a.lzStats[((long long)(2 * r + 1)) * kLzSlots + (blockIdx.x & (kLzSlots - 1))], 1);
+    lean_tail<NB>(a, d, s, f, li, fl, w[0], y);
+  }
+}
+
+}  // namespace danse

@@ -104,10 +104,12 @@ struct LDS2 {
   // Li (float32) from the factor to the back-transform, lower triangle packed
   // by columns (ls_col); it never lives in registers, so the float32 phases
   // hold one NB x NB block (the Ryy / C block) instead of two.
-  cf Ls[DM * (DM + 1) / 2];
-  // Householder vectors u_j (i > j), packed by j (u_row)
-  cf U[DM * (DM - 1) / 2];
+  alignas(16) cf Ls[DM * (DM + 1) / 2];   // (16-byte aligned: LDS-DMA destination, kernels_2dc.hpp)
   cf g[VL];           // g = L^H e_ref (lane layout), written by the factor phase
+  // Householder vectors u_j (i > j), packed by j (u_row); the warm Lanczos
+  // keeps its basis in the first kLz DM entries.  Last member: the lean
+  // kernel (kernels_2dc.hpp) allocates the struct up to that basis only.
+  cf U[DM * (DM - 1) / 2];
 };
 
 // column-packed lower triangle: (i, c), i >= c, column c at c DM - c (c - 1) / 2
@@ -1117,6 +1119,9 @@ DANSE_DEV bool lanczos2d(const Blk<NB>& A, LDS2<NB, G>& S, int li, int D, const 
       h[j] = acc;
     });
     sfor<0, k + 1>([&](auto jc) { h[decltype(jc)::value] = sumq<G>(h[decltype(jc)::value]); });
+    // (the basis entries are read again below, not kept in registers from the
+    // coefficient pass: at k = 7 they were 80 VGPRs)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     sfor<0, k + 1>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
       sfor<0, NB>([&](auto tc) {

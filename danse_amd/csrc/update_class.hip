@@ -2,6 +2,7 @@
 // once per DMAX with -DDANSE_DMAX=N.
 #include "classes.hpp"
 #include "kernels_2d.hpp"
+#include "kernels_2dc.hpp"
 #include "kernels_big.hpp"
 #include "kernels_lane.hpp"
 
@@ -78,6 +79,17 @@ bool DANSE_CAT(launch_split_solve_d, DANSE_DMAX)(const UpdateArgs& a, int nItems
     return true;
   } else {
     (void)a; (void)nItems; (void)st;
+    return false;
+  }
+}
+
+bool DANSE_CAT(launch_lean_solve_d, DANSE_DMAX)(const UpdateArgs& a, int nItems, int fbGrid, hipStream_t st) {
+  if constexpr (k2D && kGrid == 8) {
+    hipLaunchKernelGGL((update_kernel_2dc<kNB>), dim3((unsigned)(nItems * a.F)), dim3(64), 0, st, a);
+    hipLaunchKernelGGL((fallback_kernel_2d<kNB>), dim3((unsigned)fbGrid), dim3(64), 0, st, a);
+    return true;
+  } else {
+    (void)a; (void)nItems; (void)fbGrid; (void)st;
     return false;
   }
 }
