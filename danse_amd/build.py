@@ -71,8 +71,6 @@ def _stale(obj: Path, src: Path) -> bool:
 VARIANTS = {
     'stamp': ['-DDANSE_STAMP=1'],   # per-wave phase clocks in update_kernel_2d (DANSE_UPDATE_TRACE)
     'nodma': ['-DDANSE_LEAN_DMA=0'],   # update_kernel_2dc's factor record through VGPRs
-    'recomp': ['-DDANSE_LEAN_RECOMP=1'],   # (diagnostics) update_kernel_2dc recomputes C by the congruence
-    'noupd': ['-DDANSE_LEAN_NOUPD=1'],   # (diagnostics) update_kernel_2dc without the rank-one move of C
 }
 
 

@@ -36,7 +36,7 @@ constexpr bool class_packed(int D) { return D <= kLaneMaxD; }
 #define DANSE_DECLARE_CLASS(N)                                                                      \
   void launch_update_d##N(const UpdateArgs& a, hipStream_t st);                                     \
   bool launch_split_solve_d##N(const UpdateArgs& a, int nItems, hipStream_t st);                    \
-  bool launch_lean_solve_d##N(const UpdateArgs& a, int nItems, int fbGrid, hipStream_t st);         \
+  bool launch_lean_solve_d##N(const UpdateArgs& a, int nCre, int nCn, int fbGrid, hipStream_t st);  \
   void launch_filter_update_d##N(const cd* Ryy, const cd* Rnn, int B, int D, int gevd, int rank,   \
                                  int ref, cf* w, int* diag, hipStream_t st);
 DANSE_FOR_EACH_CLASS(DANSE_DECLARE_CLASS)
@@ -62,12 +62,13 @@ inline bool launch_split_solve_class(int DMAX, const UpdateArgs& a, int nItems, 
   }
 }
 // the solves on the cached factor and C of an 8 x 8 grid class
-// (kernels_2dc.hpp): update_kernel_2dc over nItems items, then
+// (kernels_2dc.hpp): update_kernel_2dc over the nCre VAD-frame and nCn
+// noise-frame items, then
 // fallback_kernel_2d (fbGrid workgroups) over the bins it sent back
-inline bool launch_lean_solve_class(int DMAX, const UpdateArgs& a, int nItems, int fbGrid, hipStream_t st) {
+inline bool launch_lean_solve_class(int DMAX, const UpdateArgs& a, int nCre, int nCn, int fbGrid, hipStream_t st) {
   switch (DMAX) {
 #define DANSE_CASE(N) \
-  case N: return launch_lean_solve_d##N(a, nItems, fbGrid, st);
+  case N: return launch_lean_solve_d##N(a, nCre, nCn, fbGrid, st);
     DANSE_FOR_EACH_CLASS(DANSE_CASE)
 #undef DANSE_CASE
     default: return false;

@@ -45,8 +45,10 @@ struct Class {
   // items for update_kernel_2dc, [R][S * nFN] (the first creCount[r] of a row
   // used), and the fallback list / per-round counters
   bool lean = false;
+  bool leanNoise = false;   // (every node's beta > 0: li_rank1_2d)
   int* dCreItems = nullptr;
-  std::vector<int> creCount;
+  int* dCnItems = nullptr;
+  std::vector<int> creCount, cnCount;
   int* dFbList = nullptr;
   int* dFbCount = nullptr;
 };
@@ -472,23 +474,31 @@ static int build_split_lists(danse_engine* eng, const uint8_t* flags) {
         const FamNode& d = cl.host[t % nn];
         return flags[(((size_t)r * S + t / nn) * kMaxFam + d.fam) * K + d.k];
       };
-      std::vector<int> items((size_t)R * S * nn, 0);
+      std::vector<int> items((size_t)R * S * nn, 0), nitems((size_t)R * S * nn, 0);
       cl.creCount.assign(R, 0);
+      cl.cnCount.assign(R, 0);
       for (int r = 0; r < R; ++r)
         for (int t = 0; t < S * nn; ++t) {
           const uint8_t fl = flag(r, t);
-          if (!(fl & DANSE_FLAG_SOLVE) || (fl & DANSE_FLAG_PREGIVEN) || ((fl >> 2) & 3) != DANSE_OP_KEEP) continue;
-          if (cl.host[t % nn].cOff < 0) continue;
+          const int opY = fl & 3, opN = (fl >> 2) & 3;
+          if (!(fl & DANSE_FLAG_SOLVE) || (fl & DANSE_FLAG_PREGIVEN)) continue;
+          const bool vad = opN == DANSE_OP_KEEP;
+          const bool noise = cl.leanNoise && opN == DANSE_OP_AVG && opY == DANSE_OP_KEEP;
+          if ((!vad && !noise) || cl.host[t % nn].cOff < 0) continue;
           bool ok = false;
           for (int rr = r - 1; rr >= 0 && rr >= r - kLiScan; --rr) {
             const uint8_t f2 = flag(rr, t);
             if ((f2 & DANSE_FLAG_SOLVE) && !(f2 & DANSE_FLAG_PREGIVEN)) { ok = true; break; }
             if (f2 & 15) break;
           }
-          if (ok) items[(size_t)r * S * nn + cl.creCount[r]++] = t;
+          if (!ok) continue;
+          if (vad) items[(size_t)r * S * nn + cl.creCount[r]++] = t;
+          else nitems[(size_t)r * S * nn + cl.cnCount[r]++] = t;
         }
       if (!cl.dCreItems) HIPCHK(dalloc(&cl.dCreItems, items.size()));
+      if (!cl.dCnItems) HIPCHK(dalloc(&cl.dCnItems, nitems.size()));
       HIPCHK(hipMemcpy(cl.dCreItems, items.data(), items.size() * sizeof(int), hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(cl.dCnItems, nitems.data(), nitems.size() * sizeof(int), hipMemcpyHostToDevice));
     }
     if (!cl.split) continue;
     const int n = (int)cl.host.size();
@@ -813,6 +823,10 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
         cl.lean = any;
       }
       if (cl.lean) {
+        // (the noise-frame variant moves the float64 factor by rank one,
+        // li_rank1_2d, which needs beta > 0 -- as update_kernel_2d's choice)
+        cl.leanNoise = !std::getenv("DANSE_NO_LEAN_NOISE");
+        for (int i = 0; i < S * K; ++i) cl.leanNoise = cl.leanNoise && c->beta[i] > 0.0;
         HIPCHK(dalloc(&cl.dFbList, (size_t)S * cl.host.size() * F));
         HIPCHK(dalloc(&cl.dFbCount, (size_t)R));
         HIPCHK(hipMemset(cl.dFbCount, 0, (size_t)R * sizeof(int)));
@@ -1058,6 +1072,7 @@ void danse_engine_destroy(danse_engine* eng) {
     if (cl.devIds) (void)hipFree(cl.devIds);
     if (cl.dSolveItems) (void)hipFree(cl.dSolveItems);
     if (cl.dCreItems) (void)hipFree(cl.dCreItems);
+    if (cl.dCnItems) (void)hipFree(cl.dCnItems);
     if (cl.dFbList) (void)hipFree(cl.dFbList);
     if (cl.dFbCount) (void)hipFree(cl.dFbCount);
   }
@@ -1215,17 +1230,19 @@ static void launch_update(danse_engine* e, int r, hipStream_t st, unsigned mask 
     // the solves on the cached factor and C: update_kernel_2dc (whole-round
     // launches only; the fewSamples node-subset steps keep one kernel)
     const int nItems = e->S * (int)cl.host.size();
-    const int nCre = (cl.lean && mask == ~0u && (int)cl.creCount.size() > r) ? cl.creCount[r] : 0;
-    if (nCre > 0) {
-      a.leanOn = 1;
-      a.creItems = cl.dCreItems + (size_t)r * nItems;
-      a.fbList = cl.dFbList;
-      a.fbCount = cl.dFbCount;
-    }
-    if (nCre < nItems) launch_update_class(cl.DMAX, a, st);   // D > kMaxDMax rejected at create time
-    if (nCre > 0) {
+    const bool leanRound = cl.lean && mask == ~0u && (int)cl.creCount.size() > r;
+    const int nCre = leanRound ? cl.creCount[r] : 0;
+    const int nCn = leanRound ? cl.cnCount[r] : 0;
+    a.leanOn = nCre > 0 ? 1 : 0;
+    a.leanNoise = nCn > 0 ? 1 : 0;
+    a.creItems = cl.dCreItems + (size_t)r * nItems;
+    a.cnItems = cl.dCnItems + (size_t)r * nItems;
+    a.fbList = cl.dFbList;
+    a.fbCount = cl.dFbCount;
+    if (nCre + nCn < nItems) launch_update_class(cl.DMAX, a, st);   // D > kMaxDMax rejected at create time
+    if (nCre + nCn > 0) {
       (void)fill_async(cl.dFbCount + r, 0, sizeof(int), st);
-      launch_lean_solve_class(cl.DMAX, a, nCre, std::min(nCre * e->F, 256), st);
+      launch_lean_solve_class(cl.DMAX, a, nCre, nCn, std::min((nCre + nCn) * e->F, 256), st);
     }
     if (cl.split && cl.solveCount[r] > 0) {
       a.solveItems = cl.dSolveItems + (size_t)r * e->S * cl.host.size();

@@ -125,8 +125,10 @@ struct UpdateArgs {
   // the solves on the cached factor and C run on update_kernel_2dc this round
   // (items listed in creItems, their failed warm solves in fbList / fbCount
   // for fallback_kernel_2d): update_kernel_2d skips them
-  int leanOn;
-  const int* creItems;     // this round's items (s * nFN + fni) for update_kernel_2dc
+  int leanOn;              // VAD-frame solves on update_kernel_2dc<NB, false>
+  int leanNoise;           // noise-frame solves on update_kernel_2dc<NB, true>
+  const int* creItems;     // this round's items (s * nFN + fni) for update_kernel_2dc<NB, false>
+  const int* cnItems;      // this round's items for update_kernel_2dc<NB, true>
   int* fbList;             // failed warm solves (item * F + f)
   int* fbCount;            // their count (one counter per round)
   // DANSE_STAMP builds only (diagnostics): per launch wave, kStampN shader

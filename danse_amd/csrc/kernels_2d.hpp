@@ -93,7 +93,9 @@ update_kernel_2d(const UpdateArgs a) {
   // every congruence: the solves on the cached factor and C (kernels.hpp
   // c_reusable) run on update_kernel_2dc (kernels_2dc.hpp) and skip this one
   const bool hasC = G == 8 && !PK && SM == 0 && a.cCache && d.cOff >= 0;
-  if (hasC && a.leanOn && reuse && c_reusable(a, d, s)) return;   // wave-uniform
+  if (hasC && (a.leanOn || a.leanNoise) && c_reusable(a, d, s) &&
+      ((a.leanOn && reuse) || (a.leanNoise && solve && opN == DANSE_OP_AVG && opY == DANSE_OP_KEEP)))
+    return;   // wave-uniform: update_kernel_2dc runs this item
 
   // Loads of the solve on a cached factor (the common solve: a VAD frame,
   // Rnn unchanged since the last factorisation) issued with the observation's:

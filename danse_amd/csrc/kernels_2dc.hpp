@@ -19,12 +19,6 @@
 #pragma once
 #include "kernels_2d.hpp"
 
-#ifndef DANSE_LEAN_RECOMP
-#define DANSE_LEAN_RECOMP 0   // (diagnostics) C by the full congruence
-#endif
-#ifndef DANSE_LEAN_NOUPD
-#define DANSE_LEAN_NOUPD 0    // (diagnostics) no rank-one move of C
-#endif
 #ifndef DANSE_LEAN_DMA
 #define DANSE_LEAN_DMA 1   // the factor record by LDS-DMA (0: through VGPRs, diagnostics)
 #endif
@@ -49,8 +43,39 @@ DANSE_DEV void lean_tail(const UpdateArgs& a, const FamNode& d, int s, int f, in
   node_bin_tail(a, d, s, f, li, fl, false, true, w, y, dh);
 }
 
-template <int NB>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) update_kernel_2dc(const UpdateArgs a) {
+// float32 prefix sums over the lanes of a bin: over the row groups p' < p
+// (lanes q + G p', inclusive) and over the lanes q' < q of the row group
+template <int G>
+DANSE_DEV float scan_pf(float x, int p) {
+#pragma unroll
+  for (int o = 1; o < G; o <<= 1) {
+    const float u = __shfl_up(x, o * G, G * G);
+    if (p >= o) x += u;
+  }
+  return x;
+}
+template <int G>
+DANSE_DEV float scan_qf(float x, int q) {
+#pragma unroll
+  for (int o = 1; o < G; o <<= 1) {
+    const float u = __shfl_up(x, o, G);
+    if (q >= o) x += u;
+  }
+  return x;
+}
+
+// NZ = false: a VAD-active frame (Ryy update, cached factor):
+//   C' = by C + cy (Li y)(Li y)^H.
+// NZ = true: a noise frame one solve after the last (Rnn update by rank one,
+// Ryy kept): the float64 factor record moves by li_rank1_2d (solver2d.hpp),
+// Li' = beta^-1/2 T Li with T = Mf^-1 = diag(dd) - tril(pe p^H, -1), so
+//   C' = Li' Ryy Li'^H = beta^-1 T C T^H,
+// two O(D^2) passes with prefix sums: Y = T C (over the rows), C' = Y T^H / beta
+// (over the columns).
+template <int NB, bool NZ>
+// (the noise-frame variant's float64 factor move and two prefix passes need
+// the 2-waves-per-SIMD register budget)
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NZ ? 2 : 3))) update_kernel_2dc(const UpdateArgs a) {
   using namespace t2d;
   constexpr int G = 8, DM = G * NB;
   static_assert(vpl<NB, G>() == 1, "one lane-layout entry per lane");
@@ -59,25 +84,26 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) up
   const int li = threadIdx.x, p = li / G, q = li % G;
   const int F = a.F;
   const int f = blockIdx.x % F;
-  const int tt = a.creItems[blockIdx.x / F];
+  const int tt = (NZ ? a.cnItems : a.creItems)[blockIdx.x / F];
   const int fni = tt % a.nFN, s = tt / a.nFN;
   const FamNode d = a.fn[fni];
   const int D = d.D, r = a.r;
   const uint8_t fl = a.flags[(((long long)r * a.S + s) * kMaxFam + d.fam) * a.K + d.k];
   const int opY = fl & 3;
   constexpr int kRec = li_record<NB, G>();
-  const cf* liC = a.liCache + (long long)s * a.liStride + d.liOff + (long long)f * kRec;
+  cf* liC = a.liCache + (long long)s * a.liStride + d.liOff + (long long)f * kRec;
   cf* cC = a.cCache + (long long)s * a.cStride + d.cOff + (long long)f * (NB * NB * 64) + li;
   const long long tri = (long long)s * a.scmStride + d.scmOff + (long long)f * (D * (D + 1) / 2);
   auto ent = [&](int i, int c) -> long long {
     const int hi = i >= c ? i : c, lo = i >= c ? c : i;
     return tri + hi * (hi + 1) / 2 + lo;
   };
+  const double beta = a.beta[s * a.K + d.k];
 
-  // the factor record straight into LDS (LDS-DMA, [S.Ls | S.g] is the
-  // record's layout; no VGPR staging), the C block and y
+  if constexpr (!NZ) {
+    // the factor record straight into LDS (LDS-DMA, [S.Ls | S.g] is the
+    // record's layout; no VGPR staging)
 #if DANSE_LEAN_DMA
-  {
     constexpr int kChunks = (kRec * (int)sizeof(cf) + 1023) / 1024;   // 16 B per lane per instruction
     static_assert(kChunks * 1024 <= lean_lds_bytes<NB>() - (int)__builtin_offsetof(LDS2<NB>, Ls),
                   "the record's last chunk stays inside the lean LDS");
@@ -89,9 +115,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) up
                                        (__attribute__((address_space(3))) void*)(reinterpret_cast<char*>(S.Ls) + 1024 * j),
                                        16, 0, 0);
     });
-  }
 #else
-  {
     constexpr int kRecL = (kRec + 63) / 64, kNL = DM * (DM + 1) / 2;
     cf lrec[kRecL];
     sfor<0, kRecL>([&](auto jc) {
@@ -106,103 +130,149 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) up
       if (e < kNL) S.Ls[e] = lrec[j];
       else if (e < kRec) S.g[e - kNL] = lrec[j];
     });
-  }
 #endif
+  }
   const int ych = chan_of(a, d, li, li < D);
   Blk<NB> A;
-  sfor<0, NB>([&](auto sc) {
-    constexpr int sb = decltype(sc)::value;
-    sfor<0, NB>([&](auto tc) { A.v[sb][decltype(tc)::value] = cC[(sb * NB + decltype(tc)::value) * 64]; });
-  });
+  if constexpr (!NZ) {
+    sfor<0, NB>([&](auto sc) {
+      constexpr int sb = decltype(sc)::value;
+      sfor<0, NB>([&](auto tc) { A.v[sb][decltype(tc)::value] = cC[(sb * NB + decltype(tc)::value) * 64]; });
+    });
+  }
   const cf y = load_y_c(a, d, s, f, ych, li < D);
   S.vb[li] = y;
-  __builtin_amdgcn_s_waitcnt(0);   // (the record's LDS-DMA landed)
+  if constexpr (!NZ) __builtin_amdgcn_s_waitcnt(0);   // (the record's LDS-DMA landed)
   wsync();
   cf yc[NB];
   sfor<0, NB>([&](auto sc) { yc[decltype(sc)::value] = S.vb[q + G * decltype(sc)::value]; });
   wsync();
 
-#if DANSE_LEAN_RECOMP
-  // (diagnostics: C by the full congruence of this round's Ryy)
-  if (true) {
-    const double beta = a.beta[s * a.K + d.k];
-    const float by = (float)beta, cy = (opY == DANSE_OP_SET) ? (float)(1.0 / D) : (float)((1.0 - beta) / D);
-    cf yr2[NB];
-    sfor<0, NB>([&](auto sc) { yr2[decltype(sc)::value] = S.vb[p + G * decltype(sc)::value]; });
+  bool ok = true;
+  if constexpr (!NZ) {
+    if (opY) {
+      const float by = (float)beta, cy = (opY == DANSE_OP_SET) ? (float)(1.0 / D) : (float)((1.0 - beta) / D);
+      // u = Li y: partial sums over the row group (row layout: every lane of
+      // row group p holds u[p + G sb]), the column layout through LDS
+      cf ur[NB], uc[NB];
+      sfor<0, NB>([&](auto sc) {
+        constexpr int sb = decltype(sc)::value;
+        cf acc = cf{0.0f, 0.0f};
+        sfor<0, sb + 1>([&](auto tc) {
+          constexpr int tb = decltype(tc)::value;
+          acc = acc + ls_get<DM>(S.Ls, p + G * sb, q + G * tb) * yc[tb];   // (cmul would conjugate Li)
+        });
+        ur[sb] = sumq<G>(acc);
+        if (q == 0) S.vb[p + G * sb] = ur[sb];
+      });
+      wsync();
+      sfor<0, NB>([&](auto tc) { uc[decltype(tc)::value] = S.vb[q + G * decltype(tc)::value]; });
+      wsync();
+      sfor<0, NB>([&](auto sc) {
+        constexpr int sb = decltype(sc)::value;
+        sfor<0, NB>([&](auto tc) {
+          constexpr int tb = decltype(tc)::value;
+          const cf uu = cy * mulc(ur[sb], uc[tb]);
+          cf x = csel(opY == DANSE_OP_SET, uu, by * A.v[sb][tb] + uu);
+          if (sb == tb && p == q) x.im = 0.0f;
+          A.v[sb][tb] = x;
+          cC[(sb * NB + tb) * 64] = x;
+        });
+      });
+    }
+  } else {
+    // the float64 factor record by rank one (Li', g in S.Ls / S.g, record
+    // rewritten), then the float32 factor cache of the later solves
+    const double cyN = (1.0 - beta) / D;
+    cd* l64 = a.l64Cache + (long long)s * a.l64Stride + d.l64Off + (long long)f * l64_record<NB, G>();
+    ok = li_rank1_2d<NB, G>(S, li, yc, beta, cyN, l64, true);
+    li_store2d<NB, G>(S, liC, li);
     sfor<0, NB>([&](auto sc) {
       constexpr int sb = decltype(sc)::value;
+      sfor<0, NB>([&](auto tc) { A.v[sb][decltype(tc)::value] = cC[(sb * NB + decltype(tc)::value) * 64]; });
+    });
+    // T's coefficients from li_rank1_2d's LDS (S.invd: a_i = alpha |p_i|^2,
+    // S.rb64[0]: p_i): t_i = 1 + sum_(k < i) a_k, dd_i = sqrt(t_i / t_(i+1)),
+    // pe_i = alpha p_i / sqrt(t_i t_(i+1)); this lane's rows i = p + G sb
+    const double alpha = cyN / beta;
+    float ddr[NB];
+    cf per[NB], pcr[NB];   // pe_i, conj(p_i)
+    double tlo[NB];
+    {
+      double carry = 1.0;
+      sfor<0, NB>([&](auto sc) {
+        constexpr int sb = decltype(sc)::value;
+        const double av = S.invd[p + G * sb];
+        const double inc = scan_p<G>(av, p);
+        tlo[sb] = carry + (inc - av);
+        carry += __shfl(inc, (G - 1) * G + q, G * G);
+        const double thi = tlo[sb] + av;
+        const cd pi = S.rb64[0][p + G * sb];
+        ddr[sb] = (float)sqrt(tlo[sb] / thi);
+        per[sb] = cfk((alpha / sqrt(tlo[sb] * thi)) * pi);
+        pcr[sb] = conjg(cfk(pi));
+      });
+    }
+    // Y = T C: Y[i][c] = dd_i C[i][c] - pe_i sum_(k < i) conj(p_k) C[k][c]
+    // (a prefix over the row groups plus the earlier block rows' sums)
+    {
+      cf carP[NB];
+      sfor<0, NB>([&](auto tc) { carP[decltype(tc)::value] = cf{0.0f, 0.0f}; });
+      sfor<0, NB>([&](auto sc) {
+        constexpr int sb = decltype(sc)::value;
+        sfor<0, NB>([&](auto tc) {
+          constexpr int tb = decltype(tc)::value;
+          const cf x = A.v[sb][tb];
+          const cf u = pcr[sb] * x;
+          const float ire = scan_pf<G>(u.re, p), iim = scan_pf<G>(u.im, p);
+          const float tre = __shfl(ire, (G - 1) * G + q, G * G), tim = __shfl(iim, (G - 1) * G + q, G * G);
+          const cf ex = cf{carP[tb].re + (ire - u.re), carP[tb].im + (iim - u.im)};
+          carP[tb] = cf{carP[tb].re + tre, carP[tb].im + tim};
+          A.v[sb][tb] = ddr[sb] * x - per[sb] * ex;
+        });
+      });
+    }
+    // C' = Y T^H / beta: C'[i][c] = (dd_c Y[i][c] - conj(pe_c) sum_(k < c) Y[i][k] p_k) / beta
+    // (a prefix over the lanes of the row group plus the earlier block
+    // columns' sums); the column coefficients from row group q
+    {
+      const float ib = (float)(1.0 / beta);
+      cf carQ[NB];
+      sfor<0, NB>([&](auto sc) { carQ[decltype(sc)::value] = cf{0.0f, 0.0f}; });
       sfor<0, NB>([&](auto tc) {
         constexpr int tb = decltype(tc)::value;
-        const int i = p + G * sb, c = q + G * tb;
-        const bool in = i < D && c < D;
-        cf x = in ? a.Ryy[ent(i, c)] : cf{0.0f, 0.0f};
-        if (i < c) x = conjg(x);
-        if (opY) {
-          const cf yy = cy * mulc(yr2[sb], yc[tb]);
-          x = csel(opY == DANSE_OP_SET, yy, by * x + yy);
-          if (i == c) x.im = 0.0f;
-        }
-        A.v[sb][tb] = x;
+        const float ddc = __shfl(ddr[tb], G * q, G * G);
+        const cf pec = cf{__shfl(per[tb].re, G * q, G * G), __shfl(per[tb].im, G * q, G * G)};
+        const cf pc = conjg(cf{__shfl(pcr[tb].re, G * q, G * G), __shfl(pcr[tb].im, G * q, G * G)});   // p_c
+        sfor<0, NB>([&](auto sc) {
+          constexpr int sb = decltype(sc)::value;
+          const cf yv = A.v[sb][tb];
+          const cf v = yv * pc;
+          const float ire = scan_qf<G>(v.re, q), iim = scan_qf<G>(v.im, q);
+          const float tre = __shfl(ire, G - 1, G), tim = __shfl(iim, G - 1, G);
+          const cf ex = cf{carQ[sb].re + (ire - v.re), carQ[sb].im + (iim - v.im)};
+          carQ[sb] = cf{carQ[sb].re + tre, carQ[sb].im + tim};
+          cf x = ib * (ddc * yv - conjg(pec) * ex);
+          if (sb == tb && p == q) x.im = 0.0f;
+          A.v[sb][tb] = x;
+          cC[(sb * NB + tb) * 64] = x;
+        });
       });
-    });
-    wsync();
-    congruence2d<NB, G>(A, S, li, D);
-  }
-  if (false) {
-#else
-  if (opY) {
-#endif
-    const double beta = a.beta[s * a.K + d.k];
-    const float by = (float)beta, cy = (opY == DANSE_OP_SET) ? (float)(1.0 / D) : (float)((1.0 - beta) / D);
-    // u = Li y: partial sums over the row group (row layout: every lane of
-    // row group p holds u[p + G sb]), the column layout through LDS
-    cf ur[NB], uc[NB];
-    sfor<0, NB>([&](auto sc) {
-      constexpr int sb = decltype(sc)::value;
-      cf acc = cf{0.0f, 0.0f};
-      sfor<0, sb + 1>([&](auto tc) {
-        constexpr int tb = decltype(tc)::value;
-        acc = acc + ls_get<DM>(S.Ls, p + G * sb, q + G * tb) * yc[tb];   // (cmul would conjugate Li)
-      });
-      ur[sb] = sumq<G>(acc);
-      if (q == 0) S.vb[p + G * sb] = ur[sb];
-    });
-    wsync();
-    sfor<0, NB>([&](auto tc) { uc[decltype(tc)::value] = S.vb[q + G * decltype(tc)::value]; });
-    wsync();
-    if (!DANSE_LEAN_NOUPD)
-    sfor<0, NB>([&](auto sc) {
-      constexpr int sb = decltype(sc)::value;
-      sfor<0, NB>([&](auto tc) {
-        constexpr int tb = decltype(tc)::value;
-        const cf uu = cy * mulc(ur[sb], uc[tb]);
-        cf x = csel(opY == DANSE_OP_SET, uu, by * A.v[sb][tb] + uu);
-        if (sb == tb && p == q) x.im = 0.0f;
-        A.v[sb][tb] = x;
-        cC[(sb * NB + tb) * 64] = x;
-      });
-    });
+    }
   }
 
   cf* vC = a.vCache + (long long)s * a.vStride + d.vOff + (long long)f * DM;
   cf vv[1];
   float lam1;
   bool warm;
-  // this round's Ryy recursion (as update_kernel_2d), after the solve: no
-  // register of it is live across the Lanczos phase
-  auto ryy_recursion = [&]() {
-    if (!opY) return;
+  // this round's SCM recursion (as update_kernel_2d: Ryy in float32, or on a
+  // noise frame Rnn in float64), after the solve: none of its registers is
+  // live across the Lanczos phase
+  auto recursion = [&]() {
+    if constexpr (!NZ) {
+      if (!opY) return;
+    }
     constexpr int kLo = NB * (NB + 1) / 2;
-    cf rlo[kLo];
-    sfor<0, NB>([&](auto sc) {
-      constexpr int sb = decltype(sc)::value;
-      sfor<0, sb + 1>([&](auto tc) {
-        constexpr int tb = decltype(tc)::value;
-        const int i = p + G * sb, c = q + G * tb;
-        const bool lo = i < D && c < D && i >= c;
-        rlo[sb * (sb + 1) / 2 + tb] = a.Ryy[lo ? ent(i, c) : tri];
-      });
-    });
     wsync();   // (the solve's LDS reads before the staging write)
     S.vb[li] = y;
     wsync();
@@ -212,23 +282,64 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) up
       yr[sb] = S.vb[p + G * sb];
       yq[sb] = S.vb[q + G * sb];
     });
-    const double beta = a.beta[s * a.K + d.k];
-    const float by = (float)beta, cy = (opY == DANSE_OP_SET) ? (float)(1.0 / D) : (float)((1.0 - beta) / D);
-    sfor<0, NB>([&](auto sc) {
-      constexpr int sb = decltype(sc)::value;
-      sfor<0, sb + 1>([&](auto tc) {
-        constexpr int tb = decltype(tc)::value;
-        const int i = p + G * sb, c = q + G * tb;
-        const cf yy = cy * mulc(yr[sb], yq[tb]);
-        cf x = csel(opY == DANSE_OP_SET, yy, by * rlo[sb * (sb + 1) / 2 + tb] + yy);
-        if (i == c) x.im = 0.0f;
-        if (i < D && c < D && i >= c) a.Ryy[ent(i, c)] = x;
+    if constexpr (!NZ) {
+      cf rlo[kLo];
+      sfor<0, NB>([&](auto sc) {
+        constexpr int sb = decltype(sc)::value;
+        sfor<0, sb + 1>([&](auto tc) {
+          constexpr int tb = decltype(tc)::value;
+          const int i = p + G * sb, c = q + G * tb;
+          const bool lo = i < D && c < D && i >= c;
+          rlo[sb * (sb + 1) / 2 + tb] = a.Ryy[lo ? ent(i, c) : tri];
+        });
       });
-    });
+      const float by = (float)beta, cy = (opY == DANSE_OP_SET) ? (float)(1.0 / D) : (float)((1.0 - beta) / D);
+      sfor<0, NB>([&](auto sc) {
+        constexpr int sb = decltype(sc)::value;
+        sfor<0, sb + 1>([&](auto tc) {
+          constexpr int tb = decltype(tc)::value;
+          const int i = p + G * sb, c = q + G * tb;
+          const cf yy = cy * mulc(yr[sb], yq[tb]);
+          cf x = csel(opY == DANSE_OP_SET, yy, by * rlo[sb * (sb + 1) / 2 + tb] + yy);
+          if (i == c) x.im = 0.0f;
+          if (i < D && c < D && i >= c) a.Ryy[ent(i, c)] = x;
+        });
+      });
+    } else {
+      // Rnn' = beta Rnn + cy y y^H (opN = AVG), float64, lower entries
+      const double cy = (1.0 - beta) / D;
+      sfor<0, NB>([&](auto sc) {
+        constexpr int sb = decltype(sc)::value;
+        cd rn[sb + 1];
+        sfor<0, sb + 1>([&](auto tc) {
+          constexpr int tb = decltype(tc)::value;
+          const int i = p + G * sb, c = q + G * tb;
+          const bool lo = i < D && c < D && i >= c;
+          rn[tb] = ld_cd(a.Rnn + (lo ? ent(i, c) : tri));
+        });
+        hold(rn);
+        sfor<0, sb + 1>([&](auto tc) {
+          constexpr int tb = decltype(tc)::value;
+          const int i = p + G * sb, c = q + G * tb;
+          cd yy = cd{0.0, 0.0};
+          fma_cc(yy, cdk(yr[sb]), cdk(yq[tb]));
+          cd x = beta * rn[tb];
+          x.re = fma(cy, yy.re, x.re);
+          x.im = (i == c) ? 0.0 : fma(cy, yy.im, x.im);
+          if (i < D && c < D && i >= c) st_cd(a.Rnn + ent(i, c), x);
+        });
+      });
+    }
   };
-  if (!lanczos2d<NB, G>(A, S, li, D, vC, vv, lam1, warm)) {
-    ryy_recursion();
-    // (wave-uniform) the Householder path of fallback_kernel_2d writes this bin
+  if constexpr (NZ) {
+    if (!ok && li == 0) atomicOr(&a.diag[(s * a.K + d.k) * kMaxFam + d.fam], 1);
+  }
+  const bool conv = lanczos2d<NB, G>(A, S, li, D, vC, vv, lam1, warm);
+  if (!conv) {
+    // (wave-uniform) fallback_kernel_2d writes this bin: a restart from this
+    // attempt's Ritz vector, else the Householder path
+    if (warm && li < DM) vC[li] = vv[0];
+    recursion();
     if (li == 0) {
       const int e = atomicAdd(&a.fbCount[r], 1);
       a.fbList[e] = tt * F + f;
@@ -240,7 +351,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) up
   if (li < DM) vC[li] = vv[0];
   if (a.lzStats && li == 0) atomicAdd(&a.lzStats[((long long)(2 * r)) * kLzSlots + (blockIdx.x & (kLzSlots - 1))], 1);
   lean_tail<NB>(a, d, s, f, li, fl, w[0], y);
-  ryy_recursion();
+  recursion();
 }
 
 // The warm solves update_kernel_2dc sent back: the Householder path
@@ -271,11 +382,24 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) fa
     const cf y = load_y(a, d, s, f, li, li < D);
     wsync();   // the previous item's LDS reads before this item's writes
     li_load2d<NB, G>(S, a.liCache + (long long)s * a.liStride + d.liOff + (long long)f * li_record<NB, G>(), li);
-    tridiag2d<NB, G>(A, S, li, D);
+    cf* vC = a.vCache + (long long)s * a.vStride + d.vOff + (long long)f * DM;
     cf w[1];
-    eigen2d<NB, 1, G>(S, li, D, 1, w, a.vCache + (long long)s * a.vStride + d.vOff + (long long)f * DM, true);
-    if (a.lzStats && li == 0)
-      atomicAdd(&a.lzStats[((long long)(2 * r + 1)) * kLzSlots + (blockIdx.x & (kLzSlots - 1))], 1);
+    // kLz more Lanczos steps from update_kernel_2dc's Ritz vector (counted as
+    // accepted warm solves), else the Householder path (counted sent back)
+    cf vv[1];
+    float lam1;
+    bool warm;
+    if (lanczos2d<NB, G>(A, S, li, D, vC, vv, lam1, warm)) {
+      rank1_w2d<NB, G>(S, li, D, vv, lam1, w);
+      if (li < DM) vC[li] = vv[0];
+      if (a.lzStats && li == 0)
+        atomicAdd(&a.lzStats[((long long)(2 * r)) * kLzSlots + (blockIdx.x & (kLzSlots - 1))], 1);
+    } else {
+      tridiag2d<NB, G>(A, S, li, D);
+      eigen2d<NB, 1, G>(S, li, D, 1, w, vC, true);
+      if (a.lzStats && li == 0)
+        atomicAdd(&a.lzStats[((long long)(2 * r + 1)) * kLzSlots + (blockIdx.x & (kLzSlots - 1))], 1);
+    }
     lean_tail<NB>(a, d, s, f, li, fl, w[0], y);
   }
 }

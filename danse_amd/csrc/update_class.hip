@@ -83,13 +83,14 @@ bool DANSE_CAT(launch_split_solve_d, DANSE_DMAX)(const UpdateArgs& a, int nItems
   }
 }
 
-bool DANSE_CAT(launch_lean_solve_d, DANSE_DMAX)(const UpdateArgs& a, int nItems, int fbGrid, hipStream_t st) {
+bool DANSE_CAT(launch_lean_solve_d, DANSE_DMAX)(const UpdateArgs& a, int nCre, int nCn, int fbGrid, hipStream_t st) {
   if constexpr (k2D && kGrid == 8) {
-    hipLaunchKernelGGL((update_kernel_2dc<kNB>), dim3((unsigned)(nItems * a.F)), dim3(64), 0, st, a);
+    if (nCre > 0) hipLaunchKernelGGL((update_kernel_2dc<kNB, false>), dim3((unsigned)(nCre * a.F)), dim3(64), 0, st, a);
+    if (nCn > 0) hipLaunchKernelGGL((update_kernel_2dc<kNB, true>), dim3((unsigned)(nCn * a.F)), dim3(64), 0, st, a);
     hipLaunchKernelGGL((fallback_kernel_2d<kNB>), dim3((unsigned)fbGrid), dim3(64), 0, st, a);
     return true;
   } else {
-    (void)a; (void)nItems; (void)fbGrid; (void)st;
+    (void)a; (void)nCre; (void)nCn; (void)fbGrid; (void)st;
     return false;
   }
 }
