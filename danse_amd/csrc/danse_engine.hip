@@ -484,7 +484,7 @@ static int build_split_lists(danse_engine* eng, const uint8_t* flags) {
           if (!(fl & DANSE_FLAG_SOLVE) || (fl & DANSE_FLAG_PREGIVEN)) continue;
           const bool vad = opN == DANSE_OP_KEEP;
           const bool noise = cl.leanNoise && opN == DANSE_OP_AVG && opY == DANSE_OP_KEEP;
-          if ((!vad && !noise) || cl.host[t % nn].cOff < 0) continue;
+          if ((!vad && !noise) || cl.host[t % nn].cOff < 0 || r % kCRefresh == 0) continue;
           bool ok = false;
           for (int rr = r - 1; rr >= 0 && rr >= r - kLiScan; --rr) {
             const uint8_t f2 = flag(rr, t);
@@ -698,7 +698,7 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
       if (fn.vOff >= 0 && fn.l64Off >= 0 && class_grid(class_dmax(fn.D)) == 8 && !std::getenv("DANSE_NO_CCACHE")) {
         const long long nb = class_dmax(fn.D) / 8;
         fn.cOff = cOff;
-        cOff += (long long)F * nb * nb * 64;
+        cOff += (long long)F * nb * (nb + 1) / 2 * 64;   // (kernels_2d.hpp c_record)
       }
       eng->fns.push_back(fn);
     }

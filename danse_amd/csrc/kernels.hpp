@@ -220,6 +220,12 @@ DANSE_DEV bool li_updatable(const UpdateArgs& a, const FamNode& d, int s, int op
 // the current factor and of Ryy before this round's update: the factor is
 // reused (li_reusable) and no round since that solve updated either SCM.
 // This round's Ryy update then moves C by the same rank one, through Li y.
+// (every kCRefresh-th round, r % kCRefresh == 0, takes the full congruence
+// instead: the rank-one moves of the cached C, exact in arithmetic, carry
+// float32 roundings from frame to frame, the noise-frame transforms without
+// the forgetting factor's decay.  Whole rounds, not a stagger over items: a
+// partial full-kernel launch every round cost N2 10 ms per run)
+constexpr int kCRefresh = 32;
 DANSE_DEV bool c_reusable(const UpdateArgs& a, const FamNode& d, int s) {
   for (int rr = a.r - 1; rr >= 0 && rr >= a.r - kLiScan; --rr) {
     const uint8_t f2 = a.flags[(((long long)rr * a.S + s) * kMaxFam + d.fam) * a.K + d.k];

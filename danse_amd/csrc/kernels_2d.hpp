@@ -34,6 +34,46 @@ namespace danse {
 // conjugates of the stored lower ones, only the lower ones are written back,
 // the diagonals are kept real), bin-major; PK (with SM = 2): a lane class's
 // bin-minor triangles (kernels_lane.hpp).
+// The C cache of a bin (UpdateArgs.cCache): the lane-layout blocks sb >= tb
+// of C, [NB (NB + 1) / 2][64] (the blocks above come back by an 8 x 8 lane
+// transpose: entry (p + 8 sb, q + 8 tb) of an upper block is the conjugate of
+// lane (q, p)'s entry of block (tb, sb)).  cC points at this lane's column.
+template <int NB>
+constexpr int c_record() { return NB * (NB + 1) / 2 * 64; }
+template <int NB>
+DANSE_DEV void c_store(cf* cC, const t2d::Blk<NB>& A) {
+  sfor<0, NB>([&](auto sc) {
+    constexpr int sb = decltype(sc)::value;
+    sfor<0, sb + 1>([&](auto tc) {
+      constexpr int tb = decltype(tc)::value;
+      cC[(sb * (sb + 1) / 2 + tb) * 64] = A.v[sb][tb];
+    });
+  });
+}
+template <int NB>
+DANSE_DEV void c_load_lower(t2d::Blk<NB>& A, const cf* cC) {
+  sfor<0, NB>([&](auto sc) {
+    constexpr int sb = decltype(sc)::value;
+    sfor<0, sb + 1>([&](auto tc) {
+      constexpr int tb = decltype(tc)::value;
+      A.v[sb][tb] = cC[(sb * (sb + 1) / 2 + tb) * 64];
+    });
+  });
+}
+// the upper blocks from the lower ones through buf (LDS, (NB - 1) * 64 entries)
+template <int NB>
+DANSE_DEV void c_fill_upper(t2d::Blk<NB>& A, cf* buf, int li) {
+  const int p = li / 8, q = li % 8;
+  sfor<1, NB>([&](auto tc) {
+    constexpr int tb = decltype(tc)::value;
+    t2d::wsync();
+    sfor<0, tb>([&](auto sc) { buf[decltype(sc)::value * 64 + q * 8 + p] = A.v[tb][decltype(sc)::value]; });
+    t2d::wsync();
+    sfor<0, tb>([&](auto sc) { A.v[decltype(sc)::value][tb] = conjg(buf[decltype(sc)::value * 64 + p * 8 + q]); });
+  });
+  t2d::wsync();
+}
+
 template <int NB, int RMAX, int G = 8, bool PK = false, int SM = 0>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NB <= 5 ? DANSE_2D_WPE : 1)))
 update_kernel_2d(const UpdateArgs a) {
@@ -93,7 +133,7 @@ update_kernel_2d(const UpdateArgs a) {
   // every congruence: the solves on the cached factor and C (kernels.hpp
   // c_reusable) run on update_kernel_2dc (kernels_2dc.hpp) and skip this one
   const bool hasC = G == 8 && !PK && SM == 0 && a.cCache && d.cOff >= 0;
-  if (hasC && (a.leanOn || a.leanNoise) && c_reusable(a, d, s) &&
+  if (hasC && (a.leanOn || a.leanNoise) && r % kCRefresh != 0 && c_reusable(a, d, s) &&
       ((a.leanOn && reuse) || (a.leanNoise && solve && opN == DANSE_OP_AVG && opY == DANSE_OP_KEEP)))
     return;   // wave-uniform: update_kernel_2dc runs this item
 
@@ -293,13 +333,8 @@ update_kernel_2d(const UpdateArgs a) {
     stamp(4);
     if (solve) {
       congruence2d<NB, G>(A, S, li, D);
-      if (hasC && fvalid) {
-        cf* cC = a.cCache + (long long)s * a.cStride + a.fn[fni].cOff + (long long)f * (NB * NB * 64) + li;
-        sfor<0, NB>([&](auto sc) {
-          constexpr int sb = decltype(sc)::value;
-          sfor<0, NB>([&](auto tc) { cC[(sb * NB + decltype(tc)::value) * 64] = A.v[sb][decltype(tc)::value]; });
-        });
-      }
+      if (hasC && fvalid)
+        c_store<NB>(a.cCache + (long long)s * a.cStride + a.fn[fni].cOff + (long long)f * c_record<NB>() + li, A);
       stamp(5);
       const int path = gevd2d_solve<NB, RMAX, G>(A, S, li, D, a.rank, w, vC, fvalid);
       // (one atomic per wave -- the path is wave-uniform -- into one of

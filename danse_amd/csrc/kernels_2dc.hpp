@@ -92,7 +92,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NZ ? 2 
   const int opY = fl & 3;
   constexpr int kRec = li_record<NB, G>();
   cf* liC = a.liCache + (long long)s * a.liStride + d.liOff + (long long)f * kRec;
-  cf* cC = a.cCache + (long long)s * a.cStride + d.cOff + (long long)f * (NB * NB * 64) + li;
+  cf* cC = a.cCache + (long long)s * a.cStride + d.cOff + (long long)f * c_record<NB>() + li;
   const long long tri = (long long)s * a.scmStride + d.scmOff + (long long)f * (D * (D + 1) / 2);
   auto ent = [&](int i, int c) -> long long {
     const int hi = i >= c ? i : c, lo = i >= c ? c : i;
@@ -134,12 +134,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NZ ? 2 
   }
   const int ych = chan_of(a, d, li, li < D);
   Blk<NB> A;
-  if constexpr (!NZ) {
-    sfor<0, NB>([&](auto sc) {
-      constexpr int sb = decltype(sc)::value;
-      sfor<0, NB>([&](auto tc) { A.v[sb][decltype(tc)::value] = cC[(sb * NB + decltype(tc)::value) * 64]; });
-    });
-  }
+  if constexpr (!NZ) c_load_lower<NB>(A, cC);
   const cf y = load_y_c(a, d, s, f, ych, li < D);
   S.vb[li] = y;
   if constexpr (!NZ) __builtin_amdgcn_s_waitcnt(0);   // (the record's LDS-DMA landed)
@@ -147,6 +142,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NZ ? 2 
   cf yc[NB];
   sfor<0, NB>([&](auto sc) { yc[decltype(sc)::value] = S.vb[q + G * decltype(sc)::value]; });
   wsync();
+  // (after the record's LDS-DMA drained: its last chunk runs into S.U)
+  if constexpr (!NZ) c_fill_upper<NB>(A, S.U, li);
 
   bool ok = true;
   if constexpr (!NZ) {
@@ -176,9 +173,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NZ ? 2 
           cf x = csel(opY == DANSE_OP_SET, uu, by * A.v[sb][tb] + uu);
           if (sb == tb && p == q) x.im = 0.0f;
           A.v[sb][tb] = x;
-          cC[(sb * NB + tb) * 64] = x;
         });
       });
+      c_store<NB>(cC, A);
     }
   } else {
     // the float64 factor record by rank one (Li', g in S.Ls / S.g, record
@@ -187,10 +184,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NZ ? 2 
     cd* l64 = a.l64Cache + (long long)s * a.l64Stride + d.l64Off + (long long)f * l64_record<NB, G>();
     ok = li_rank1_2d<NB, G>(S, li, yc, beta, cyN, l64, true);
     li_store2d<NB, G>(S, liC, li);
-    sfor<0, NB>([&](auto sc) {
-      constexpr int sb = decltype(sc)::value;
-      sfor<0, NB>([&](auto tc) { A.v[sb][decltype(tc)::value] = cC[(sb * NB + decltype(tc)::value) * 64]; });
-    });
+    c_load_lower<NB>(A, cC);
+    c_fill_upper<NB>(A, S.U, li);
     // T's coefficients from li_rank1_2d's LDS (S.invd: a_i = alpha |p_i|^2,
     // S.rb64[0]: p_i): t_i = 1 + sum_(k < i) a_k, dd_i = sqrt(t_i / t_(i+1)),
     // pe_i = alpha p_i / sqrt(t_i t_(i+1)); this lane's rows i = p + G sb
@@ -255,9 +250,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NZ ? 2 
           cf x = ib * (ddc * yv - conjg(pec) * ex);
           if (sb == tb && p == q) x.im = 0.0f;
           A.v[sb][tb] = x;
-          cC[(sb * NB + tb) * 64] = x;
         });
       });
+      c_store<NB>(cC, A);
     }
   }
 
@@ -373,14 +368,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) fa
     const FamNode d = a.fn[fni];
     const int D = d.D;
     const uint8_t fl = a.flags[(((long long)r * a.S + s) * kMaxFam + d.fam) * a.K + d.k];
-    const cf* cC = a.cCache + (long long)s * a.cStride + d.cOff + (long long)f * (NB * NB * 64) + li;
+    const cf* cC = a.cCache + (long long)s * a.cStride + d.cOff + (long long)f * c_record<NB>() + li;
     Blk<NB> A;
-    sfor<0, NB>([&](auto sc) {
-      constexpr int sb = decltype(sc)::value;
-      sfor<0, NB>([&](auto tc) { A.v[sb][decltype(tc)::value] = cC[(sb * NB + decltype(tc)::value) * 64]; });
-    });
+    c_load_lower<NB>(A, cC);
     const cf y = load_y(a, d, s, f, li, li < D);
     wsync();   // the previous item's LDS reads before this item's writes
+    c_fill_upper<NB>(A, S.U, li);
     li_load2d<NB, G>(S, a.liCache + (long long)s * a.liStride + d.liOff + (long long)f * li_record<NB, G>(), li);
     cf* vC = a.vCache + (long long)s * a.vStride + d.vOff + (long long)f * DM;
     cf w[1];
