@@ -25,9 +25,14 @@
 
 namespace danse {
 
-template <int NB>
+// Lanczos steps of the first attempt: kLz (8) on VAD frames; two more on the
+// noise frames, whose transform moves C further (most of the restarts were
+// there; the VAD variant would spill at its 3-waves-per-SIMD budget)
+template <int NB, bool NZ>
+constexpr int lean_lz() { return t2d::kLz<8 * NB>() + (NZ ? 2 : 0); }
+template <int NB, bool NZ = true>
 constexpr int lean_lds_bytes() {
-  return (int)__builtin_offsetof(t2d::LDS2<NB>, U) + t2d::kLz<8 * NB>() * 8 * NB * (int)sizeof(cf);
+  return (int)__builtin_offsetof(t2d::LDS2<NB>, U) + lean_lz<NB, NZ>() * 8 * NB * (int)sizeof(cf);
 }
 
 // w[r + 1], its history slot, and the per-bin tail (external filters, dhat)
@@ -79,7 +84,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NZ ? 2 
   using namespace t2d;
   constexpr int G = 8, DM = G * NB;
   static_assert(vpl<NB, G>() == 1, "one lane-layout entry per lane");
-  __shared__ __attribute__((aligned(16))) char ldsRaw[lean_lds_bytes<NB>()];
+  __shared__ __attribute__((aligned(16))) char ldsRaw[lean_lds_bytes<NB, NZ>()];
   LDS2<NB, G>& S = *reinterpret_cast<LDS2<NB, G>*>(ldsRaw);   // (members up to the Lanczos basis)
   const int li = threadIdx.x, p = li / G, q = li % G;
   const int F = a.F;
@@ -105,7 +110,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NZ ? 2 
     // record's layout; no VGPR staging)
 #if DANSE_LEAN_DMA
     constexpr int kChunks = (kRec * (int)sizeof(cf) + 1023) / 1024;   // 16 B per lane per instruction
-    static_assert(kChunks * 1024 <= lean_lds_bytes<NB>() - (int)__builtin_offsetof(LDS2<NB>, Ls),
+    static_assert(kChunks * 1024 <= lean_lds_bytes<NB, NZ>() - (int)__builtin_offsetof(LDS2<NB>, Ls),
                   "the record's last chunk stays inside the lean LDS");
     sfor<0, kChunks>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
@@ -329,7 +334,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NZ ? 2 
   if constexpr (NZ) {
     if (!ok && li == 0) atomicOr(&a.diag[(s * a.K + d.k) * kMaxFam + d.fam], 1);
   }
-  const bool conv = lanczos2d<NB, G>(A, S, li, D, vC, vv, lam1, warm);
+  const bool conv = lanczos2d<NB, G, lean_lz<NB, NZ>()>(A, S, li, D, vC, vv, lam1, warm);
   if (!conv) {
     // (wave-uniform) fallback_kernel_2d writes this bin: a restart from this
     // attempt's Ritz vector, else the Householder path

@@ -1057,10 +1057,10 @@ constexpr float kLzBreak = 1.0e-6f;   // first-step breakdown test (relative to 
 
 // true (wave-uniform) if every bin of the wave converged: then vv (lane
 // layout) is the unit eigenvector of C and lam1 its eigenvalue
-template <int NB, int G = 8>
+template <int NB, int G = 8, int M = kLz<G * NB>()>
 DANSE_DEV bool lanczos2d(const Blk<NB>& A, LDS2<NB, G>& S, int li, int D, const cf* vIn, cf (&vv)[vpl<NB, G>()],
                          float& lam1, bool& warm) {
-  constexpr int DM = G * NB, L = bin_lanes<G>(), V = vpl<NB, G>(), M = kLz<DM>();
+  constexpr int DM = G * NB, L = bin_lanes<G>(), V = vpl<NB, G>();
   static_assert(M * DM <= DM * (DM - 1) / 2, "the Lanczos basis lives in the reflector space");
   const int p = li / G, q = li % G;
   cf* Q = S.U;   // [M][DM] basis vectors (the Householder vectors' space: unused on this path)
