@@ -21,6 +21,7 @@
 #include "resident_api.hpp"
 #include "cond.hpp"
 #include "wide_online.hpp"
+#include "span.hpp"
 
 using namespace danse;
 
@@ -176,6 +177,12 @@ struct danse_engine {
   int resNFam = 0;
   // condition numbers of Ryy (cond.hpp), every condEvery-th iteration
   int condEvery = 0;
+  // pre-solve prefix fast-forward (span.hpp): rounds [0, ffP) run the tail
+  // only, their recursion in one span_rec_kernel before round ffP; ffPraw
+  // from the flag table (build_split_lists), ffAlloc the histories' rounds
+  int ffP = 0, ffPraw = 0, ffAlloc = 0;
+  bool ffOk = false;
+  cf *yHist = nullptr, *zHist = nullptr;
   double* condHist = nullptr;   // [S][nFN][R][F]
 };
 
@@ -457,6 +464,29 @@ static void build_wide_lists(danse_engine* eng, const uint8_t* flags) {
 
 static int build_split_lists(danse_engine* eng, const uint8_t* flags) {
   const int S = eng->S, K = eng->K, R = eng->R;
+  {
+    // the pre-solve prefix: the rounds before the first solve of any item
+    // and before the first round at which the frame counters allow a start
+    // (the reference gate's check reads the SCMs there: ny > D and nn > D,
+    // the counts of the rounds whose Ryy / Rnn op is not KEEP)
+    int P = R;
+    const int nf = (int)eng->fns.size();
+    for (int t = 0; t < S * nf; ++t) {
+      const FamNode& d = eng->fns[t % nf];
+      int ny = 0, nn = 0;
+      for (int r = 0; r < P; ++r) {
+        const uint8_t fl = flags[(((size_t)r * S + t / nf) * kMaxFam + d.fam) * K + d.k];
+        ny += (fl & 3) != 0;
+        nn += ((fl >> 2) & 3) != 0;
+        if (((fl & DANSE_FLAG_SOLVE) && !(fl & DANSE_FLAG_PREGIVEN)) || (ny > d.D && nn > d.D)) {
+          P = r;
+          break;
+        }
+      }
+    }
+    eng->ffPraw = (P < R && P >= 8) ? P : 0;
+    eng->ffP = eng->ffOk ? std::min(eng->ffPraw, eng->ffAlloc) : 0;
+  }
   for (auto& cl : eng->classes) {
     const int nn = (int)cl.host.size();
     cl.anySolve.assign(R, 0);
@@ -1038,6 +1068,25 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
     HIPCHK(hipMemcpy(eng->dTgtOff, tgtOff.data(), K * sizeof(long long), hipMemcpyHostToDevice));
   }
   {
+    // the prefix fast-forward: synchronous wholeChunk runs whose spectra the
+    // recursion reads straight (no lags, phases, raw frames), no per-round
+    // state beside the SCMs (CohDrift, DXCP, T(z) conv), the size classes'
+    // packed SCMs (no wide class, no split solves, the recursion-only
+    // variants on) -- DANSE_NO_FF=1: off
+    bool ok = !std::getenv("DANSE_NO_FF") && !eng->noRO && !eng->dZLag && !eng->dZPhase && !eng->dCEnd &&
+              !eng->dCPhase && !eng->cohDrift && !eng->dxcpOn && !eng->dFsTab && !eng->desConv &&
+              eng->wideIds.empty() && eng->ffPraw > 0;
+    for (const auto& cl : eng->classes) ok = ok && !cl.split;
+    for (const auto& fn : eng->fns) ok = ok && (fn.packed == 1 || fn.packed == 2) && fn.D <= 64;
+    if (ok) {
+      eng->ffAlloc = eng->ffPraw;
+      HIPCHK(dalloc(&eng->yHist, (size_t)eng->ffAlloc * S * eng->MT * F));
+      HIPCHK(dalloc(&eng->zHist, (size_t)eng->ffAlloc * K * S * F));
+      eng->ffOk = true;
+      eng->ffP = eng->ffPraw;
+    }
+  }
+  {
     int rc = danse_engine_reset(eng, nullptr);
     if (rc) return rc;
   }
@@ -1063,7 +1112,7 @@ void danse_engine_destroy(danse_engine* eng) {
                   eng->resUFlag, eng->resZFlag, eng->resGateRound, eng->resDanseFni, eng->resErr, eng->resFams,
                   eng->resFrames, eng->resChanNode, eng->resTrace, eng->condHist, eng->dxRecFrames,
                   eng->dxRecOut, eng->dFsEv, eng->rawStream, eng->vCache, eng->l64Cache, eng->lzStats,
-                  eng->dWideIds, eng->wideWork, eng->convIR, eng->dSnConv, eng->cCache};
+                  eng->dWideIds, eng->wideWork, eng->convIR, eng->dSnConv, eng->cCache, eng->yHist, eng->zHist};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (eng->dx) danse_dxcp_destroy(eng->dx);
@@ -1216,10 +1265,31 @@ static void launch_wide(danse_engine* e, int r, hipStream_t st, unsigned mask) {
   hipLaunchKernelGGL(wide_tail_kernel, dim3(F, S * nW), dim3(64), 0, st, a, e->dFnAll, e->dWideIds, nW);
 }
 
+static int ff_prefix(const danse_engine* e) { return e->condEvery == 0 ? e->ffP : 0; }
+
+// the prefix's recursion over every bin of every family-node (span.hpp)
+static void launch_span(danse_engine* e, hipStream_t st) {
+  for (auto& cl : e->classes) {
+    SpanArgs a{};
+    a.S = e->S; a.K = e->K; a.MT = e->MT; a.F = e->F; a.P = ff_prefix(e); a.nFN = (int)cl.host.size();
+    a.flags = e->dFlags; a.fn = cl.dev; a.chanList = e->dChan; a.yHist = e->yHist; a.zHist = e->zHist;
+    a.Ryy = e->Ryy; a.Rnn = e->Rnn; a.scmStride = e->scmStride; a.beta = e->dBeta;
+    launch_span_class(cl.DMAX, a, (unsigned)(e->S * a.nFN * e->F), st);
+  }
+}
+
 static void launch_update(danse_engine* e, int r, hipStream_t st, unsigned mask = ~0u, bool full = true) {
   if (!e->wideIds.empty()) launch_wide(e, r, st, mask);
+  const bool ff = r < ff_prefix(e) && mask == ~0u && full;
+  if (ff) {
+    // this round's update-frame and fused spectra into the histories
+    const size_t ny = (size_t)e->S * e->MT * e->F, nz = (size_t)e->K * e->S * e->F;
+    (void)copy_async(e->yHist + (size_t)r * ny, e->Yspec + (size_t)((r + 1) & 1) * ny, ny * sizeof(cf), st);
+    (void)copy_async(e->zHist + (size_t)r * nz, e->Zspec + (size_t)(r & 1) * nz, nz * sizeof(cf), st);
+  }
   for (auto& cl : e->classes) {
     UpdateArgs a = make_update(e, r);
+    a.noRec = ff ? 1 : 0;
     a.nodeMask = mask;
     a.nFN = (int)cl.host.size();
     a.fn = cl.dev;
@@ -1319,6 +1389,7 @@ static void launch_fs(danse_engine* e, int row, hipStream_t st) {
 // analysis alone (no local-frame analyses, no estimate synthesis)
 static void launch_bcast(danse_engine* e, int r, int synth, int bc, hipStream_t st, unsigned zMask = ~0u,
                          int zOnly = 0) {
+  if (bc && r > 0 && r == ff_prefix(e)) launch_span(e, st);   // (before round r's gate and update)
   if (e->desConv) synth = 0;   // ('conv': conv_d_kernel writes the estimates after each update)
   if (!synth && !bc) return;
   BcastArgs a = make_bcast(e, r, synth, bc);

@@ -97,6 +97,10 @@ struct UpdateArgs {
   // table): the recursion-only kernel variants run, not held to the solver's
   // registers / LDS
   int noSolve;
+  // pre-solve prefix fast-forward (span.hpp): this round's SCM recursion is
+  // deferred to span_rec_kernel; the recursion-only variants run their tail
+  // (filters, external filters, d-hat) only
+  int noRec;
   // fewSamples step lists (compile_rounds_fs): the nodes this launch updates
   // (bit k: node k); the others are left untouched
   unsigned nodeMask;

@@ -226,7 +226,8 @@ update_kernel_2d(const UpdateArgs a) {
 
   // ---- Rnn (float64): recursion, store, factor -> Li in S.Ls -------------
   bool ok = true;
-  if (opN || (solve && !reuse)) {
+  const bool rec = !(SM == 1 && a.noRec);   // (span.hpp: the prefix's recursion deferred)
+  if (rec && (opN || (solve && !reuse))) {
     BlkD<NB> M;
     const double cy = (opN == DANSE_OP_SET) ? 1.0 / D : (1.0 - beta) / D;
     const double cx = (opN == DANSE_OP_SET) ? 0.0 : beta;
@@ -292,7 +293,7 @@ update_kernel_2d(const UpdateArgs a) {
   // ---- Ryy (float32): recursion, store, filter ---------------------------
   cf w[V];
   sfor<0, V>([&](auto vc) { w[decltype(vc)::value] = cf{0.0f, 0.0f}; });
-  if (opY || solve) {
+  if (rec && (opY || solve)) {
     const float by = (float)beta, cy = (opY == DANSE_OP_SET) ? (float)(1.0 / D) : (float)((1.0 - beta) / D);
     auto ld_row_Ryy = [&](auto sc) {
       constexpr int sb = decltype(sc)::value;

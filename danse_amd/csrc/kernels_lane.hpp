@@ -71,7 +71,7 @@ __global__ void __launch_bounds__(64) update_kernel_lane(const UpdateArgs a) {
   __shared__ cf Gs[D][64];
 
   cf y[D];
-  if (opY || opN) {
+  if ((opY || opN) && !(RO && a.noRec)) {
     load_y_all<D>(a, d, s, f, y);
   }
   stamp(1);
@@ -105,7 +105,8 @@ __global__ void __launch_bounds__(64) update_kernel_lane(const UpdateArgs a) {
   // frame: the recursion, the store and the congruence share it)
   if constexpr (RO) {
     // one entry at a time (loads, recursion, store): no triangle is held
-    if (opY || opN) {
+    // (noRec: the prefix's recursion is deferred to span_rec_kernel)
+    if ((opY || opN) && !a.noRec) {
       const bool isY = opY != 0;
       const int op = isY ? opY : opN;
       const double cy = (op == DANSE_OP_SET) ? 1.0 / D : (1.0 - beta) / D;
