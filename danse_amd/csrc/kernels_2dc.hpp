@@ -87,6 +87,15 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NZ ? 2 
   __shared__ __attribute__((aligned(16))) char ldsRaw[lean_lds_bytes<NB, NZ>()];
   LDS2<NB, G>& S = *reinterpret_cast<LDS2<NB, G>*>(ldsRaw);   // (members up to the Lanczos basis)
   const int li = threadIdx.x, p = li / G, q = li % G;
+  // DANSE_STAMP builds (kernels_2d.hpp, scripts/update_trace.py): marks 0
+  // start, 1 y staged (VAD: the record landed), 2 VAD: C upper blocks /
+  // noise: the factor moved and cached, 3 noise: C loaded, 4 C moved and
+  // stored, 5 Lanczos, 6 w, 7 tail issued, 8 recursion and stores drained
+  unsigned long long tsv[kStampN];
+  auto stamp = [&](int i) {
+    if constexpr (DANSE_STAMP) tsv[i] = __builtin_amdgcn_s_memtime();
+  };
+  stamp(0);
   const int F = a.F;
   const int f = blockIdx.x % F;
   const int tt = (NZ ? a.cnItems : a.creItems)[blockIdx.x / F];
@@ -147,8 +156,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NZ ? 2 
   cf yc[NB];
   sfor<0, NB>([&](auto sc) { yc[decltype(sc)::value] = S.vb[q + G * decltype(sc)::value]; });
   wsync();
+  stamp(1);
   // (after the record's LDS-DMA drained: its last chunk runs into S.U)
   if constexpr (!NZ) c_fill_upper<NB>(A, S.U, li);
+  stamp(2);
 
   bool ok = true;
   if constexpr (!NZ) {
@@ -189,8 +200,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NZ ? 2 
     cd* l64 = a.l64Cache + (long long)s * a.l64Stride + d.l64Off + (long long)f * l64_record<NB, G>();
     ok = li_rank1_2d<NB, G>(S, li, yc, beta, cyN, l64, true);
     li_store2d<NB, G>(S, liC, li);
+    stamp(2);
     c_load_lower<NB>(A, cC);
     c_fill_upper<NB>(A, S.U, li);
+    stamp(3);
     // T's coefficients from li_rank1_2d's LDS (S.invd: a_i = alpha |p_i|^2,
     // S.rb64[0]: p_i): t_i = 1 + sum_(k < i) a_k, dd_i = sqrt(t_i / t_(i+1)),
     // pe_i = alpha p_i / sqrt(t_i t_(i+1)); this lane's rows i = p + G sb
@@ -261,6 +274,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NZ ? 2 
     }
   }
 
+  if constexpr (!NZ) stamp(3);
+  stamp(4);
   cf* vC = a.vCache + (long long)s * a.vStride + d.vOff + (long long)f * DM;
   cf vv[1];
   float lam1;
@@ -335,6 +350,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NZ ? 2 
     if (!ok && li == 0) atomicOr(&a.diag[(s * a.K + d.k) * kMaxFam + d.fam], 1);
   }
   const bool conv = lanczos2d<NB, G, lean_lz<NB, NZ>()>(A, S, li, D, vC, vv, lam1, warm);
+  stamp(5);
   if (!conv) {
     // (wave-uniform) fallback_kernel_2d writes this bin: a restart from this
     // attempt's Ritz vector, else the Householder path
@@ -348,10 +364,23 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NZ ? 2 
   }
   cf w[1];
   rank1_w2d<NB, G>(S, li, D, vv, lam1, w);
+  stamp(6);
   if (li < DM) vC[li] = vv[0];
   if (a.lzStats && li == 0) atomicAdd(&a.lzStats[((long long)(2 * r)) * kLzSlots + (blockIdx.x & (kLzSlots - 1))], 1);
   lean_tail<NB>(a, d, s, f, li, fl, w[0], y);
+  stamp(7);
   recursion();
+  if constexpr (DANSE_STAMP) {
+    __builtin_amdgcn_s_waitcnt(0);
+    stamp(8);
+    if (a.stamps && threadIdx.x <= kStampN) {
+      // lane i stores mark i (vector stores), lane kStampN the path code
+      // (128 lean, 256 noise frame, 32 Lanczos accepted)
+      unsigned long long v = 128ull | (NZ ? 256ull : 0ull) | 32ull;
+      sfor<0, kStampN>([&](auto ic) { v = (threadIdx.x == decltype(ic)::value) ? tsv[decltype(ic)::value] : v; });
+      a.stamps[(long long)blockIdx.x * (kStampN + 1) + threadIdx.x] = v;
+    }
+  }
 }
 
 // The warm solves update_kernel_2dc sent back: the Householder path

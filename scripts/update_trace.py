@@ -32,6 +32,10 @@ PHASES = ['y', 'Rnn', 'factor', 'Ryy', 'congr', 'solve', 'tail', 'drain']
 # frames), 3 factor (float64 Cholesky + inverse, or the cached factor into
 # LDS), 4 Ryy recursion, 5 congruence, 6 eigen part + filter, 7 / 8 as above
 PHASES_LANE = ['y', 'Rnn', 'factor', 'Ryy', 'congr', 'eigen', 'tail', 'drain']
+# update_kernel_2dc (code bit 128; 256 = the noise-frame variant): 1 y staged,
+# 2 C upper blocks (VAD) / factor moved + cached (noise), 3 C loaded (noise),
+# 4 C moved + stored, 5 Lanczos, 6 w, 7 tail issued, 8 recursion + drain
+PHASES_LEAN = ['y', 'Cfill/factor', 'Cload', 'Cmove', 'lanczos', 'w', 'tail', 'rec+drain']
 
 
 def main():
@@ -73,8 +77,9 @@ def main():
     for c in np.unique(code):
         sel = code == c
         bits = [nm for b, nm in ((1, 'noise'), (2, 'rank1'), (4, 'fullfactor'), (8, 'reuse'), (16, 'solve'),
-                                 (32, 'lz-ok'), (64, 'lz-back')) if c & b]
-        row = ' '.join(f'{nm} {np.mean(dt[sel, i]):7.0f}' for i, nm in enumerate(phases))
+                                 (32, 'lz-ok'), (64, 'lz-back'), (128, 'lean'), (256, 'noise-lean')) if c & b]
+        ph = PHASES_LEAN if c & 128 else phases
+        row = ' '.join(f'{nm} {np.mean(dt[sel, i]):7.0f}' for i, nm in enumerate(ph))
         print(f'code {c:3d} ({"+".join(bits) or "-"}): {sel.sum():6d} waves, life {np.mean(life[sel]):7.0f}: {row}')
     # concurrency: waves alive over the launch
     print('mean phase share of wave life:',
