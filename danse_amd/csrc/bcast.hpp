@@ -179,7 +179,7 @@ __global__ void __launch_bounds__(NW * 64) bcast_kernel(const BcastArgs a) {
       cf* dst = (kind == 2) ? a.Cspec + (((long long)(r & 1) * a.S + s) * a.MT + ch) * F
                             : a.Yspec + (((long long)((up ? r + 1 : r) & 1) * a.S + s) * a.MT + ch) * F;
       // (fewSamples: z comes from the T(z) chunk, no fused spectrum here)
-      const bool zk0 = kind == 0 && !a.fsTab && owned;
+      const bool zk0 = kind == 0 && !a.fsTab;   // (a foreign block's partial sums go unused)
       if (zk0) {
         cf w[16];   // the weights first, at clamped bins (hold())
 #pragma unroll
