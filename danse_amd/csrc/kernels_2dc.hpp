@@ -28,8 +28,11 @@ namespace danse {
 // Lanczos steps of the first attempt: kLz (8) on VAD frames; two more on the
 // noise frames, whose transform moves C further (most of the restarts were
 // there; the VAD variant would spill at its 3-waves-per-SIMD budget)
+#ifndef DANSE_LEAN_LZ_VAD_DELTA
+#define DANSE_LEAN_LZ_VAD_DELTA 0   // (A/B builds: steps added to kLz on VAD frames)
+#endif
 template <int NB, bool NZ>
-constexpr int lean_lz() { return t2d::kLz<8 * NB>() + (NZ ? 2 : 0); }
+constexpr int lean_lz() { return t2d::kLz<8 * NB>() + (NZ ? 2 : DANSE_LEAN_LZ_VAD_DELTA); }
 template <int NB, bool NZ = true>
 constexpr int lean_lds_bytes() {
   return (int)__builtin_offsetof(t2d::LDS2<NB>, U) + lean_lz<NB, NZ>() * 8 * NB * (int)sizeof(cf);
