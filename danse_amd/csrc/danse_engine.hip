@@ -1284,8 +1284,11 @@ static void launch_update(danse_engine* e, int r, hipStream_t st, unsigned mask 
   if (ff) {
     // this round's update-frame and fused spectra into the histories
     const size_t ny = (size_t)e->S * e->MT * e->F, nz = (size_t)e->K * e->S * e->F;
-    (void)copy_async(e->yHist + (size_t)r * ny, e->Yspec + (size_t)((r + 1) & 1) * ny, ny * sizeof(cf), st);
-    (void)copy_async(e->zHist + (size_t)r * nz, e->Zspec + (size_t)(r & 1) * nz, nz * sizeof(cf), st);
+    const size_t n = ny + nz;
+    const unsigned blocks = (unsigned)(n < (size_t)256 * 4096 ? (n + 255) / 256 : 4096);
+    hipLaunchKernelGGL(ff_copy_kernel, dim3(blocks), dim3(256), 0, st, e->yHist + (size_t)r * ny,
+                       e->Yspec + (size_t)((r + 1) & 1) * ny, ny, e->zHist + (size_t)r * nz,
+                       e->Zspec + (size_t)(r & 1) * nz, nz);
   }
   for (auto& cl : e->classes) {
     UpdateArgs a = make_update(e, r);

@@ -29,6 +29,17 @@ struct SpanArgs {
 
 constexpr int kSpanChunk = 16;    // rounds staged in LDS at once
 
+// a prefix round's two history copies in one launch (complex64 entries):
+// the update-frame spectra and the fused spectra
+__global__ void __launch_bounds__(256) ff_copy_kernel(cf* __restrict__ dy, const cf* __restrict__ sy, size_t ny,
+                                                      cf* __restrict__ dz, const cf* __restrict__ sz, size_t nz) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < ny + nz; i += stride) {
+    if (i < ny) dy[i] = sy[i];
+    else dz[i - ny] = sz[i - ny];
+  }
+}
+
 // one THREADS-thread workgroup per (scene, family-node, bin); thread t holds
 // the lower entries e = t + THREADS j (j < PER) of both SCMs for the whole
 // prefix; YW >= D (the staged observation rows)
