@@ -428,6 +428,8 @@ int danse_engine_reset(danse_engine* eng, void* stream) {
   HIPCHK(fill_async(eng->diag, 0, (size_t)S * K * kMaxFam * sizeof(int), st));
   if (eng->vCache) HIPCHK(fill_async(eng->vCache, 0, (size_t)S * eng->vStride * sizeof(cf), st));
   if (eng->lzStats) HIPCHK(fill_async(eng->lzStats, 0, (size_t)2 * eng->R * kLzSlots * sizeof(int), st));
+  for (auto& cl : eng->classes)
+    if (cl.dFbCount) HIPCHK(fill_async(cl.dFbCount, 0, (size_t)eng->R * sizeof(int), st));
   const int nFN = (int)eng->fns.size();
   hipLaunchKernelGGL(reset_fam_kernel, dim3(64, S * nFN), dim3(256), 0, st, eng->dFnAll, nFN, eng->dInitW0Off,
                      eng->dInitScmOff, eng->dW0, eng->dScm0, eng->wHist, eng->wStride, eng->Ryy, eng->Rnn,
@@ -1314,7 +1316,8 @@ static void launch_update(danse_engine* e, int r, hipStream_t st, unsigned mask 
     a.fbCount = cl.dFbCount;
     if (nCre + nCn < nItems) launch_update_class(cl.DMAX, a, st);   // D > kMaxDMax rejected at create time
     if (nCre + nCn > 0) {
-      (void)fill_async(cl.dFbCount + r, 0, sizeof(int), st);
+      // (one counter per round, zeroed by danse_engine_reset: each round's
+      // lean launch counts its own failed warm solves)
       launch_lean_solve_class(cl.DMAX, a, nCre, nCn, std::min((nCre + nCn) * e->F, 256), st);
     }
     if (cl.split && cl.solveCount[r] > 0) {
