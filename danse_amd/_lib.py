@@ -87,6 +87,7 @@ SIGNATURES = {
     'danse_engine_create': (_c_i32, [ctypes.POINTER(DanseCfg), _c_i32, ctypes.POINTER(ctypes.c_void_p)]),
     'danse_engine_destroy': (None, [ctypes.c_void_p]),
     'danse_last_error': (ctypes.c_char_p, [ctypes.c_void_p]),
+    'danse_mi355x_build_id': (ctypes.c_char_p, []),
     'danse_engine_set_inputs': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p]),
     'danse_engine_reset': (_c_i32, [ctypes.c_void_p, ctypes.c_void_p]),
     'danse_engine_run': (_c_i32, [ctypes.c_void_p, _c_i32, _c_i32, ctypes.c_void_p, _c_i32]),
@@ -192,6 +193,7 @@ def load_library(path: os.PathLike | None = None):
     if not p.exists():
         raise RuntimeError(f'{p} not found: build the HIP extension first (python -c "import __graft_entry__ as g; g.build()")')
     lib = ctypes.CDLL(str(p))
+    _check_build_id(lib, p)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.restype = res
@@ -199,6 +201,25 @@ def load_library(path: os.PathLike | None = None):
     if path is None:
         _lib = lib
     return lib
+
+
+def _check_build_id(lib, p: Path) -> None:
+    """The library must be the build of the sources next to it (build.py
+    embeds their hash).  Without sources (an installed copy) there is nothing
+    to compare.  DANSE_LIB points at A/B variants, which carry their own."""
+    from . import build as _b
+    if not _b.CSRC.exists():
+        return
+    fn = lib.danse_mi355x_build_id
+    fn.restype = ctypes.c_char_p
+    fn.argtypes = []
+    have = (fn() or b'').decode()
+    name = p.name
+    variant = name[len('libdanse_'):-3] if name.startswith('libdanse_') and name != LIB_NAME else None
+    want = _b.source_hash(variant if variant in _b.VARIANTS else None)
+    if have != want:
+        raise RuntimeError(f'{p} was built from other sources (build id {have[:16]}, sources {want[:16]}): '
+                           'rebuild it (python -c "import __graft_entry__ as g; g.build()")')
 
 
 class DanseError(RuntimeError):

@@ -13,6 +13,7 @@ box.
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import subprocess
 import sys
@@ -75,6 +76,34 @@ VARIANTS = {
 }
 
 
+MARK = b'DANSE_SRC_HASH:'
+
+
+def source_hash(variant: str | None = None) -> str:
+    """sha256 over every HIP / C++ source and header of the library, the
+    compile flags and the size classes.  build() embeds it in the library
+    (``danse_mi355x_build_id``); ``_lib.load_library`` refuses a library whose
+    id differs from the sources next to it, so a shipped ``.so`` is provably
+    the build of the shipped sources."""
+    h = hashlib.sha256()
+    files = sorted([*CSRC.glob('*.hip'), *CSRC.glob('*.hpp'), *INC.glob('*.h')])
+    for f in files:
+        h.update(f.name.encode())
+        h.update(f.read_bytes())
+    h.update(repr((FLAGS, CLASSES, VARIANTS.get(variant) if variant else None)).encode())
+    return h.hexdigest()
+
+
+def embedded_hash(lib: Path) -> str | None:
+    """The source hash a built library carries (None: none)."""
+    try:
+        b = lib.read_bytes()
+    except OSError:
+        return None
+    i = b.find(MARK)
+    return b[i + len(MARK):i + len(MARK) + 64].decode() if i >= 0 else None
+
+
 def _paths(variant):
     if variant is None:
         return OBJ, OUT
@@ -85,8 +114,7 @@ def up_to_date(variant: str | None = None) -> bool:
     obj, out = _paths(variant)
     if not out.exists():
         return False
-    t = out.stat().st_mtime
-    return all(not _stale(obj / o, s) and (obj / o).stat().st_mtime <= t for o, s, _ in _units())
+    return embedded_hash(out) == source_hash(variant)
 
 
 def build(force: bool = False, verbose: bool = True, jobs: int | None = None, variant: str | None = None) -> Path:
@@ -113,8 +141,16 @@ def build(force: bool = False, verbose: bool = True, jobs: int | None = None, va
     todo.sort(key=lambda it: -int(it[0][8:-2]) if it[0].startswith('update_d') else 0)
     with ThreadPoolExecutor(max_workers=n) as ex:
         list(ex.map(compile_one, todo))
+    # the build id: the source hash as a string and an exported C function
+    sh = source_hash(variant)
+    bid = obj / 'build_id.cpp'
+    bid.write_text('// generated by danse_amd/build.py\n'
+                   f'static const char kId[] = "{MARK.decode()}{sh}";\n'
+                   'extern "C" __attribute__((visibility("default"))) const char* danse_mi355x_build_id() '
+                   '{ return kId + ' + str(len(MARK)) + '; }\n')
+    subprocess.run(['g++', '-O2', '-fPIC', '-c', str(bid), '-o', str(obj / 'build_id.o')], check=True)
     cmd = [hipcc, '--offload-arch=gfx950', '-fPIC', '-shared', *[str(obj / o) for o, _, _ in _units()],
-           '-o', str(out) + '.tmp']
+           str(obj / 'build_id.o'), '-o', str(out) + '.tmp']
     if verbose:
         print(' '.join(cmd), flush=True)
     subprocess.run(cmd, check=True)

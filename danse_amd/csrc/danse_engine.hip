@@ -181,6 +181,9 @@ struct danse_engine {
   // only, their recursion in one span_rec_kernel before round ffP; ffPraw
   // from the flag table (build_split_lists), ffAlloc the histories' rounds
   int ffP = 0, ffPraw = 0, ffAlloc = 0;
+  // a launch error inside a launch helper that has no return path (the wide
+  // filter chunks): sticky until the next entry point reports it
+  hipError_t launchErr = hipSuccess;
   bool ffOk = false;
   cf *yHist = nullptr, *zHist = nullptr;
   double* condHist = nullptr;   // [S][nFN][R][F]
@@ -203,6 +206,14 @@ static int fail(danse_engine* eng, const std::string& m) {
   if (eng) eng->err = m;
   g_lastErr = m;
   return -1;
+}
+
+// the sticky launch error of a helper (launch_wide), reported once
+static int take_launch_err(danse_engine* eng) {
+  if (!eng || eng->launchErr == hipSuccess) return 0;
+  const hipError_t e = eng->launchErr;
+  eng->launchErr = hipSuccess;
+  return fail(eng, std::string("wide filter launch: ") + hipGetErrorString(e));
 }
 
 static void pick_class(int D, int& G, int& DMAX) {
@@ -429,7 +440,7 @@ int danse_engine_reset(danse_engine* eng, void* stream) {
   if (eng->vCache) HIPCHK(fill_async(eng->vCache, 0, (size_t)S * eng->vStride * sizeof(cf), st));
   if (eng->lzStats) HIPCHK(fill_async(eng->lzStats, 0, (size_t)2 * eng->R * kLzSlots * sizeof(int), st));
   for (auto& cl : eng->classes)
-    if (cl.dFbCount) HIPCHK(fill_async(cl.dFbCount, 0, (size_t)eng->R * sizeof(int), st));
+    if (cl.dFbCount) HIPCHK(fill_async(cl.dFbCount, 0, ((size_t)eng->R + 1) * sizeof(int), st));
   const int nFN = (int)eng->fns.size();
   hipLaunchKernelGGL(reset_fam_kernel, dim3(64, S * nFN), dim3(256), 0, st, eng->dFnAll, nFN, eng->dInitW0Off,
                      eng->dInitScmOff, eng->dW0, eng->dScm0, eng->wHist, eng->wStride, eng->Ryy, eng->Rnn,
@@ -860,8 +871,8 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
         cl.leanNoise = !std::getenv("DANSE_NO_LEAN_NOISE");
         for (int i = 0; i < S * K; ++i) cl.leanNoise = cl.leanNoise && c->beta[i] > 0.0;
         HIPCHK(dalloc(&cl.dFbList, (size_t)S * cl.host.size() * F));
-        HIPCHK(dalloc(&cl.dFbCount, (size_t)R));
-        HIPCHK(hipMemset(cl.dFbCount, 0, (size_t)R * sizeof(int)));
+        HIPCHK(dalloc(&cl.dFbCount, (size_t)R + 1));   // (+1: fallback_kernel_2d's done counter)
+        HIPCHK(hipMemset(cl.dFbCount, 0, ((size_t)R + 1) * sizeof(int)));
       }
     }
     if (int rc = build_split_lists(eng, c->flags)) return rc;
@@ -1080,12 +1091,18 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
               eng->wideIds.empty() && eng->ffPraw > 0;
     for (const auto& cl : eng->classes) ok = ok && !cl.split;
     for (const auto& fn : eng->fns) ok = ok && (fn.packed == 1 || fn.packed == 2) && fn.D <= 64;
-    if (ok) {
-      eng->ffAlloc = eng->ffPraw;
+    // the histories' byte budget (DANSE_FF_MB, default 4096 MB): a longer
+    // prefix is cut to the rounds that fit, the rest run per round
+    const size_t perRound = ((size_t)S * eng->MT * F + (size_t)K * S * F) * sizeof(cf);
+    const char* fb = std::getenv("DANSE_FF_MB");
+    const size_t budget = (size_t)(fb ? std::max(0, std::atoi(fb)) : 4096) << 20;
+    const int fit = (int)std::min<size_t>((size_t)eng->ffPraw, budget / perRound);
+    if (ok && fit > 0) {
+      eng->ffAlloc = fit;
       HIPCHK(dalloc(&eng->yHist, (size_t)eng->ffAlloc * S * eng->MT * F));
       HIPCHK(dalloc(&eng->zHist, (size_t)eng->ffAlloc * K * S * F));
       eng->ffOk = true;
-      eng->ffP = eng->ffPraw;
+      eng->ffP = std::min(eng->ffPraw, eng->ffAlloc);
     }
   }
   {
@@ -1262,7 +1279,8 @@ static void launch_wide(danse_engine* e, int r, hipStream_t st, unsigned mask) {
     wa.work = e->wideWork;
     wa.flags = e->dFlags + ((size_t)r * S * kMaxFam + fn.fam) * K + fn.k;
     wa.flagStride = (long long)kMaxFam * K;
-    (void)wide::launch_wide_filters(wa, e->wideChunk, st);
+    const hipError_t le = wide::launch_wide_filters(wa, e->wideChunk, st);
+    if (le != hipSuccess && e->launchErr == hipSuccess) e->launchErr = le;
   }
   hipLaunchKernelGGL(wide_tail_kernel, dim3(F, S * nW), dim3(64), 0, st, a, e->dFnAll, e->dWideIds, nW);
 }
@@ -1316,8 +1334,9 @@ static void launch_update(danse_engine* e, int r, hipStream_t st, unsigned mask 
     a.fbCount = cl.dFbCount;
     if (nCre + nCn < nItems) launch_update_class(cl.DMAX, a, st);   // D > kMaxDMax rejected at create time
     if (nCre + nCn > 0) {
-      // (one counter per round, zeroed by danse_engine_reset: each round's
-      // lean launch counts its own failed warm solves)
+      // (one counter per round: each round's lean launch counts its own
+      // failed warm solves, and its fallback launch zeroes the counter when
+      // its last block is done)
       launch_lean_solve_class(cl.DMAX, a, nCre, nCn, std::min((nCre + nCn) * e->F, 256), st);
     }
     if (cl.split && cl.solveCount[r] > 0) {
@@ -1488,7 +1507,7 @@ int danse_engine_update(danse_engine* eng, int32_t r, void* stream) {
   else
     launch_update(eng, r, (hipStream_t)stream);
   HIPCHK(hipGetLastError());
-  return 0;
+  return take_launch_err(eng);
 }
 
 int danse_engine_run_steps(danse_engine* eng, int32_t s0, int32_t s1, void* stream) {
@@ -1499,7 +1518,7 @@ int danse_engine_run_steps(danse_engine* eng, int32_t s0, int32_t s1, void* stre
   HIPCHK(hipSetDevice(eng->dev));
   run_fs_steps(eng, s0, s1, (hipStream_t)stream);
   HIPCHK(hipGetLastError());
-  return 0;
+  return take_launch_err(eng);
 }
 
 int danse_engine_finish(danse_engine* eng, void* stream) {
@@ -1531,7 +1550,7 @@ int danse_engine_run(danse_engine* eng, int32_t r0, int32_t r1, void* stream, in
   if (!graph) {
     seq(st);
     HIPCHK(hipGetLastError());
-    return 0;
+    return take_launch_err(eng);
   }
   if (!(eng->graphExec && eng->graphR0 == r0 && eng->graphR1 == r1)) {
     if (eng->graphExec) {
@@ -1548,6 +1567,11 @@ int danse_engine_run(danse_engine* eng, int32_t r0, int32_t r1, void* stream, in
     HIPCHK(hipStreamBeginCapture(cap, hipStreamCaptureModeThreadLocal));
     seq(cap);
     HIPCHK(hipStreamEndCapture(cap, &g));
+    if (eng->launchErr != hipSuccess) {
+      (void)hipGraphDestroy(g);
+      if (own) (void)hipStreamDestroy(cap);
+      return take_launch_err(eng);
+    }
     HIPCHK(hipGraphInstantiate(&eng->graphExec, g, nullptr, nullptr, 0));
     HIPCHK(hipGraphDestroy(g));
     if (own) HIPCHK(hipStreamDestroy(cap));

@@ -432,6 +432,16 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) fa
     }
     lean_tail<NB>(a, d, s, f, li, fl, w[0], y);
   }
+  // the last block to finish has seen every block read n: it zeroes this
+  // round's counter (and the done counter fbCount[R]), so a later run without
+  // danse_engine_reset starts from an empty list
+  if (li == 0) {
+    __threadfence();
+    if (atomicAdd(&a.fbCount[a.R], 1) == (int)gridDim.x - 1) {
+      atomicExch(&a.fbCount[r], 0);
+      atomicExch(&a.fbCount[a.R], 0);
+    }
+  }
 }
 
 }  // namespace danse

@@ -27,7 +27,9 @@ __global__ void __launch_bounds__(64) update_kernel_big(const UpdateArgs a) {
   const bool act = li < D;
   const int r = a.r;
   const uint8_t fl = a.flags[(((long long)r * a.S + s) * kMaxFam + d.fam) * a.K + d.k];
-  const int opY = fl & 3, opN = (fl >> 2) & 3;
+  // noRec: a prefix round (span.hpp) -- its recursion is deferred to
+  // span_rec_kernel, this launch runs the tail only (no item solves there)
+  const int opY = a.noRec ? 0 : (fl & 3), opN = a.noRec ? 0 : ((fl >> 2) & 3);
   const bool solve = (fl & DANSE_FLAG_SOLVE) != 0;
 
   const cf y = load_y(a, d, s, f, li, act);

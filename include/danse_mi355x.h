@@ -180,6 +180,9 @@ enum danse_output {
 int danse_engine_create(const danse_cfg* cfg, int device, danse_engine** out);
 void danse_engine_destroy(danse_engine* eng);
 const char* danse_last_error(const danse_engine* eng);   /* eng may be NULL */
+/* sha256 (hex) of the sources and flags this library was built from
+ * (danse_amd/build.py source_hash); the Python side refuses a mismatch. */
+const char* danse_mi355x_build_id(void);
 
 /* Re-initialise all state (filters, SCMs, z streams, estimates) to the
  * configured initial values, asynchronously on `stream` (NULL: synchronous). */

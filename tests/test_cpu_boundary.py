@@ -169,3 +169,13 @@ def test_get_metrics_rejects_metrics_off_the_device_path():
             DM.get_metrics(x, x, x, x, x, metricsToPlot=m)
     with pytest.raises(NotImplementedError):
         DM.get_metrics(x, x, x, x, x, metricsToPlot=['snr'], dynamic=object())
+
+
+def test_library_build_id_matches_sources():
+    """The shipped library is the build of the shipped sources: build.py
+    embeds the sources' hash, _lib refuses a mismatch."""
+    from danse_amd import build as B
+    from danse_amd import _lib as L
+    lib = L.load_library()
+    assert lib.danse_mi355x_build_id().decode() == B.source_hash()
+    assert B.embedded_hash(L.LIB_PATH) == B.source_hash()

@@ -19,6 +19,14 @@ pytest.importorskip('torch')
 
 CASES = [c for c in ONLINE_CASES if c['name'] in ('online_B_k4m3_asy', 'online_B_k4m3_seq', 'online_ragged_asy_r2')]
 CASES.append(dict(name='online_K8x4_asy_4s', M=[4] * 8, dur=4.0, seed=31, danse=dict(BATTERY, nodeUpdating='asy')))
+# the row-per-lane classes (update_kernel_big: the MWF above D = 12, the GEVD
+# of D 49..64) without the first-frame basis: the random init is then
+# averaged from round 0, so a prefix round that ran the recursion in place
+# AND was replayed by span_rec_kernel would decay the SCMs twice
+CASES.append(dict(name='online_big_D20_mwf_nobasis', M=[17, 4, 4, 5], dur=3.0, seed=23,
+                  danse=dict(BATTERY, nodeUpdating='asy', performGEVD=False, use1stFrameAsBasis=False)))
+CASES.append(dict(name='online_big_D51_nobasis', M=[48, 2, 2, 2], dur=4.0, seed=25,
+                  danse=dict(BATTERY, nodeUpdating='asy', use1stFrameAsBasis=False)))
 
 
 def _run(case, ff):
