@@ -141,6 +141,16 @@ def update_kernel_name(Dmax, gevd=True):
     return 'update_kernel_2d' if (gevd and Dmax <= 48) else 'update_kernel_big'
 
 
+def update_kernel_mix(Dmax, gevd=True):
+    """The kernels one solve round's update launches run at filter size Dmax
+    (danse_engine.hip launch_update): the lean cached-C solves of the 8 x 8
+    grid classes (DMAX 24-48, rank 1) sit beside the full kernel."""
+    k = update_kernel_name(Dmax, gevd)
+    if k == 'update_kernel_2d' and Dmax > 20:
+        return 'update_kernel_2d + update_kernel_2dc<VAD> + update_kernel_2dc<noise> + fallback_kernel_2d'
+    return k
+
+
 def alg_bytes_update(D, opY, opN, solve):
     """Algorithmic HBM bytes of one node x bin x frame of update_kernel,
     SURVEY §8d (complex64, packed Hermitian: one SCM one way = 4 D(D+1) B):
@@ -214,6 +224,7 @@ def main():
                     help='N=1, workload B: skip the extra single-WASN lines (B at S=1, N2 K=32x8 at S=1)')
     ap.add_argument('--cpu-only', action='store_true', help=argparse.SUPPRESS)
     ap.add_argument('--rounds', type=int, default=None, help=argparse.SUPPRESS)
+    ap.add_argument('--cpu-seed', type=int, default=1000, help=argparse.SUPPRESS)
     ap.add_argument('--pmc-child', action='store_true', help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.L is not None:
@@ -233,7 +244,7 @@ def main():
             print(json.dumps(cpu_baseline_batch(wl['M'], wl, dp, wp, args.cpu_seconds)))
             return
         dp, wp = _wl_params(wl)
-        print(json.dumps(cpu_baseline(wl['M'], wl, dp, wp, args.cpu_seconds, args.rounds)))
+        print(json.dumps(cpu_baseline(wl['M'], wl, dp, wp, args.cpu_seconds, args.rounds, seed=args.cpu_seed)))
         return
 
     import torch
@@ -273,16 +284,24 @@ def main():
         # D (batch K = 32 x 8, 20 iterations) and E at the battery's SRO
         # setting (K = 2, MK = [2, 3], fewSamples L = 64, 512 scenes)
         extra['C_dxcp'] = run_online(args, WORKLOADS['C_dxcp'], WORKLOADS['C_dxcp']['scenes'], rank, world, local,
-                                     dist, traffic=False)
+                                     dist)
         extra['D'] = run_batch(args, WORKLOADS['D'], 1, rank, world, local, dist)
         extra['E_L64_sro200'] = run_online(args, WORKLOADS['E_L64_sro200'], 512, rank, world, local, dist,
                                            traffic=False)
+        # the battery's cell as the battery configures it (local and
+        # centralised families on, Oracle compensation with flags; FU counts
+        # the DANSE family, the other families are extra solves)
+        extra['E_comp'] = run_online(args, WORKLOADS['E_comp'], 512, rank, world, local, dist, traffic=False)
     cpu = {}
     if rank == 0 and not args.no_cpu_baseline:
         cpu[args.workload] = cpu_child(args.workload, args.cpu_seconds, res['rounds'])
-        for key in ('N2', 'C_dxcp', 'D', 'E_L64_sro200'):
+        for key in ('N2', 'C_dxcp', 'D', 'E_L64_sro200', 'E_comp'):
             if key in extra:
                 cpu[key] = cpu_child(key, args.cpu_seconds, extra[key].get('rounds'))
+        for key in ('E_L64_sro200', 'E_comp'):
+            # for E also a P-process scene-parallel CPU leg
+            if key in extra and cpu.get(key) and 'value' in cpu[key]:
+                cpu[key]['scene_parallel'] = cpu_parallel(key, args.cpu_seconds, extra[key].get('rounds'))
     if rank == 0:
         line = {
             'metric': 'DANSE frame-updates/sec (nodes x bins)',
@@ -337,6 +356,43 @@ def cpu_child(workload, seconds, rounds):
         return json.loads(cp.stdout.strip().splitlines()[-1])
     except Exception:
         return {'error': (cp.stderr or '')[-500:]}
+
+
+def cpu_parallel(workload, seconds, rounds):
+    """The scene-parallel CPU leg: P = the host's
+    CPU share (affinity, capped by the thread-count env the box sets) single-
+    threaded oracle processes, each on its own scene seed, run at once; the
+    aggregate is the sum of their frame-update rates over the common wall."""
+    import subprocess
+    cores, threads, env0 = _threads()
+    P = max(1, threads)
+    env = dict(os.environ, HIP_VISIBLE_DEVICES='', CUDA_VISIBLE_DEVICES='', ROCR_VISIBLE_DEVICES='',
+               OMP_NUM_THREADS='1', OPENBLAS_NUM_THREADS='1', MKL_NUM_THREADS='1')
+    for k in ('RANK', 'WORLD_SIZE', 'LOCAL_RANK'):
+        env.pop(k, None)
+    t0 = time.perf_counter()
+    procs = []
+    for i in range(P):
+        cmd = [sys.executable, str(ROOT / 'bench.py'), '--cpu-only', '--workload', workload, '--cpu-seconds',
+               str(seconds), '--cpu-seed', str(1000 + i), *_CHILD_ARGS]
+        if rounds is not None:
+            cmd += ['--rounds', str(rounds)]
+        procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    vals, errs = [], []
+    for pr in procs:
+        o, e = pr.communicate()
+        try:
+            vals.append(json.loads(o.strip().splitlines()[-1])['value'])
+        except Exception:
+            errs.append((e or '')[-200:])
+    wall = time.perf_counter() - t0
+    if not vals:
+        return {'error': errs[:1]}
+    return {'value': float(np.sum(vals)), 'unit': 'frame-updates/s', 'cores': P, 'processes': len(vals),
+            'kind': 'port', 'per_process_median': float(np.median(vals)), 'wall_s': wall,
+            'sample': f'{len(vals)} concurrent single-threaded float64 oracle processes (scene seeds 1000..'
+                      f'{1000 + P - 1}), each timed as the one-process leg; value = the sum of their rates; host '
+                      f'affinity {cores} cpus, thread env {env0 or "unset"}'}
 
 
 def run_online(args, wl, S, rank, world, local, dist, traffic=True, pmc_child=False, small_grid=False, resident=False):
@@ -494,7 +550,14 @@ def run_online(args, wl, S, rank, world, local, dist, traffic=True, pmc_child=Fa
 
     tr = None
     if traffic and rank == 0 and world == 1 and not args.no_traffic:
-        tr = pmc_traffic(wl, S, 'update_kernel', dom if not resident else None)
+        # (the round groups need one broadcast dispatch per round: wholeChunk)
+        fs = wl.get('extra', {}).get('broadcastType') == 'fewSamples'
+        if resident:
+            tr = pmc_traffic(wl, S, 'resident_kernel')
+        elif fs:
+            tr = pmc_traffic(wl, S, 'update_kernel', dom)
+        else:
+            tr = pmc_traffic(wl, S, None, dom)
     valu = max(Dk) > VALU_RIDGE_D
     roof = {'bound': 'valu' if valu else 'hbm',
             'achieved': tfs if valu else gbs,
@@ -505,9 +568,10 @@ def run_online(args, wl, S, rank, world, local, dist, traffic=True, pmc_child=Fa
             'traffic_detail': tr,
             'kernel': ('resident_kernel (one persistent launch per run; achieved = all rounds\' algorithmic bytes '
                        '/ the run)' if resident else
+                       'the update launches of the solve rounds (' +
                        ('update_kernel_2d (4 x 4 grid)' if small_grid and max(Dk) <= 12
-                        else update_kernel_name(max(Dk), gevd=bool(wl.get('gevd', True))))
-                       + f', solve rounds ({int(dom.sum())} of {R})'),
+                        else update_kernel_mix(max(Dk), gevd=bool(wl.get('gevd', True))))
+                       + f'), {int(dom.sum())} of {R} rounds; the measured dispatch mix in traffic_detail.kernel_mix'),
             'avg_launch_ms': avg_ms,
             'alg_bytes_per_launch': float(byts[dom].mean()), 'alg_flops_per_launch': float(flops[dom].mean()),
             'bytes_model': 'SURVEY §8d: complex64 packed Hermitian SCMs (achieved); storage_* = the engine\'s '
@@ -688,7 +752,15 @@ def pmc_traffic(wl, S, kernel_substr, rounds=None):
     """HBM bytes per launch of the dominant kernel from two rocprofv3 PMC
     passes over the same workload (MI355X_MICROARCH.md, HBM section):
     FETCH_SIZE and WRITE_SIZE (KiB) in separate passes, FETCH_SIZE doubled
-    (gfx950 reports half the bytes of a wide streaming read)."""
+    (gfx950 reports half the bytes of a wide streaming read).
+
+    kernel_substr None: the per-round update group, exactly what the HIP
+    events of run_online bracket (danse_engine_update: the class launches,
+    the lean cached-C solves, their fallback launch, ff copies and the
+    per-round estimators) -- in the un-graphed pass every dispatch between
+    round r's bcast_kernel and round r + 1's, gate checks excluded; the
+    counters are summed per round and averaged over the rounds mask.  The
+    kernel mix of those rounds (dispatches per kernel) comes back with it."""
     import csv
     import shutil
     import subprocess
@@ -697,6 +769,7 @@ def pmc_traffic(wl, S, kernel_substr, rounds=None):
     if exe is None:
         return None
     out = {}
+    mix = None
     tmp = tempfile.mkdtemp(prefix='danse_pmc_')
     env = dict(os.environ, TMPDIR=os.environ.get('TMPDIR', '/tmp'))
     for counter in ('FETCH_SIZE', 'WRITE_SIZE'):
@@ -709,24 +782,53 @@ def pmc_traffic(wl, S, kernel_substr, rounds=None):
         except Exception as e:   # profiler unavailable or refused: report null, never fail the bench
             return {'error': f'{counter}: {type(e).__name__}'}
         files = [os.path.join(r, f) for r, _, fs in os.walk(d) for f in fs if f.endswith('counter_collection.csv')]
-        rows = [row for fn in files for row in csv.DictReader(open(fn))
-                if row['Counter_Name'] == counter and kernel_substr in row['Kernel_Name']]
-        if not rows:
-            return {'error': f'{counter}: no samples'}
-        if 'Dispatch_Id' in rows[0]:
+        rows = [row for fn in files for row in csv.DictReader(open(fn)) if row['Counter_Name'] == counter]
+        if rows and 'Dispatch_Id' in rows[0]:
             rows.sort(key=lambda row: int(row['Dispatch_Id']))
-        vals = np.array([float(row['Counter_Value']) * 1024.0 for row in rows])
-        # (one update dispatch per round in the un-graphed pass: the rounds
-        # mask picks the solve rounds the roofline's duration is taken over)
-        if rounds is not None and len(vals) == len(rounds):
-            vals = vals[np.asarray(rounds, dtype=bool)]
+        if kernel_substr is None:
+            # group by round: a bcast_kernel dispatch opens each round
+            groups, names, cur = [], [], None
+            for row in rows:
+                kn = row['Kernel_Name']
+                if 'bcast_kernel' in kn:
+                    cur = [0.0]
+                    groups.append(cur)
+                    names.append([])
+                    continue
+                if cur is None or 'gate_kernel' in kn or 'span_rec' in kn:
+                    continue
+                cur[0] += float(row['Counter_Value']) * 1024.0
+                names[-1].append(kn.split('(')[0].replace('void ', '').strip())
+            nR = len(rounds) if rounds is not None else len(groups) - 1
+            if len(groups) < nR or nR == 0:
+                return {'error': f'{counter}: {len(groups)} broadcast dispatches for {nR} rounds'}
+            m = np.asarray(rounds, dtype=bool) if rounds is not None else np.ones(nR, dtype=bool)
+            vals = np.array([g[0] for g in groups[:nR]])[m]
+            if mix is None:
+                mix = {}
+                for r in np.nonzero(m)[0]:
+                    for kn in names[r]:
+                        mix[kn] = mix.get(kn, 0) + 1
+        else:
+            rows = [row for row in rows if kernel_substr in row['Kernel_Name']]
+            if not rows:
+                return {'error': f'{counter}: no samples'}
+            vals = np.array([float(row['Counter_Value']) * 1024.0 for row in rows])
+            # (one update dispatch per round in the un-graphed pass: the rounds
+            # mask picks the solve rounds the roofline's duration is taken over)
+            if rounds is not None and len(vals) == len(rounds):
+                vals = vals[np.asarray(rounds, dtype=bool)]
         out[counter] = float(np.mean(vals))
         out['dispatches'] = int(len(vals))
     shutil.rmtree(tmp, ignore_errors=True)
     b = 2.0 * out['FETCH_SIZE'] + out['WRITE_SIZE']
-    return {'bytes_per_launch': b, 'fetch_bytes_raw': out['FETCH_SIZE'], 'write_bytes': out['WRITE_SIZE'],
-            'dispatches': out['dispatches'], 'method': 'rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, '
-            'FETCH_SIZE x2 (gfx950)'}
+    res = {'bytes_per_launch': b, 'fetch_bytes_raw': out['FETCH_SIZE'], 'write_bytes': out['WRITE_SIZE'],
+           'dispatches': out['dispatches'], 'method': 'rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, '
+           'FETCH_SIZE x2 (gfx950)' + ('; summed over each round\'s update group (the HIP-event span), averaged '
+                                       'over the same rounds' if kernel_substr is None else '')}
+    if mix is not None:
+        res['kernel_mix'] = dict(sorted(mix.items(), key=lambda kv: -kv[1]))
+    return res
 
 
 def ctypes_void(p):
@@ -758,7 +860,7 @@ def _threads():
     return cores, (min([cores] + lim) if lim else cores), env
 
 
-def cpu_baseline(M, wl, dp, wp, seconds, rounds=None):
+def cpu_baseline(M, wl, dp, wp, seconds, rounds=None, seed=1000):
     """The float64 CPU oracle (oracle/danse_ref_cpu.py: the reference's
     per-frame NumPy/SciPy algorithm, per-bin scipy.linalg.eigh(Ryy, Rnn))
     timed on this host, one process, BLAS/OpenMP at their default threads
@@ -782,7 +884,7 @@ def cpu_baseline(M, wl, dp, wp, seconds, rounds=None):
     rate is, if anything, over-stated."""
     from danse_amd.scene import make_scene
     from oracle import danse_ref_cpu as O
-    sc = make_scene(M, sigDur=wl['dur'], seed=1000, SROperNode=wl.get('sros'))
+    sc = make_scene(M, sigDur=wl['dur'], seed=seed, SROperNode=wl.get('sros'))
     sc.get_vad_per_frame(dp.DFTsize, dp.Ns, wp.vadMinProportionActive)
     K, F = len(M), dp.DFTsize // 2 + 1
     D = max(M) + K - 1
@@ -855,7 +957,7 @@ def cpu_baseline(M, wl, dp, wp, seconds, rounds=None):
     cores, threads, env = _threads()
     return {'value': K * F * R / total, 'unit': 'frame-updates/s', 'cores': threads, 'kind': 'port',
             'sample': f'float64 oracle (reference algorithm, per-bin scipy eigh), one process, default BLAS threads '
-                      f'({env or "no thread env set"}), scene seed 1000, {method}; {sampled:.1f} s sampled; '
+                      f'({env or "no thread env set"}), scene seed {seed}, {method}; {sampled:.1f} s sampled; '
                       f'whole run projected over {R} rounds: {total:.1f} s; host affinity {cores} cpus',
             't_round_s': t_round, 't_solve_node_s': t_solve, 't_solve_sample_s': t_solve_sample,
             'gate_rounds': [int(starts.min()), int(starts.max())], 'projected_run_s': total}
