@@ -216,8 +216,17 @@ static int take_launch_err(danse_engine* eng) {
   return fail(eng, std::string("wide filter launch: ") + hipGetErrorString(e));
 }
 
+// The size class a filter dimension runs on: class_dmax, except that
+// DANSE_D20_ON_G8=1 moves D 17..20 from the 4 x 4 grid class 20 (four bins per
+// wave) to the 8 x 8 grid class 24 (one bin per wave), which carries the
+// float64 factor records and the lean cached-C solves (A/B)
+static int eng_class_dmax(int D) {
+  const char* e = std::getenv("DANSE_D20_ON_G8");
+  const bool g8 = e && std::atoi(e) != 0;
+  return (g8 && D > 16 && D <= 20) ? 24 : class_dmax(D);
+}
 static void pick_class(int D, int& G, int& DMAX) {
-  DMAX = class_dmax(D);
+  DMAX = eng_class_dmax(D);
   G = class_group(DMAX);
 }
 // (G = 1: lane kernels on packed SCMs; 16: lane groups; 64: one bin per wave)
@@ -716,30 +725,30 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
         // (no factor caches: the wide solve factors every time)
       } else if (c->gevd && fn.packed == 1)
         liOff += (long long)F * std::max<long long>(fn.D * (fn.D + 1) / 2 + fn.D,
-                                                    class_split(class_dmax(fn.D)) ? class_split_li_record() : 0);
+                                                    class_split(eng_class_dmax(fn.D)) ? class_split_li_record() : 0);
       else if (c->gevd && gridSmall) liOff += (long long)F * class_li_record(16);
-      else if (c->gevd && class_grid(class_dmax(fn.D)) > 0) liOff += (long long)F * class_li_record(class_dmax(fn.D));
+      else if (c->gevd && class_grid(eng_class_dmax(fn.D)) > 0) liOff += (long long)F * class_li_record(eng_class_dmax(fn.D));
       fn.vOff = -1;
       fn.l64Off = -1;
       // float64 factor records (li_rank1_2d) of the one-bin-per-wave grid
       // classes (DMAX 24-48; at G = 4, DMAX <= 20, the O(D^3) factor is short
       // and the update measured slower: C 360 -> 372 us, N2 263 -> 255 us)
-      if (!wideFn && c->gevd && fn.packed == 2 && !gridSmall && class_grid(class_dmax(fn.D)) > 0 &&
-          class_dmax(fn.D) >= 24 && !std::getenv("DANSE_NO_R1")) {
-        const int DMr = class_dmax(fn.D);
+      if (!wideFn && c->gevd && fn.packed == 2 && !gridSmall && class_grid(eng_class_dmax(fn.D)) > 0 &&
+          eng_class_dmax(fn.D) >= 24 && !std::getenv("DANSE_NO_R1")) {
+        const int DMr = eng_class_dmax(fn.D);
         fn.l64Off = l64Off;
         l64Off += (long long)F * (DMr * (DMr + 1) / 2 + DMr);
       }
       // (grid classes of 20 and more: solver2d.hpp gevd2d_filter)
-      if (!wideFn && warm && fn.packed == 2 && !gridSmall && class_grid(class_dmax(fn.D)) > 0 && class_dmax(fn.D) >= 20) {
+      if (!wideFn && warm && fn.packed == 2 && !gridSmall && class_grid(eng_class_dmax(fn.D)) > 0 && eng_class_dmax(fn.D) >= 20) {
         fn.vOff = vOff;
-        vOff += (long long)F * class_dmax(fn.D);
+        vOff += (long long)F * eng_class_dmax(fn.D);
       }
       // C = Li Ryy Li^H per bin (kernels_2d.hpp): the 8 x 8 grid classes with
       // the warm start and the float64 factor record (DANSE_NO_CCACHE=1: off)
       fn.cOff = -1;
-      if (fn.vOff >= 0 && fn.l64Off >= 0 && class_grid(class_dmax(fn.D)) == 8 && !std::getenv("DANSE_NO_CCACHE")) {
-        const long long nb = class_dmax(fn.D) / 8;
+      if (fn.vOff >= 0 && fn.l64Off >= 0 && class_grid(eng_class_dmax(fn.D)) == 8 && !std::getenv("DANSE_NO_CCACHE")) {
+        const long long nb = eng_class_dmax(fn.D) / 8;
         fn.cOff = cOff;
         cOff += (long long)F * nb * (nb + 1) / 2 * 64;   // (kernels_2d.hpp c_record)
       }

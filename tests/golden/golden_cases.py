@@ -72,6 +72,17 @@ ONLINE_CASES = [
     dict(name='online_C_cohdrift_asy', M=[2, 3, 2], dur=3.0, seed=15, sros=[0, 60, 120],
          danse=_d(BATTERY, nodeUpdating='asy', compensateSROs=True, includeFSDflags=True, estimateSROs='CohDrift',
                   cohDrift=dict(estimationMethod='ls'))),
+    # the open loop (cohDrift.loop 'open', d_classes.py:2439-2450,2580-2584):
+    # the coherence of the UNcompensated observation, the residual phase
+    # corrected by the full-sample-drift flags of the last segLength rounds
+    # (d_sros.py:19-95), the residual itself as the estimate
+    dict(name='online_C_cohdrift_open_asy', M=[2, 3, 2], dur=3.0, seed=15, sros=[0, 60, 120],
+         danse=_d(BATTERY, nodeUpdating='asy', compensateSROs=True, includeFSDflags=True, estimateSROs='CohDrift',
+                  cohDrift=dict(estimationMethod='ls', loop='open'))),
+    # CohDrift under sequential node updating (closed loop)
+    dict(name='online_C_cohdrift_seq', M=[2, 2, 3], dur=3.0, seed=23, sros=[0, 80, 160],
+         danse=_d(BATTERY, nodeUpdating='seq', compensateSROs=True, includeFSDflags=True, estimateSROs='CohDrift',
+                  cohDrift=dict(estimationMethod='ls'))),
     dict(name='online_C_sro_noflags_seq', M=[2, 2, 2, 2], dur=3.0, seed=9, sros=[50, 0, 200, 120],
          danse=_d(BATTERY, nodeUpdating='seq', compensateSROs=True, includeFSDflags=False, estimateSROs='Oracle')),
     # config E shape (tests/battery20230919_perf_asfctofL.py:14-110): MK = [2, 3],
@@ -323,7 +334,7 @@ def get_metrics_inputs(case):
 
 
 FIELD_CASES = ['online_C_sro_comp_asy', 'online_C_sro_noflags_seq', 'online_B_k4m3_seq', 'online_ragged_asy_r2',
-               'online_E_fs_L64_asy']
+               'online_E_fs_L64_asy', 'online_C_cohdrift_open_asy', 'online_C_cohdrift_seq']
 FIELD_STFT_BIN_STEP = 37
 
 
