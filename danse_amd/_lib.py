@@ -58,7 +58,7 @@ class DanseCfg(ctypes.Structure):
         ('cdCompensate', _c_i32), ('cdNIter', _c_i32), ('cdAlpha', ctypes.c_double), ('cdAlphaEps', ctypes.c_double),
         ('cEnd', _p_i32), ('cPhase', ctypes.POINTER(ctypes.c_double)), ('dxcp', _c_i32), ('smallDGrid', _c_i32),
         ('fsEv', _p_i32), ('nFsEv', _c_i32), ('fsSteps', _p_i32), ('nFsSteps', _c_i32), ('rawStreams', _c_i32),
-        ('desSigConv', _c_i32),
+        ('desSigConv', _c_i32), ('cdFlagWin', ctypes.POINTER(ctypes.c_double)),
     ]
 
 

@@ -1,4 +1,4 @@
-// CohDrift SRO estimation, closed loop, least-squares fit over bins
+// CohDrift SRO estimation, closed or open loop, least-squares fit over bins
 // (update_sro_estimates + build_phase_shifts_for_srocomp,
 // danse_toolbox/d_classes.py:2364-2621; cohdrift_sro_estimation with
 // method 'ls', danse_toolbox/d_sros.py:19-95), one workgroup per (scene,
@@ -16,6 +16,12 @@
 //     b_kappa = pi kappa ld Ns / (2 F);
 //   * eps = sro / (1 + sro) alphaEps; the sender's phase accumulator
 //     (added to zPhase in load_y from the next round on) loses eps Ns.
+// Open loop (cohDrift.loop 'open', d_classes.py:2439-2450,2580-2584): the
+// coherence of the UNcompensated observation (no zPhase / accumulator
+// rotation), every residual-product entry n of the 2 (F - 1)-bin spectrum
+// times exp(j 2 pi n W / (2 (F - 1))) with W = bufferFlagPos - bufferFlagPri
+// (flagWin, the full-sample drifts inside the segment; d_sros.py:19-95), and
+// eps = sro / (1 + sro) (no alphaEps).
 #pragma once
 #include "kernels.hpp"
 
@@ -32,6 +38,8 @@ struct CohDriftArgs {
   double* est;          // [S][K][R][K - 1]
   double* res;          // [S][K][R][K - 1]
   int R;
+  int open;                     // 1: open loop
+  const double* flagWin;        // open loop: [R][K][K] bufferFlagPos - bufferFlagPri
 };
 
 constexpr int kCdThreads = 576;   // >= F = 513, nine waves
@@ -53,7 +61,7 @@ __global__ void __launch_bounds__(kCdThreads) cohdrift_kernel(const UpdateArgs a
     const long long lk = ((long long)r * K + k) * K + qg;
     const int lag = a.zLag ? a.zLag[lk] : 0;
     cf yq = a.Zspec[((((long long)((r - lag) & 1)) * K + qg) * a.S + s) * F + t];
-    if (a.zPhase) {
+    if (a.zPhase && !c.open) {
       double ph = a.zPhase[lk];
       if (a.cdPhase) ph += a.cdPhase[((long long)s * K + k) * K + qg];
       double tt = (double)t * ph / (double)(2 * (F - 1));
@@ -82,6 +90,15 @@ __global__ void __launch_bounds__(kCdThreads) cohdrift_kernel(const UpdateArgs a
     const cd cp = coh[f];
     cd rv = cd{cp.re * pri.re + cp.im * pri.im, cp.im * pri.re - cp.re * pri.im};   // coh conj(pri)
     if (kap != 0) rv.im = -rv.im;                                                    // conj for the mirrored half
+    if (c.open) {
+      // entry n = F - 2 + kap of the 2 (F - 1)-bin spectrum times
+      // exp(j 2 pi n W / (2 (F - 1))), in double (the reference's complex128)
+      const double W = c.flagWin[((long long)r * K + k) * K + qg];
+      const double ang = 2.0 * M_PI * (double)(F - 2 + kap) * W / (double)(2 * (F - 1));
+      double sn, cs;
+      sincos(ang, &sn, &cs);
+      rv = cd{rv.re * cs - rv.im * sn, rv.re * sn + rv.im * cs};
+    }
     cd* av = c.avgTail + chunk + kap;
     const cd avg = first ? rv : cd{c.alpha * av->re + (1.0 - c.alpha) * rv.re, c.alpha * av->im + (1.0 - c.alpha) * rv.im};
     *av = avg;
@@ -105,7 +122,7 @@ __global__ void __launch_bounds__(kCdThreads) cohdrift_kernel(const UpdateArgs a
       sb += red[1][w];
     }
     const double sro = -sn / sb;
-    const double eps = sro / (1.0 + sro) * c.alphaEps;
+    const double eps = c.open ? sro / (1.0 + sro) : sro / (1.0 + sro) * c.alphaEps;
     const long long o = (((long long)s * K + k) * c.R + r) * (K - 1) + qi;
     c.res[o] = sro;
     c.est[o] = c.compensate ? eps : 0.0;

@@ -110,6 +110,8 @@ struct danse_engine {
   int nGate = 0;
   // CohDrift (cohdrift.hpp)
   int cohDrift = 0, cdLd = 0, cdStart = 0, cdEvery = 1, cdComp = 0, cdNIter = 0;
+  int cdOpen = 0;
+  double* cdFlagWin = nullptr;   // open loop: [R][K][K] flag windows (danse_cfg.cdFlagWin)
   double cdAlpha = 0.0, cdAlphaEps = 0.0;
   cd *cdRing = nullptr, *cdAvg = nullptr;
   double *cdPhase = nullptr, *cdEst = nullptr, *cdRes = nullptr;
@@ -751,6 +753,12 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
         const long long nb = eng_class_dmax(fn.D) / 8;
         fn.cOff = cOff;
         cOff += (long long)F * nb * (nb + 1) / 2 * 64;   // (kernels_2d.hpp c_record)
+      } else if (fn.vOff >= 0 && class_grid(eng_class_dmax(fn.D)) == 4 && !std::getenv("DANSE_NO_CCACHE")) {
+        // the 4 x 4 grid class (four bins per wave): one record per bin group
+        // of four (kernels_2d.hpp c4_ptr), used inside update_kernel_2d
+        const long long nb = eng_class_dmax(fn.D) / 4;
+        fn.cOff = cOff;
+        cOff += (long long)((F + 3) / 4) * nb * (nb + 1) / 2 * 64;
       }
       eng->fns.push_back(fn);
     }
@@ -1008,6 +1016,14 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
     eng->cohDrift = 1;
     eng->cdLd = c->cdSegLength; eng->cdStart = c->cdStart; eng->cdEvery = c->cdEvery; eng->cdComp = c->cdCompensate;
     eng->cdNIter = c->cdNIter; eng->cdAlpha = c->cdAlpha; eng->cdAlphaEps = c->cdAlphaEps;
+    if (c->cohDrift == 2) {
+      if (!c->cdFlagWin) return fail(eng, "CohDrift open loop needs cdFlagWin");
+      eng->cdOpen = 1;
+      HIPCHK(dalloc(&eng->cdFlagWin, (size_t)R * K * K));
+      HIPCHK(hipMemcpy(eng->cdFlagWin, c->cdFlagWin, (size_t)R * K * K * sizeof(double), hipMemcpyHostToDevice));
+    } else if (c->cohDrift != 1) {
+      return fail(eng, "cohDrift: 1 closed loop, 2 open loop");
+    }
     const size_t nq = (size_t)S * K * (K - 1);
     HIPCHK(dalloc(&eng->cdRing, (size_t)(c->cdSegLength + 1) * nq * F));
     HIPCHK(dalloc(&eng->cdAvg, nq * F));
@@ -1140,7 +1156,8 @@ void danse_engine_destroy(danse_engine* eng) {
                   eng->resUFlag, eng->resZFlag, eng->resGateRound, eng->resDanseFni, eng->resErr, eng->resFams,
                   eng->resFrames, eng->resChanNode, eng->resTrace, eng->condHist, eng->dxRecFrames,
                   eng->dxRecOut, eng->dFsEv, eng->rawStream, eng->vCache, eng->l64Cache, eng->lzStats,
-                  eng->dWideIds, eng->wideWork, eng->convIR, eng->dSnConv, eng->cCache, eng->yHist, eng->zHist};
+                  eng->dWideIds, eng->wideWork, eng->convIR, eng->dSnConv, eng->cCache, eng->yHist, eng->zHist,
+                  eng->cdFlagWin};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (eng->dx) danse_dxcp_destroy(eng->dx);
@@ -1370,6 +1387,7 @@ static void launch_update(danse_engine* e, int r, hipStream_t st, unsigned mask 
     c.every = e->cdEvery; c.nIter = e->cdNIter; c.compensate = e->cdComp; c.alpha = e->cdAlpha;
     c.alphaEps = e->cdAlphaEps; c.Ns = (double)e->Ns; c.base = e->dBase; c.ring = e->cdRing; c.avgTail = e->cdAvg;
     c.phase = e->cdPhase; c.est = e->cdEst; c.res = e->cdRes; c.R = e->R;
+    c.open = e->cdOpen; c.flagWin = e->cdFlagWin;
     c.k0 = e->k0; c.nOwn = e->k1 - e->k0;
     hipLaunchKernelGGL(cohdrift_kernel, dim3(e->S * c.nOwn * (e->K - 1)), dim3(kCdThreads), 0, st, make_update(e, r), c);
   }

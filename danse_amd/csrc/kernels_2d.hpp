@@ -60,18 +60,57 @@ DANSE_DEV void c_load_lower(t2d::Blk<NB>& A, const cf* cC) {
     });
   });
 }
-// the upper blocks from the lower ones through buf (LDS, (NB - 1) * 64 entries)
-template <int NB>
+// the upper blocks from the lower ones through buf (LDS, (NB - 1) * G * G
+// entries; li the bin-local lane: G = 4 runs four bins per wave, each with
+// its own buf)
+template <int NB, int G = 8>
 DANSE_DEV void c_fill_upper(t2d::Blk<NB>& A, cf* buf, int li) {
-  const int p = li / 8, q = li % 8;
+  const int p = li / G, q = li % G;
   sfor<1, NB>([&](auto tc) {
     constexpr int tb = decltype(tc)::value;
     t2d::wsync();
-    sfor<0, tb>([&](auto sc) { buf[decltype(sc)::value * 64 + q * 8 + p] = A.v[tb][decltype(sc)::value]; });
+    sfor<0, tb>([&](auto sc) { buf[decltype(sc)::value * G * G + q * G + p] = A.v[tb][decltype(sc)::value]; });
     t2d::wsync();
-    sfor<0, tb>([&](auto sc) { A.v[decltype(sc)::value][tb] = conjg(buf[decltype(sc)::value * 64 + p * 8 + q]); });
+    sfor<0, tb>([&](auto sc) { A.v[decltype(sc)::value][tb] = conjg(buf[decltype(sc)::value * G * G + p * G + q]); });
   });
   t2d::wsync();
+}
+// G = 4 (four bins per wave, kernels' bin group fg): the cache holds the
+// wave's lower blocks [NB (NB + 1) / 2][64] per bin GROUP, so that each block
+// is one 512-byte wave access; cC points at this lane's entry of block 0
+template <int NB>
+DANSE_DEV cf* c4_ptr(const UpdateArgs& a, const FamNode& d, int s, int fg) {
+  return a.cCache + (long long)s * a.cStride + d.cOff + (long long)fg * c_record<NB>() + threadIdx.x;
+}
+
+// G = 4: the four bins' float32 factor records (S.Ls | S.g, li_record
+// entries each, contiguous per bin in the cache and in LDS2) straight into
+// LDS by LDS-DMA (global_load_lds_dwordx4: 1 KiB per wave instruction, no
+// VGPR staging); the last chunk of a bin runs into its S.U, which the solver
+// writes before it reads.  Waited for by the caller (s_waitcnt vmcnt(0)).
+template <int NB>
+DANSE_DEV void li_dma4(char* ldsRaw, const cf* rec0, int fg, int F) {
+  constexpr int G = 4, W = 4;
+  constexpr int kRec = t2d::li_record<NB, G>();
+  constexpr int kChunks = (kRec * (int)sizeof(cf) + 1023) / 1024;
+  static_assert(kRec % 2 == 0, "16-byte pieces of the record");
+  static_assert(sizeof(t2d::LDS2<NB, G>) % 16 == 0 && __builtin_offsetof(t2d::LDS2<NB, G>, Ls) % 16 == 0,
+                "every bin's S.Ls 16-byte aligned in LDS");
+  static_assert(kChunks * 1024 <= (int)sizeof(t2d::LDS2<NB, G>) - (int)__builtin_offsetof(t2d::LDS2<NB, G>, Ls),
+                "the record's last chunk stays inside the bin's LDS2");
+  const int lane = threadIdx.x;
+  sfor<0, W>([&](auto bc) {
+    constexpr int b = decltype(bc)::value;
+    const int fb = min(fg * W + b, F - 1);
+    const cf* rec = rec0 + (long long)fb * kRec;
+    char* dst = ldsRaw + b * (int)sizeof(t2d::LDS2<NB, G>) + (int)__builtin_offsetof(t2d::LDS2<NB, G>, Ls);
+    sfor<0, kChunks>([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      const int e = 2 * (64 * j + lane);
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(rec + (e + 1 < kRec ? e : kRec - 2)),
+                                       (__attribute__((address_space(3))) void*)(dst + 1024 * j), 16, 0, 0);
+    });
+  });
 }
 
 template <int NB, int RMAX, int G = 8, bool PK = false, int SM = 0>
@@ -136,6 +175,18 @@ update_kernel_2d(const UpdateArgs a) {
   if (hasC && (a.leanOn || a.leanNoise) && r % kCRefresh != 0 && c_reusable(a, d, s) &&
       ((a.leanOn && reuse) || (a.leanNoise && solve && opN == DANSE_OP_AVG && opY == DANSE_OP_KEEP)))
     return;   // wave-uniform: update_kernel_2dc runs this item
+  // G = 4 (four bins per wave, DMAX 20): the C cache in this kernel -- a solve
+  // on the cached factor whose item solved last round with no SCM update
+  // since (kernels.hpp c_reusable) moves the cached C by this round's rank
+  // one (C' = by C + cy (Li y)(Li y)^H) instead of the O(D^3) congruence
+  const bool hasC4 = G == 4 && !PK && SM == 0 && a.cCache && d.cOff >= 0;
+  const bool useC4 = hasC4 && reuse && r % kCRefresh != 0 && c_reusable(a, d, s);
+  // G = 4: the cached factor records of the four bins by LDS-DMA, issued
+  // before the observation loads (they land while the y chain runs)
+  constexpr bool kDma4 = G == 4 && !PK && SM == 0;
+  if constexpr (kDma4) {
+    if (reuse) li_dma4<NB>(ldsRaw, a.liCache + (long long)s * a.liStride + d.liOff, fg, F);
+  }
 
   // Loads of the solve on a cached factor (the common solve: a VAD frame,
   // Rnn unchanged since the last factorisation) issued with the observation's:
@@ -286,7 +337,14 @@ update_kernel_2d(const UpdateArgs a) {
   } else {
     stamp(2);
   }
-  if (!kPre && reuse) li_load2d<NB, G>(S, liC, li);
+  if constexpr (kDma4) {
+    if (reuse) {
+      __builtin_amdgcn_s_waitcnt(0);   // (the records' LDS-DMA landed)
+      t2d::wsync();
+    }
+  } else {
+    if (!kPre && reuse) li_load2d<NB, G>(S, liC, li);
+  }
   tcode |= (opN ? 1 : 0) | (reuse ? 8 : 0) | (solve ? 16 : 0);
   stamp(3);
 
@@ -333,9 +391,49 @@ update_kernel_2d(const UpdateArgs a) {
     });
     stamp(4);
     if (solve) {
-      congruence2d<NB, G>(A, S, li, D);
-      if (hasC && fvalid)
-        c_store<NB>(a.cCache + (long long)s * a.cStride + a.fn[fni].cOff + (long long)f * c_record<NB>() + li, A);
+      if (useC4) {
+        // C' = by C + cy u u^H, u = Li y (Ryy' = by Ryy + cy y y^H; the
+        // factor is unchanged): u in the row layout by row-group sums, the
+        // column layout through LDS (as kernels_2dc.hpp)
+        cf* cC = c4_ptr<NB>(a, d, s, fg);
+        c_load_lower<NB>(A, cC);
+        c_fill_upper<NB, G>(A, S.U, li);
+        if (opY) {
+          constexpr int DMc = G * NB;
+          const float by = (float)beta, cy = (opY == DANSE_OP_SET) ? (float)(1.0 / D) : (float)((1.0 - beta) / D);
+          cf ur[NB], uc[NB];
+          sfor<0, NB>([&](auto sc) {
+            constexpr int sb = decltype(sc)::value;
+            cf acc = cf{0.0f, 0.0f};
+            sfor<0, sb + 1>([&](auto tc) {
+              constexpr int tb = decltype(tc)::value;
+              acc = acc + ls_get<DMc>(S.Ls, p + G * sb, q + G * tb) * yc[tb];   // (cmul would conjugate Li)
+            });
+            ur[sb] = sumq<G>(acc);
+            if (q == 0) S.vb[p + G * sb] = ur[sb];
+          });
+          t2d::wsync();
+          sfor<0, NB>([&](auto tc) { uc[decltype(tc)::value] = S.vb[q + G * decltype(tc)::value]; });
+          t2d::wsync();
+          sfor<0, NB>([&](auto sc) {
+            constexpr int sb = decltype(sc)::value;
+            sfor<0, NB>([&](auto tc) {
+              constexpr int tb = decltype(tc)::value;
+              const cf uu = cy * mulc(ur[sb], uc[tb]);
+              cf x = csel(opY == DANSE_OP_SET, uu, by * A.v[sb][tb] + uu);
+              if (sb == tb && p == q) x.im = 0.0f;
+              A.v[sb][tb] = x;
+            });
+          });
+          c_store<NB>(cC, A);
+        }
+        tcode |= 128;
+      } else {
+        congruence2d<NB, G>(A, S, li, D);
+        if (hasC && fvalid)
+          c_store<NB>(a.cCache + (long long)s * a.cStride + a.fn[fni].cOff + (long long)f * c_record<NB>() + li, A);
+        if (hasC4) c_store<NB>(c4_ptr<NB>(a, d, s, fg), A);   // (each bin of the group its own slot)
+      }
       stamp(5);
       const int path = gevd2d_solve<NB, RMAX, G>(A, S, li, D, a.rank, w, vC, fvalid);
       // (one atomic per wave -- the path is wave-uniform -- into one of

@@ -298,10 +298,24 @@ class DanseEngine:
                 raise NotImplementedError('centralised estimates with DXCP-PhaT SRO estimation')
         elif self.cohDrift:
             cd = p.cohDrift
-            if cd.loop != 'closed' or cd.estimationMethod != 'ls':
-                raise NotImplementedError("CohDrift on the device path: closed loop, estimationMethod 'ls'")
-            if 'asy' not in p.nodeUpdating or self.fewSamples or p.computeCentralised:
-                raise NotImplementedError('CohDrift on the device path: asy node updating, wholeChunk, no centralised')
+            if cd.loop not in ('closed', 'open') or cd.estimationMethod != 'ls':
+                raise NotImplementedError("CohDrift on the device path: estimationMethod 'ls' (paderwasn's 'gs' is "
+                                          "absent)")
+            if self.fewSamples or p.computeCentralised:
+                raise NotImplementedError('CohDrift on the device path: wholeChunk broadcasts, no centralised family')
+            self._cdFlagWin = None
+            if cd.loop == 'open':
+                # bufferFlagPos - bufferFlagPri (update_sro_estimates,
+                # d_classes.py:2376-2386): broadcastLength x the flags of the
+                # last segLength rounds, per (round, receiver, sender)
+                fl = np.asarray(self.rt.flags[:R], dtype=np.float64)
+                if not np.all(np.isfinite(fl)):
+                    raise NotImplementedError('CohDrift open loop with undefined (NaN) buffer flags')
+                cum = np.cumsum(fl, axis=0)
+                ld = int(cd.segLength)
+                win = cum.copy()
+                win[ld:] -= cum[:-ld]
+                self._cdFlagWin = np.ascontiguousarray(float(p.broadcastLength) * win)
         elif p.estimateSROs != 'Oracle':
             raise ValueError(f'estimateSROs={p.estimateSROs!r}')
         if not p.compensateSROs:
@@ -557,7 +571,9 @@ class DanseEngine:
         c.scmInitPerBin = 0 if p.covMatSameInitForAllFreqs else 1
         if self.cohDrift:
             cd = p.cohDrift
-            c.cohDrift, c.cdSegLength, c.cdEvery = 1, int(cd.segLength), int(cd.estEvery)
+            c.cohDrift, c.cdSegLength, c.cdEvery = (2 if cd.loop == 'open' else 1), int(cd.segLength), int(cd.estEvery)
+            if self._cdFlagWin is not None:
+                c.cdFlagWin = _ptr(self._cdFlagWin, ctypes.c_double)
             c.cdStart = int(cd.startAfterNups + cd.estEvery)
             c.cdCompensate = int(bool(p.compensateSROs))
             c.cdNIter = int(self.nIter)

@@ -95,7 +95,7 @@ typedef struct danse_cfg {
    * the coherence ring, the averaged residual products and a per-(scene,
    * node, sender) phase accumulator that adds to zPhase (which then holds the
    * full-sample-drift flags only).  0 = off.                               */
-  int32_t cohDrift;         /* 1: closed loop                                   */
+  int32_t cohDrift;         /* 1: closed loop, 2: open loop (cohDrift.loop)     */
   int32_t cdSegLength;      /* segLength (ld)                                   */
   int32_t cdStart;          /* startAfterNups + estEvery (first estimate)       */
   int32_t cdEvery;          /* estEvery                                         */
@@ -156,6 +156,14 @@ typedef struct danse_cfg {
    * win_s, win_s, Ns) of the same filter columns, written to d[end - Ns,
    * end) (no overlap-add); dhat is NaN (the reference stores None).      */
   int32_t desSigConv;
+  /* CohDrift open loop (cohDrift == 2; update_sro_estimates, d_classes.py:
+   * 2376-2386,2439-2450; cohdrift_sro_estimation, d_sros.py:19-95): per
+   * (round r, receiver k, sender q) broadcastLength * (sum of the buffer flags
+   * of rounds r - segLength + 1 .. r) -- bufferFlagPos - bufferFlagPri, the
+   * full-sample drifts inside the coherence segment, whose linear phase the
+   * residual product loses; the coherence is taken on the UNcompensated
+   * observation.  [R*K*K] doubles; NULL with the closed loop.              */
+  const double* cdFlagWin;
 } danse_cfg;
 
 typedef struct danse_engine danse_engine;

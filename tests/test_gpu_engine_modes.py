@@ -559,14 +559,17 @@ def test_config_C_shape_K16_sro_vs_oracle(est):
         assert dr <= 1e-4
 
 
-def test_cohdrift_sro_estimates_vs_oracle():
-    """CohDrift SRO estimation (closed loop, 'ls'; d_sros.py:19-95,
-    d_classes.py:2364-2621) on the device: the per-update residual SRO
-    estimates and the compensated estimates they feed match the float64
-    oracle (itself pinned to the reference by online_C_cohdrift_asy)."""
+@pytest.mark.parametrize('name', ['online_C_cohdrift_asy', 'online_C_cohdrift_open_asy', 'online_C_cohdrift_seq'])
+def test_cohdrift_sro_estimates_vs_oracle(name):
+    """CohDrift SRO estimation ('ls'; d_sros.py:19-95, d_classes.py:
+    2364-2621) on the device, closed loop (asy and seq node updating) and
+    open loop (the uncompensated coherence, the flag-window phase,
+    d_classes.py:2439-2450,2580-2584): the per-update residual SRO estimates
+    and the estimates they feed match the float64 oracle (itself pinned to the
+    reference's own estimates by the fields_* fixtures, test_dv_fields.py)."""
     from danse_amd.core import danse_multi
     from oracle import danse_ref_cpu as O
-    case = _case('online_C_cohdrift_asy')
+    case = _case(name)
     sc, dp, wp = _scene_params(case)
     dv = danse_multi([sc], dp)[0]
     ov = O.OnlineDANSE(sc, dp, vadMinProp=wp.vadMinProportionActive)
