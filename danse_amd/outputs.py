@@ -174,6 +174,35 @@ class DANSEoutputs:
         self.initialised = True
         return self
 
+    # ---- disk formats (d_post.py:184-212,
+    # dataclass_methods.py:13-117): <folder>/DANSEoutputs.pkl.gz (gzip'ed
+    # pickle of the object), <folder>/DANSEoutputs_text.txt (one line per
+    # field, nested objects indented) and <folder>/metrics.pkl
+    def check_init(self):
+        """``check_init`` (d_post.py:184-187): returns (does not raise) the
+        error of an empty object, as the reference does."""
+        if not self.initialised:
+            return ValueError('The DANSEoutputs object is empty.')
+
+    def save(self, foldername, light=False, exportType='pkl'):
+        """``save`` (d_post.py:189-199).  With ``light`` the reference strips
+        the '*signal*' fields from a copy and then saves the full object
+        anyway; kept as such."""
+        _save(self, foldername, exportType=exportType)
+
+    def save_metrics(self, foldername):
+        """``save_metrics`` (d_post.py:201-205): ``self.metrics`` pickled to
+        <folder>/metrics.pkl."""
+        self.check_init()
+        import pickle
+        with open(f'{foldername}/metrics.pkl', 'wb') as f:
+            pickle.dump(self.metrics, f)
+
+    def load(self, foldername, dataType='pkl'):
+        """``load`` (d_post.py:207-209, dataclass_methods.py:45-95): the
+        object this class saved to <folder>/DANSEoutputs.pkl.gz."""
+        return _load(self, foldername, dataType=dataType)
+
     def from_snr_signals(self, snrSigs: dict):
         self.TDfiltSpeech = snrSigs['s']
         self.TDfiltNoise = snrSigs['n']
@@ -202,3 +231,57 @@ class DANSEoutputs:
                                     for k in range(outBP.nNodes)]).T,
         }
         return self
+
+
+def _save(obj, foldername, exportType='pkl'):
+    """``dataclass_methods.save`` (dataclass_methods.py:13-42): the gzip'ed
+    pickle (or JSON, which raises in the reference: NOT YET CORRECTLY
+    IMPLEMENTED) plus the text view."""
+    import gzip
+    import pickle
+    from pathlib import Path
+    Path(foldername).mkdir(parents=True, exist_ok=True)
+    full = f'{foldername}/{type(obj).__name__}'
+    if exportType == 'pkl':
+        with gzip.open(full + '.pkl.gz', 'wb') as f:
+            pickle.dump(obj, f)
+    elif exportType == 'json':
+        raise ValueError('NOT YET CORRECTLY IMPLEMENTED')
+    _save_as_txt(obj, foldername)
+
+
+def _load(obj, foldername, dataType='pkl'):
+    """``dataclass_methods.load`` (dataclass_methods.py:45-95), for the
+    files ``_save`` wrote (this package's own pickles only)."""
+    import gzip
+    import pickle
+    from pathlib import Path
+    if not Path(foldername).is_dir():
+        raise ValueError(f'The folder "{foldername}" cannot be found.')
+    base, alt = ('.pkl.gz', '.json') if dataType == 'pkl' else ('.json', '.pkl.gz')
+    path = f'{foldername}/{type(obj).__name__}{base}'
+    if not Path(path).is_file():
+        other = f'{foldername}/{type(obj).__name__}{alt}'
+        if not Path(other).is_file():
+            raise ValueError(f'Import issue, file\n"{path}"\nnot found (with either possible extensions).')
+        path, base = other, alt
+    if base == '.json':
+        raise ValueError('NOT YET CORRECTLY IMPLEMENTED')
+    with gzip.open(path, 'rb') as f:
+        return pickle.load(f)
+
+
+def _save_as_txt(obj, foldername):
+    """``save_as_txt`` (dataclass_methods.py:97-117): one ' - name = value'
+    line per field, nested parameter objects indented with ' |'."""
+    def lines(o, f, n=0):
+        tab = ' |' * n
+        f.write(f'{tab}>--------{type(o).__name__} class instance\n')
+        for name, val in vars(o).items():
+            if hasattr(val, '__dataclass_fields__'):
+                lines(val, f, n + 1)
+            else:
+                f.write(f'{tab} - {name} = {val}\n')
+        f.write(f'{tab}_______\n')
+    with open(f'{foldername}/{type(obj).__name__}_text.txt', 'w') as f:
+        lines(obj, f)

@@ -140,3 +140,39 @@ def test_sandbox_mirror_errors():
     wp = P.WASNparameters(trueRoom=True, nSensorPerNode=[1, 1])
     with pytest.raises(NotImplementedError):
         sandbox.build_wasn(wp)
+
+
+def test_outputs_disk_format(tmp_path):
+    """DANSEoutputs.save / load / save_metrics (d_post.py:184-212,
+    dataclass_methods.py:13-117): <folder>/DANSEoutputs.pkl.gz, the text view
+    and metrics.pkl; 'json' raises as in the reference; load round-trips."""
+    import gzip
+    import pickle
+    from danse_amd.params import DANSEparameters
+    p = DANSEparameters(simType='online')
+    p.__post_init__()
+    out = OUT.DANSEoutputs().import_params(p)
+    assert isinstance(out.check_init(), ValueError)
+    out.TDdesiredSignals_est = np.arange(12.0).reshape(6, 2)
+    out.filters = [np.ones((3, 4, 2), dtype=np.complex64)]
+    out.metrics = {'snr': {'Node1': 1.5}}
+    out.initialised = True
+    d = tmp_path / 'res'
+    out.save(str(d), light=True)
+    assert (d / 'DANSEoutputs.pkl.gz').is_file() and (d / 'DANSEoutputs_text.txt').is_file()
+    txt = (d / 'DANSEoutputs_text.txt').read_text()
+    assert txt.startswith('>--------DANSEoutputs class instance') and ' - simType = online' in txt
+    back = OUT.DANSEoutputs().load(str(d))
+    assert np.array_equal(back.TDdesiredSignals_est, out.TDdesiredSignals_est)
+    assert back.filters[0].dtype == np.complex64 and back.simType == 'online'
+    # (light: the reference saves the full object anyway)
+    assert hasattr(back, 'TDdesiredSignals_est')
+    out.save_metrics(str(d))
+    with open(d / 'metrics.pkl', 'rb') as f:
+        assert pickle.load(f) == out.metrics
+    with gzip.open(d / 'DANSEoutputs.pkl.gz', 'rb') as f:
+        assert type(pickle.load(f)).__name__ == 'DANSEoutputs'
+    with pytest.raises(ValueError, match='NOT YET'):
+        out.save(str(tmp_path / 'j'), exportType='json')
+    with pytest.raises(ValueError):
+        OUT.DANSEoutputs().load(str(tmp_path / 'missing'))
