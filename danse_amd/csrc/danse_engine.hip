@@ -107,6 +107,8 @@ struct danse_engine {
   int* dGateVerdict = nullptr;
   std::vector<int> gateOff;
   std::vector<int> gateDmax;   // per round: largest candidate D (LDS size)
+  cd* gateWork = nullptr;      // gate_wide_kernel workspace (candidates above kGateMaxD)
+  long long gateWorkItems = 0; // (cand, bin) workgroups per chunk
   int nGate = 0;
   // CohDrift (cohdrift.hpp)
   int cohDrift = 0, cdLd = 0, cdStart = 0, cdEvery = 1, cdComp = 0, cdNIter = 0;
@@ -706,8 +708,8 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
         // (only the centralised family reaches past 64 channels: the wide
         // classes of wide_online.hpp, synchronous wholeChunk runs, the gate's
         // matrix in LDS up to kGateMaxD)
-        if (fam != DANSE_FAM_CENTR || fn.D > kGateMaxD)
-          return fail(eng, "filter dimension > 64 outside the centralised family, or a centralised family above 96 channels");
+        if (fam != DANSE_FAM_CENTR || fn.D > wide::kMaxD)
+          return fail(eng, "filter dimension > 64 outside the centralised family, or a centralised family above 256 channels");
         if (c->cEnd || c->fsTab || c->cPhase)
           return fail(eng, "centralised family above 64 channels: synchronous wholeChunk runs only");
       }
@@ -904,12 +906,19 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
     build_wide_lists(eng, c->flags);
   }
   {
-    // the gate's [D][D + 1] complex-double matrix in dynamic LDS above 64 KiB
+    // the gate's [D][D + 1] complex-double matrix in dynamic LDS above 64 KiB;
+    // above kGateMaxD the packed lower triangle in a global workspace
+    // (gate_wide_kernel: 512 (candidate, bin) workgroups per chunk)
     int dmax = 0;
     for (const auto& x : eng->fns) dmax = std::max(dmax, x.D);
-    const size_t lds = (size_t)dmax * (dmax + 1) * sizeof(cd);
-    if (lds > 65536)
-      HIPCHK(hipFuncSetAttribute((const void*)gate_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    if (dmax > kGateMaxD) {
+      eng->gateWorkItems = 512;
+      HIPCHK(dalloc(&eng->gateWork, (size_t)eng->gateWorkItems * dmax * (dmax + 1) / 2));
+    } else {
+      const size_t lds = (size_t)dmax * (dmax + 1) * sizeof(cd);
+      if (lds > 65536)
+        HIPCHK(hipFuncSetAttribute((const void*)gate_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    }
   }
   const size_t MT = (size_t)eng->MT;
   HIPCHK(dalloc(&eng->Yspec, 2 * S * MT * F));
@@ -1157,7 +1166,7 @@ void danse_engine_destroy(danse_engine* eng) {
                   eng->resFrames, eng->resChanNode, eng->resTrace, eng->condHist, eng->dxRecFrames,
                   eng->dxRecOut, eng->dFsEv, eng->rawStream, eng->vCache, eng->l64Cache, eng->lzStats,
                   eng->dWideIds, eng->wideWork, eng->convIR, eng->dSnConv, eng->cCache, eng->yHist, eng->zHist,
-                  eng->cdFlagWin};
+                  eng->cdFlagWin, eng->gateWork};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (eng->dx) danse_dxcp_destroy(eng->dx);
@@ -1454,15 +1463,32 @@ static void launch_bcast(danse_engine* e, int r, int synth, int bc, hipStream_t 
 
 // the installed speculative gate candidates of round r (danse_engine_set_gate)
 // whose node is in `mask`
+// the gate checks of n candidates (GateCand) of filter dimensions up to dmax:
+// gate_kernel (one wave per (candidate, bin), the matrix in LDS) up to
+// kGateMaxD, gate_wide_kernel (one workgroup per (candidate, bin), the matrix
+// in eng->gateWork, in chunks) above
+static void launch_gate(danse_engine* eng, const UpdateArgs& a, const GateCand* cand, int n, int dmax, int* verdict,
+                        hipStream_t s) {
+  if (dmax <= kGateMaxD || !eng->gateWork) {
+    const size_t lds = (size_t)dmax * (dmax + 1) * sizeof(cd);
+    hipLaunchKernelGGL(gate_kernel, dim3(eng->F, n), dim3(64), lds, s, a, eng->dFnAll, cand, eng->dInitScmOff,
+                       eng->dScm0, eng->scmPerBin, verdict);
+    return;
+  }
+  const long long items = (long long)n * eng->F;
+  for (long long i0 = 0; i0 < items; i0 += eng->gateWorkItems) {
+    const long long m = std::min(eng->gateWorkItems, items - i0);
+    hipLaunchKernelGGL(gate_wide_kernel, dim3((unsigned)m), dim3(kGateWideThr), 0, s, a, eng->dFnAll, cand,
+                       eng->dInitScmOff, eng->dScm0, eng->scmPerBin, verdict, i0, eng->gateWork);
+  }
+}
+
 static void launch_gate_round(danse_engine* eng, int r, hipStream_t s, unsigned mask = ~0u) {
   if (eng->nGate > 0 && eng->gateOff[r + 1] > eng->gateOff[r]) {
     const int n = eng->gateOff[r + 1] - eng->gateOff[r];
-    const size_t lds = (size_t)eng->gateDmax[r] * (eng->gateDmax[r] + 1) * sizeof(cd);
     UpdateArgs a = make_update(eng, r);
     a.nodeMask = mask;
-    hipLaunchKernelGGL(gate_kernel, dim3(eng->F, n), dim3(64), lds, s, a, eng->dFnAll,
-                       eng->dGateCand + eng->gateOff[r], eng->dInitScmOff, eng->dScm0, eng->scmPerBin,
-                       eng->dGateVerdict + eng->gateOff[r]);
+    launch_gate(eng, a, eng->dGateCand + eng->gateOff[r], n, eng->gateDmax[r], eng->dGateVerdict + eng->gateOff[r], s);
   }
 }
 
@@ -1963,9 +1989,7 @@ int danse_engine_gate(danse_engine* eng, int32_t r, int32_t n, const int32_t* fa
   HIPCHK(hipMemcpyAsync(dC, h.data(), n * sizeof(GateCand), hipMemcpyHostToDevice, st));
   HIPCHK(hipMemcpyAsync(dV, ones.data(), n * sizeof(int), hipMemcpyHostToDevice, st));
   UpdateArgs a = make_update(eng, r);
-  const size_t lds = (size_t)dmax * (dmax + 1) * sizeof(cd);
-  hipLaunchKernelGGL(gate_kernel, dim3(eng->F, n), dim3(64), lds, st, a, eng->dFnAll, dC, eng->dInitScmOff,
-                     eng->dScm0, eng->scmPerBin, dV);
+  launch_gate(eng, a, dC, n, dmax, dV, st);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(verdict, dV, n * sizeof(int), hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));

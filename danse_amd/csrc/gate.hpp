@@ -45,7 +45,8 @@ DANSE_DEV void tri_ij(int e, int& i, int& j) {
 // test go over the packed lower triangle in storage order (coalesced), the
 // Cholesky's trailing updates over the trailing triangle's entries.
 // (filter dimensions up to kGateMaxD: the online centralised family above
-// 64 channels -- [D][D + 1] complex doubles of dynamic LDS, 147 KiB at 96)
+// 64 channels -- [D][D + 1] complex doubles of dynamic LDS, 147 KiB at 96;
+// gate_wide_kernel below takes the larger ones)
 constexpr int kGateMaxD = 96;
 __global__ void __launch_bounds__(64) gate_kernel(const UpdateArgs a, const FamNode* fns, const GateCand* cand,
                                                  const long long* initOff, const cd* scm0, int perBin, int* verdict) {
@@ -141,4 +142,109 @@ __global__ void __launch_bounds__(64) gate_kernel(const UpdateArgs a, const FamN
   if (li == 0 && !pass) atomicAnd(&verdict[blockIdx.y], 0);
 }
 
+// The same checks above kGateMaxD (the online centralised family up to 256
+// channels, wide classes): one 256-thread workgroup per (candidate, bin), the
+// packed lower triangle in a global workspace (T complex doubles per
+// workgroup, launched in chunks), the Cholesky right-looking over the packed
+// trailing triangle with the pivot test of gate_kernel (same entry-wise
+// arithmetic, so the same verdicts).
+constexpr int kGateWideThr = 256;
+DANSE_DEV long long pk_lo(int i, int j) { return (long long)i * (i + 1) / 2 + j; }
+__global__ void __launch_bounds__(kGateWideThr) gate_wide_kernel(const UpdateArgs a, const FamNode* fns,
+                                                                 const GateCand* cand, const long long* initOff,
+                                                                 const cd* scm0, int perBin, int* verdict,
+                                                                 long long item0, cd* work) {
+  const long long item = item0 + blockIdx.x;
+  const int F = a.F;
+  const int ci = (int)(item / F), f = (int)(item % F);
+  const GateCand c = cand[ci];
+  const FamNode d = fns[c.fni];
+  if (!node_in(a.nodeMask, d.k)) return;   // (workgroup-uniform)
+  const int tid = threadIdx.x;
+  const int D = d.D, s = c.s;
+  const int T = D * (D + 1) / 2;
+  cd* X = work + (long long)blockIdx.x * T;
+  const uint8_t fl = a.flags[(((long long)a.r * a.S + s) * kMaxFam + d.fam) * a.K + d.k];
+  __shared__ cf gy[256];
+  __shared__ double red[kGateWideThr / 64];
+  __shared__ int flag;
+  for (int i = tid; i < D; i += kGateWideThr) gy[i] = load_y(a, d, s, f, i, true);
+  __syncthreads();
+  const double beta = a.beta[s * a.K + d.k];
+  const cd* R0 = scm0 + initOff[c.fni] + (perBin ? (long long)f * D * D : 0ll);
+  bool pass = true;
+  for (int which = 0; which < 2 && pass; ++which) {   // 0: Ryy, 1: Rnn
+    const int op = which == 0 ? (fl & 3) : ((fl >> 2) & 3);
+    const double q = which == 0 ? c.qY : c.qN;
+    const double cy = (op == DANSE_OP_SET) ? 1.0 / D : (1.0 - beta) / D;
+    const double cx = (op == DANSE_OP_SET) ? 0.0 : beta;
+    bool herm = true;
+    double tr = 0.0;
+    for (int e = tid; e < T; e += kGateWideThr) {
+      int i, j;
+      tri_ij(e, i, j);
+      const long long ee = scm_lower(d, a.scmStride, s, F, f, i, j);
+      cd x = which == 0 ? cdk(a.Ryy[ee]) : a.Rnn[ee];
+      if (i == j) x.im = 0.0;
+      if (op != DANSE_OP_KEEP) {
+        cd yy = cd{0.0, 0.0};
+        fma_cc(yy, cdk(gy[i]), cdk(gy[j]));
+        x = cx * x;
+        x.re = fma(cy, yy.re, x.re);
+        x.im = fma(cy, (i == j) ? 0.0 : yy.im, x.im);
+      }
+      const cd r0ij = R0[i * D + j], r0ji = R0[j * D + i];
+      const cd Q = cd{0.5 * q * (r0ij.re - r0ji.re), 0.5 * q * (r0ij.im + r0ji.im)};
+      if (i == j) {
+        const double qi = q * r0ij.im;
+        herm = herm && (2.0 * fabs(qi) <= 1e-8 + 1e-5 * sqrt(x.re * x.re + qi * qi));
+        tr += x.re;
+        X[e] = cd{x.re, 0.0};
+      } else {
+        const double aq = 2.0 * sqrt(Q.re * Q.re + Q.im * Q.im);
+        const double xr = x.re, xi = x.im;
+        const double mr = xr - 2.0 * Q.re, mi = xi - 2.0 * Q.im;
+        herm = herm && (aq <= 1e-8 + 1e-5 * sqrt(xr * xr + xi * xi)) && (aq <= 1e-8 + 1e-5 * sqrt(mr * mr + mi * mi));
+        X[e] = cd{xr, xi};
+      }
+    }
+    if (a.gevd && __syncthreads_or(!herm)) pass = false;
+    // the trace (every diagonal entry, summed over the workgroup)
+    for (int o = 32; o >= 1; o >>= 1) tr += __shfl_xor(tr, o);
+    if ((tid & 63) == 0) red[tid >> 6] = tr;
+    __syncthreads();
+    tr = 0.0;
+    for (int w = 0; w < kGateWideThr / 64; ++w) tr += red[w];
+    const double tol = (double)D * 2.220446049250313e-16 * fabs(tr);
+    __threadfence_block();
+    __syncthreads();
+    for (int j = 0; j < D && pass; ++j) {
+      const double pj = X[pk_lo(j, j)].re;   // (every thread reads the same pivot: uniform)
+      if (!(a.gevd ? pj > tol : fabs(pj) > tol)) {
+        pass = false;
+        break;
+      }
+      const double inv = 1.0 / sqrt(fabs(pj));
+      for (int row = j + 1 + tid; row < D; row += kGateWideThr) X[pk_lo(row, j)] = inv * X[pk_lo(row, j)];
+      __threadfence_block();
+      __syncthreads();
+      const int n = D - 1 - j;
+      for (int e = tid; e < n * (n + 1) / 2; e += kGateWideThr) {
+        int i2, k2;
+        tri_ij(e, i2, k2);
+        const int row = j + 1 + i2, col = j + 1 + k2;
+        const cd lij = X[pk_lo(row, j)];
+        if (pj > 0.0) fms_cc(X[pk_lo(row, col)], lij, X[pk_lo(col, j)]);
+        else fma_cc(X[pk_lo(row, col)], lij, X[pk_lo(col, j)]);
+      }
+      __threadfence_block();
+      __syncthreads();
+    }
+    __syncthreads();
+  }
+  (void)flag;
+  if (tid == 0 && !pass) atomicAnd(&verdict[ci], 0);
+}
+
 }  // namespace danse
+

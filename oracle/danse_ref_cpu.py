@@ -334,8 +334,19 @@ class OnlineDANSE:
     ``DANSEvariables`` (``d_classes.py:478-2709``)."""
 
     def __init__(self, scene, p, vadMinProp=0.5, yinOverride=None, keepHistory=True, maxRounds=None,
-                 sroEstimates=None):
+                 sroEstimates=None, skipDanse=False, centrBins=None, centrNodes=None):
         self.p = p
+        # Test-side restrictions for the wide centralised family (sum(M) up to
+        # 256), exact for synchronous wholeChunk runs, where the centralised
+        # vector is the nodes' raw frames and does not depend on any filter:
+        #   skipDanse   no DANSE-family SCMs, gate or solves (the broadcasts
+        #               carry the initial filters; the node counters still run)
+        #   centrBins   the centralised family on these bins only (its SCMs,
+        #               gate and filters; dCentr / dHatCentr are not formed)
+        #   centrNodes  the centralised family of these nodes only
+        self.skipDanse = skipDanse
+        self.centrBins = None if centrBins is None else np.asarray(centrBins, dtype=int)
+        self.centrNodes = None if centrNodes is None else set(int(k) for k in centrNodes)
         self.scene = scene
         wasn = scene.wasn
         K = len(wasn)
@@ -430,7 +441,11 @@ class OnlineDANSE:
             self.ssbc.append(fam(D, p.computeSingleSensorBroadcast))
             self.wExt.append(init_complex_filter((F, nh, self.M[k]), p.referenceSensor, **fi))
             self.wExtTarget.append(init_complex_filter((F, self.M[k]), p.referenceSensor, **fi))
-            self.centr.append(fam(self.Mtot, p.computeCentralised, refC))
+            cf_ = fam(self.Mtot, p.computeCentralised and (self.centrNodes is None or k in self.centrNodes), refC)
+            if self.centrBins is not None and cf_.Ryy is not None:
+                cf_ = _SCMSet(cf_.Ryy[self.centrBins].copy(), cf_.Rnn[self.centrBins].copy(),
+                              cf_.w[self.centrBins].copy())
+            self.centr.append(cf_)
             self.local.append(fam(self.M[k], p.computeLocal))
         self.i = np.zeros(K, dtype=int)
         # condition numbers (d_classes.py:965-984)
@@ -472,6 +487,7 @@ class OnlineDANSE:
         self.lastExtFiltUp = np.zeros(K)
         self.nSensorsNeighborsCentr = [[self.M[q] for q in range(K) if q != k] for k in range(K)]
         self.startRound = np.full(K, -1)
+        self.startRoundCentr = np.full(K, -1)
         # fewSamples broadcasting state (d_classes.py:522, 658-663, 828-831):
         # T(z) IR initialised as a Dirac at tap N (not N - 1) on the reference sensor
         self.lastBroadcastInstant = np.zeros(K)
@@ -570,7 +586,7 @@ class OnlineDANSE:
             else:
                 ych = np.empty((0, self.M[k]))
             for q in range(self.K):
-                if q != k:
+                if q != k and self._centr_on(q):
                     idx = k if k < q else k - 1
                     self.yBufferCentr[q][idx] = np.concatenate((self.yBufferCentr[q][idx], ych), axis=0)
 
@@ -610,7 +626,7 @@ class OnlineDANSE:
         self.z[k] = zk
         self.bufferFlags[k][self.i[k], :] = flags
         self.zBuffer[k] = [np.array([]) for _ in self.neighbors[k]]
-        if self.p.computeCentralised:
+        if self._centr_on(k):
             self._process_buffers_centr(k)
 
     def _process_buffers_centr(self, k):
@@ -654,6 +670,12 @@ class OnlineDANSE:
     def _fft(self, y):
         return (np.fft.fft(y * self.h[:, np.newaxis], self.N, axis=0) / np.sqrt(self.Ns))[:self.F, :]
 
+    def _centr_on(self, k):
+        return self.p.computeCentralised and (self.centrNodes is None or k in self.centrNodes)
+
+    def _cbins(self, yHat):
+        return yHat if self.centrBins is None else yHat[self.centrBins]
+
     # ---- update_and_estimate (d_classes.py:1252-1330) ----
     def update_and_estimate(self, tCurr, fs, k, bypass):
         p = self.p
@@ -668,7 +690,7 @@ class OnlineDANSE:
         # build_ytilde (1893-1934)
         yT = np.concatenate((yLoc, self.z[k]), axis=1)
         yTHat = self._fft(yT)
-        if p.computeCentralised:
+        if self._centr_on(k):
             cols = []
             cov = 0
             for q in range(self.K):
@@ -717,7 +739,7 @@ class OnlineDANSE:
                 yyqq = yc[:, iq] * yc[:, iq].conj() / D
                 self.cohHist[k][i, :, q] = yy0q / np.sqrt(yy00 * yyqq)
         skipUpdateCentr = None
-        if p.computeCentralised:
+        if self._centr_on(k):
             skipUpdateCentr = False
             extraC = np.zeros(self.Mtot)
             for q in range(self.K):
@@ -745,8 +767,8 @@ class OnlineDANSE:
             self.wExt[k][:, i + 1, :] = pg.externalFilters[k][:, i + 1, :]
             if p.computeLocal:
                 self.local[k].w[:, i + 1, :] = pg.filtersLocal[k][:, i + 1, :]
-            if p.computeCentralised:
-                self.centr[k].w[:, i + 1, :] = pg.filtersCentr[k][:, i + 1, :]
+            if self._centr_on(k):
+                self.centr[k].w[:, i + 1, :] = self._cbins(pg.filtersCentr[k][:, i + 1, :])
             if p.computeSingleSensorBroadcast:
                 self.ssbc[k].w[:, i + 1, :] = pg.filtersSSBC[k][:, i + 1, :]
         else:
@@ -755,11 +777,12 @@ class OnlineDANSE:
                 self.numUpdatesRyy[k] += 1
             else:
                 self.numUpdatesRnn[k] += 1
-            self._scm_update(k, self.danse[k], yTHat, vad)
+            if not self.skipDanse:
+                self._scm_update(k, self.danse[k], yTHat, vad)
             if p.computeLocal:
                 self._scm_update(k, self.local[k], yLHat, vad)
-            if p.computeCentralised:
-                self._scm_update(k, self.centr[k], yCHat, self.centrVAD[i])
+            if self._centr_on(k):
+                self._scm_update(k, self.centr[k], self._cbins(yCHat), self.centrVAD[i])
             if p.computeSingleSensorBroadcast:
                 self._scm_update(k, self.ssbc[k], ySHat, vad)
             self._cond_numbers(k, i)
@@ -771,7 +794,7 @@ class OnlineDANSE:
                 if p.computeLocal:
                     self.local[k].w[:, i + 1, :] = self.local[k].w[:, i, :]
                 if bypass:
-                    if p.computeCentralised:
+                    if self._centr_on(k):
                         self.centr[k].w[:, i + 1, :] = self.centr[k].w[:, i, :]
                     if p.computeSingleSensorBroadcast:
                         self.ssbc[k].w[:, i + 1, :] = self.ssbc[k].w[:, i, :]
@@ -819,7 +842,7 @@ class OnlineDANSE:
         sl = slice(self.idxBeg, self.idxEnd)
         _, dh = desired_sig_chunk(self.danse[k].w[:, i + 1, :], yTHat, self.f, nf, self.d[sl, k])
         self.dhat[:, i, k] = dh
-        if p.computeCentralised:
+        if self._centr_on(k) and self.centrBins is None:
             _, dh = desired_sig_chunk(self.centr[k].w[:, i + 1, :], yCHat, self.f, nf, self.dCentr[sl, k])
             self.dHatCentr[:, i, k] = dh
         if p.computeLocal:
@@ -874,7 +897,7 @@ class OnlineDANSE:
         fams = [('DANSE', self.danse[k], 'cn_RyyDANSE', 'iter_cn_RyyDANSE', self._cnLast[0])]
         if p.computeLocal:
             fams.append(('local', self.local[k], 'cn_RyyLocal', 'iter_cn_RyyLocal', self._cnLast[1]))
-        if p.computeCentralised:
+        if self._centr_on(k):
             fams.append(('centralised', self.centr[k], 'cn_RyyCentr', 'iter_cn_RyyCentr', self._cnLast[2]))
         for _, fam, fc, fi, last in fams:
             if i - last[k] >= p.saveConditionNumberEvery:
@@ -917,9 +940,9 @@ class OnlineDANSE:
     def _check_covmats(self, k, tCurr):
         p = self.p
         g = p.performGEVD
-        fams = [('danse', self.danse[k], True)]
+        fams = [('danse', self.danse[k], not self.skipDanse)]
         if p.simType == 'online':
-            fams += [('local', self.local[k], p.computeLocal), ('centr', self.centr[k], p.computeCentralised),
+            fams += [('local', self.local[k], p.computeLocal), ('centr', self.centr[k], self._centr_on(k)),
                      ('ssbc', self.ssbc[k], p.computeSingleSensorBroadcast)]
         for name, s, on in fams:
             if not on or s.start or tCurr < p.startUpdatesAfterAtLeast:
@@ -930,6 +953,8 @@ class OnlineDANSE:
                     s.start = True
                     if name == 'danse':
                         self.startRound[k] = self.i[k]
+                    elif name == 'centr':
+                        self.startRoundCentr[k] = self.i[k]
 
     # ---- perform_update (2290-2362) ----
     def _perform_update(self, k, skipUpdateCentr):
@@ -942,7 +967,7 @@ class OnlineDANSE:
         if self.danse[k].start:
             self.danse[k].w[:, i + 1, :] = fn(self.danse[k].Ryy, self.danse[k].Rnn, refSensorIdx=p.referenceSensor, rank=rank)
             self.nInternalFilterUps[k] += 1
-        if p.computeCentralised and self.centr[k].start and p.simType != 'batch':
+        if self._centr_on(k) and self.centr[k].start and p.simType != 'batch':
             if not skipUpdateCentr:
                 self.centr[k].w[:, i + 1, :] = fn(self.centr[k].Ryy, self.centr[k].Rnn,
                                                   refSensorIdx=int(np.sum(self.M[:k]) + p.referenceSensor), rank=rank)

@@ -307,3 +307,22 @@ def test_multi_ref_filters_bit_identical():
     many = O.update_w_refs(Ryy, Rnn, refs)
     for r, w in zip(refs, many):
         assert np.array_equal(w, O.update_w(Ryy, Rnn, r))
+
+
+def test_oracle_centralised_restriction_exact():
+    """The oracle's test-side restriction for the wide centralised family
+    (skipDanse / centrBins / centrNodes, exact in synchronous wholeChunk runs:
+    the centralised vector is the nodes' raw frames) gives the full oracle's
+    centralised filters on the kept nodes and bins, and its start rounds --
+    the full oracle being pinned by the reference fixture of the case."""
+    from oracle import danse_ref_cpu as O
+    case = next(c for c in ONLINE_CASES if c['name'] == 'online_ragged_asy_r2')
+    sc = make_case_scene(case)
+    dp, wp = make_case_params(case)
+    sc.get_vad_per_frame(dp.DFTsize, dp.Ns, wp.vadMinProportionActive)
+    full = O.OnlineDANSE(sc, dp, vadMinProp=wp.vadMinProportionActive).run()
+    bins = [0, 7, 100, 512]
+    sub = O.OnlineDANSE(sc, dp, vadMinProp=wp.vadMinProportionActive, skipDanse=True, centrBins=bins,
+                        centrNodes=[1]).run()
+    assert sub.startRoundCentr[1] == full.startRoundCentr[1] >= 0
+    assert np.array_equal(sub.centr[1].w, full.centr[1].w[bins])
