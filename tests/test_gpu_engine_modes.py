@@ -446,8 +446,8 @@ def test_online_centralised_K32x8_sum256_vs_oracle():
     sandbox_config.yaml:30): per node a 256 x 256 SCM pair per bin, the
     recursion on the device (wide_rec_kernel), the reference gate at D = 256
     (gate_wide_kernel: global workspace), the float64 wide GEVD solves; the
-    DANSE family (D = 39) runs alongside.  19 s with 1.2 s pauses, so that
-    the node counters pass 256 (round ~550).  The float64 oracle is run with
+    DANSE family (D = 39) runs alongside.  20 s with 1.2 s pauses, so that
+    the node counters pass 256 (round 548 of 623).  The float64 oracle is run with
     its centralised-only restriction (skipDanse / centrBins / centrNodes,
     exact for synchronous runs: test_oracle_centralised_restriction_exact) on
     two nodes and six bins, CENTR_POST_ROUNDS rounds past the start
@@ -456,7 +456,7 @@ def test_online_centralised_K32x8_sum256_vs_oracle():
     from danse_amd.scene import make_scene
     from danse_amd import _lib as L
     from oracle import danse_ref_cpu as O
-    case = dict(name='online_centr_K32x8', M=[8] * 32, dur=19.0, seed=71,
+    case = dict(name='online_centr_K32x8', M=[8] * 32, dur=20.0, seed=71,
                 danse=dict(BATTERY, nodeUpdating='asy', computeCentralised=True))
     dp, wp = make_case_params(case)
     sc = make_scene(case['M'], sigDur=case['dur'], seed=case['seed'], pauseDuration=1.2)
