@@ -38,7 +38,7 @@ __global__ void __launch_bounds__(64) cond_kernel(const UpdateArgs a, const FamN
     const int i = li;
     for (int j = 0; j <= i; ++j) {
       const long long e = scm_lower(d, a.scmStride, s, F, f, i, j);
-      cd x = cdk(a.Ryy[e]);
+      cd x = scm_entry(a, d, true, e);
       if (i == j) x.im = 0.0;
       cA[i * P + j] = x;
       cA[j * P + i] = conjg(x);

@@ -264,6 +264,7 @@ __global__ void reset_fam_kernel(const FamNode* fns, int nFN, const long long* w
     const cd v = scm0[scmOff[i] + src];
     Ryy[s * scmStride + fn.scmOff + e] = cfk(v);
     Rnn[s * scmStride + fn.scmOff + e] = v;
+    if (fn.D > kMaxDMax) Rnn[s * scmStride + fn.scmOff + nS + e] = v;   // (the wide fns' float64 Ryy)
     if (e < nW) wHist[s * wStride + fn.wOff + e] = w0[w0Off[i] + e];
   }
 }
@@ -719,7 +720,8 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
       // row classes keep bin-major triangles (FamNode.packed 2)
       const bool gridSmall = c->smallDGrid && c->gevd && fn.D <= kLaneMaxD;
       fn.packed = (class_packed(fn.D) && !gridSmall) ? 1 : 2;
-      scmOff += (long long)F * fn.D * (fn.D + 1) / 2;
+      // (the wide fns keep Ryy in float64 past their Rnn: kernels.hpp wide_fn)
+      scmOff += (long long)F * fn.D * (fn.D + 1) / 2 * (fn.D > kMaxDMax ? 2 : 1);
       fn.wOff = wOff;
       wOff += histW * F * fn.D;
       fn.liOff = liOff;
@@ -1306,8 +1308,8 @@ static void launch_wide(danse_engine* e, int r, hipStream_t st, unsigned mask) {
     const int D = fn.D;
     const int slotNext = e->keepHistory ? r + 1 : ((r + 1) & 1);
     wide::WideArgs wa{};
-    wa.D = D; wa.rank = e->rank; wa.gevd = e->gevd; wa.F = F; wa.nItems = (long long)S * F; wa.layout = 1;
-    wa.RyyF = e->Ryy + fn.scmOff; wa.Rnn = e->Rnn + fn.scmOff;
+    wa.D = D; wa.rank = e->rank; wa.gevd = e->gevd; wa.F = F; wa.nItems = (long long)S * F; wa.layout = 2;
+    wa.RyyD = e->Rnn + fn.scmOff + (long long)F * D * (D + 1) / 2; wa.Rnn = e->Rnn + fn.scmOff;
     wa.srcScene = e->scmStride; wa.srcBin = (long long)D * (D + 1) / 2;
     wa.nOut = 1; wa.refs[0] = fn.ref; wa.wOff[0] = fn.wOff + (long long)slotNext * F * D;
     wa.w = e->wHist; wa.wScene = e->wStride; wa.wBin = D;

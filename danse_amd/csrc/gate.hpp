@@ -79,7 +79,7 @@ __global__ void __launch_bounds__(64) gate_kernel(const UpdateArgs a, const FamN
       int i, j;
       tri_ij(e, i, j);
       const long long ee = scm_lower(d, a.scmStride, s, F, f, i, j);
-      cd x = which == 0 ? cdk(a.Ryy[ee]) : a.Rnn[ee];
+      cd x = scm_entry(a, d, which == 0, ee);
       if (i == j) x.im = 0.0;   // the stored diagonal is real; its init residue is Q_ii
       if (op != DANSE_OP_KEEP) {
         cd yy = cd{0.0, 0.0};
@@ -184,7 +184,7 @@ __global__ void __launch_bounds__(kGateWideThr) gate_wide_kernel(const UpdateArg
       int i, j;
       tri_ij(e, i, j);
       const long long ee = scm_lower(d, a.scmStride, s, F, f, i, j);
-      cd x = which == 0 ? cdk(a.Ryy[ee]) : a.Rnn[ee];
+      cd x = scm_entry(a, d, which == 0, ee);
       if (i == j) x.im = 0.0;
       if (op != DANSE_OP_KEEP) {
         cd yy = cd{0.0, 0.0};

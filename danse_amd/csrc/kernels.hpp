@@ -159,6 +159,20 @@ DANSE_DEV long long scm_lower(const FamNode& d, long long scmStride, int s, int 
   return b + ((long long)f * d.D + i) * d.D + j;
 }
 
+// The wide family-nodes (D > kMaxDMax, the online centralised family above 64
+// channels) keep Ryy in float64 as Rnn, in the Rnn array F T entries past
+// their Rnn (scmOff reserves both): the reference's float64 SCMs, which the
+// start gate's rank / PSD test at sum(M) = 256 needs (a 256 x 256 Ryy after
+// 257 averaged frames is nearly singular; its float32 rounding fails the
+// check rounds after the float64 matrix passes it)
+DANSE_DEV bool wide_fn(const FamNode& d) { return d.D > 64; }
+DANSE_DEV long long wide_ryy_shift(const FamNode& d, int F) { return (long long)F * (d.D * (d.D + 1) / 2); }
+// an SCM entry as the gate reads it (Ryy: complex64, or the wide fns' float64)
+DANSE_DEV cd scm_entry(const UpdateArgs& a, const FamNode& d, bool ryy, long long ee) {
+  if (!ryy) return a.Rnn[ee];
+  return wide_fn(d) ? a.Rnn[ee + wide_ryy_shift(d, a.F)] : cdk(a.Ryy[ee]);
+}
+
 // Agent-coherent (sc1) 8-byte load / store of a complex value: the resident
 // engine's hand-offs between waves of one launch (payload stored sc1 and
 // loaded sc1, flag after s_waitcnt vmcnt(0): MI355X_MICROARCH.md,

@@ -38,6 +38,9 @@ DANSE_DEV cd src_el(const WideArgs& a, bool ryy, long long base, int i, int c) {
   if (a.layout == 0) {
     const long long e = base + (long long)hi * a.D + lo;
     v = ryy ? a.RyyD[e] : a.Rnn[e];
+  } else if (a.layout == 2) {
+    const long long e = base + (long long)hi * (hi + 1) / 2 + lo;
+    v = ryy ? a.RyyD[e] : a.Rnn[e];
   } else {
     const long long e = base + (long long)hi * (hi + 1) / 2 + lo;
     v = ryy ? cdk(a.RyyF[e]) : a.Rnn[e];

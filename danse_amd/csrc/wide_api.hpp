@@ -15,7 +15,8 @@ constexpr int kMaxOut = 64;  // outputs (reference indices) per item
 struct WideArgs {   // (passed by value: the per-output tables ride in the kernel arguments)
   int D, rank, gevd, F;
   long long nItems, item0;   // item b = item0 + blockIdx.x; (scene, bin) = (b / F, b % F)
-  int layout;                // 0: full rows [D][D] (RyyD, Rnn); 1: packed lower, bin-major (RyyF, Rnn)
+  int layout;                // 0: full rows [D][D] (RyyD, Rnn); 1: packed lower, bin-major (RyyF, Rnn);
+                             // 2: packed lower, bin-major (RyyD, Rnn)
   const cd* RyyD;
   const cf* RyyF;
   const cd* Rnn;

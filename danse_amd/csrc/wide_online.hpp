@@ -6,8 +6,8 @@
 //   wide_rec_kernel   one 256-thread workgroup per (scene, family-node, bin):
 //                     the centralised vector into LDS, then the recursion of
 //                     the SCM this round's VAD selects over its packed lower
-//                     triangle (bin-major, FamNode.packed 2: Ryy complex64,
-//                     Rnn complex128, the arithmetic of update_kernel_2d);
+//                     triangle (bin-major, FamNode.packed 2: Ryy and Rnn
+//                     complex128, kernels.hpp wide_fn);
 //   wide_filter_kernel (wide.hpp) per family-node over its solving (scene,
 //                     bin) items, float64, writing w[r + 1];
 //   wide_tail_kernel  one wave per (scene, family-node, bin): the filter of
@@ -36,15 +36,21 @@ __global__ void __launch_bounds__(kWideRecThr) wide_rec_kernel(const UpdateArgs 
   const int T = D * (D + 1) / 2;
   const long long base = (long long)s * a.scmStride + d.scmOff + (long long)f * T;
   if (opY) {
-    const float by = (float)beta, cy = (opY == DANSE_OP_SET) ? (float)(1.0 / D) : (float)((1.0 - beta) / D);
+    // (float64, in the Rnn array past this fn's Rnn: kernels.hpp wide_fn)
+    cd* RyyD = a.Rnn + wide_ryy_shift(d, F);
+    const double cy = (opY == DANSE_OP_SET) ? 1.0 / D : (1.0 - beta) / D;
+    const double cx = (opY == DANSE_OP_SET) ? 0.0 : beta;
     for (int e = threadIdx.x; e < T; e += kWideRecThr) {
       int i, j;
       tri_ij(e, i, j);
-      cf x = a.Ryy[base + e];
-      const cf yy = cy * mulc(ys[i], ys[j]);
-      x = csel(opY == DANSE_OP_SET, yy, by * x + yy);
-      if (i == j) x.im = 0.0f;
-      a.Ryy[base + e] = x;
+      cd x = RyyD[base + e];
+      if (i == j) x.im = 0.0;
+      cd yy = cd{0.0, 0.0};
+      fma_cc(yy, cdk(ys[i]), cdk(ys[j]));
+      x = cx * x;
+      x.re = fma(cy, yy.re, x.re);
+      x.im = (i == j) ? 0.0 : fma(cy, yy.im, x.im);
+      RyyD[base + e] = x;
     }
   }
   if (opN) {
