@@ -269,39 +269,52 @@ def main():
         run_online(args, wl, S, rank, world, local, dist, pmc_child=True, small_grid=args.small_grid)
         return
     res = run_online(args, wl, S, rank, world, local, dist, resident=args.resident, small_grid=args.small_grid)
+    _progress(f'{args.workload}: {res["value"] / 1e6:.1f} M FU/s')
     extra = {}
     if world == 1 and args.workload == 'B' and not args.no_extra:
         # single-WASN lines: config B at S=1 and the
         # north_star headline shape N2 (online K=32 x 8, D=39) at S=1
         extra['B_S1'] = run_online(args, wl, 1, rank, world, local, dist, traffic=False)
+        _progress(f'B_S1: {extra["B_S1"]["value"] / 1e6:.1f} M FU/s')
         # the latency layout for one WASN: D = 11 on the 4 x 4 lane-grid solver
         extra['B_S1_grid'] = run_online(args, wl, 1, rank, world, local, dist, traffic=False, small_grid=True)
+        _progress(f'B_S1_grid: {extra["B_S1_grid"]["value"] / 1e6:.1f} M FU/s')
         # N1: the whole run in one persistent launch, SCMs resident in registers
         extra['B_S1_resident'] = run_online(args, wl, 1, rank, world, local, dist, traffic=False, resident=True)
+        _progress(f'B_S1_resident: {extra["B_S1_resident"]["value"] / 1e6:.1f} M FU/s')
         extra['N2'] = run_online(args, WORKLOADS['N2'], 1, rank, world, local, dist)
+        _progress(f'N2: {extra["N2"]["value"] / 1e6:.1f} M FU/s')
         # the other BASELINE.json configs, each on its own shape: C as named
         # (DXCP-PhaT estimation + compensation, K = 16 x 4, SROs 0..200 ppm),
         # D (batch K = 32 x 8, 20 iterations) and E at the battery's SRO
         # setting (K = 2, MK = [2, 3], fewSamples L = 64, 512 scenes)
         extra['C_dxcp'] = run_online(args, WORKLOADS['C_dxcp'], WORKLOADS['C_dxcp']['scenes'], rank, world, local,
                                      dist)
+        _progress(f'C_dxcp: {extra["C_dxcp"]["value"] / 1e6:.1f} M FU/s')
         extra['D'] = run_batch(args, WORKLOADS['D'], 1, rank, world, local, dist)
+        _progress(f'D: {extra["D"]["value"] / 1e6:.1f} M FU/s')
         extra['E_L64_sro200'] = run_online(args, WORKLOADS['E_L64_sro200'], 512, rank, world, local, dist,
                                            traffic=False)
+        _progress(f'E_L64_sro200: {extra["E_L64_sro200"]["value"] / 1e6:.1f} M FU/s')
         # the battery's cell as the battery configures it (local and
         # centralised families on, Oracle compensation with flags; FU counts
         # the DANSE family, the other families are extra solves)
         extra['E_comp'] = run_online(args, WORKLOADS['E_comp'], 512, rank, world, local, dist, traffic=False)
+        _progress(f'E_comp: {extra["E_comp"]["value"] / 1e6:.1f} M FU/s')
     cpu = {}
     if rank == 0 and not args.no_cpu_baseline:
+        _progress(f'CPU leg {args.workload}')
         cpu[args.workload] = cpu_child(args.workload, args.cpu_seconds, res['rounds'])
         for key in ('N2', 'C_dxcp', 'D', 'E_L64_sro200', 'E_comp'):
             if key in extra:
+                _progress(f'CPU leg {key}')
                 cpu[key] = cpu_child(key, args.cpu_seconds, extra[key].get('rounds'))
         for key in ('E_L64_sro200', 'E_comp'):
-            # for E also a P-process scene-parallel CPU leg
+            # for E also a P-process scene-parallel CPU leg (a
+            # shorter budget per process: they run at once)
             if key in extra and cpu.get(key) and 'value' in cpu[key]:
-                cpu[key]['scene_parallel'] = cpu_parallel(key, args.cpu_seconds, extra[key].get('rounds'))
+                _progress(f'CPU leg {key}, scene-parallel')
+                cpu[key]['scene_parallel'] = cpu_parallel(key, min(args.cpu_seconds, 8.0), extra[key].get('rounds'))
     if rank == 0:
         line = {
             'metric': 'DANSE frame-updates/sec (nodes x bins)',
@@ -337,6 +350,11 @@ def main():
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def _progress(msg):
+    """A progress line on stderr (long default runs stay visibly alive)."""
+    print(f'# [{time.strftime("%H:%M:%S")}] {msg}', file=sys.stderr, flush=True)
 
 
 def cpu_child(workload, seconds, rounds):
@@ -773,6 +791,7 @@ def pmc_traffic(wl, S, kernel_substr, rounds=None):
     tmp = tempfile.mkdtemp(prefix='danse_pmc_')
     env = dict(os.environ, TMPDIR=os.environ.get('TMPDIR', '/tmp'))
     for counter in ('FETCH_SIZE', 'WRITE_SIZE'):
+        _progress(f'PMC pass {counter} ({wl["name"]})')
         d = os.path.join(tmp, counter)
         cmd = [exe, '--pmc', counter, '--kernel-trace', '-d', d, '-o', 'pmc', '--output-format', 'csv', '--',
                sys.executable, str(ROOT / 'bench.py'), '--pmc-child', '--workload', wl['name'], *_CHILD_ARGS,
