@@ -817,7 +817,7 @@ def pmc_traffic(wl, S, kernel_substr, rounds=None):
                 if cur is None or 'gate_kernel' in kn or 'span_rec' in kn:
                     continue
                 cur[0] += float(row['Counter_Value']) * 1024.0
-                names[-1].append(kn.split('(')[0].replace('void ', '').strip())
+                names[-1].append(kn.replace('(anonymous namespace)::', '').split('(')[0].replace('void ', '').strip())
             nR = len(rounds) if rounds is not None else len(groups) - 1
             if len(groups) < nR or nR == 0:
                 return {'error': f'{counter}: {len(groups)} broadcast dispatches for {nR} rounds'}
