@@ -73,6 +73,7 @@ VARIANTS = {
     'stamp': ['-DDANSE_STAMP=1'],   # per-wave phase clocks in update_kernel_2d (DANSE_UPDATE_TRACE)
     'nodma': ['-DDANSE_LEAN_DMA=0'],   # update_kernel_2dc's factor record through VGPRs
     'lz6': ['-DDANSE_LEAN_LZ_VAD_DELTA=-2'],   # update_kernel_2dc: six Lanczos steps on VAD frames
+    'lzlocal': ['-DDANSE_LZ_FULL_REORTH=0'],   # Lanczos reorthogonalised against the last two vectors only
 }
 
 

@@ -1052,6 +1052,14 @@ DANSE_DEV void eigen2d(LDS2<NB, G>& S, int li, int D, int R, cf (&w)[vpl<NB, G>(
 // a few float32 roundings of ||C||, the floor the Householder path reaches.
 template <int DM>
 constexpr int kLz() { return (DM - 1) / 2 < 8 ? (DM - 1) / 2 : 8; }
+// reorthogonalisation of each Lanczos step: 1 = one classical Gram-Schmidt
+// pass against the whole basis; 0 = against the last two basis vectors only
+// (the three-term recurrence; A/B builds)
+#ifndef DANSE_LZ_FULL_REORTH
+#define DANSE_LZ_FULL_REORTH 1
+#endif
+template <int k>
+constexpr int lz_j0() { return (DANSE_LZ_FULL_REORTH || k < 1) ? 0 : k - 1; }
 constexpr float kLzTol = 3.0e-6f;
 constexpr float kLzBreak = 1.0e-6f;   // first-step breakdown test (relative to theta)
 
@@ -1108,7 +1116,8 @@ DANSE_DEV bool lanczos2d(const Blk<NB>& A, LDS2<NB, G>& S, int li, int D, const 
     // coefficients are independent (one reduction each, side by side);
     // h_k is the Lanczos alpha_k, h_(k-1) its beta_(k-1)
     cf h[k + 1];
-    sfor<0, k + 1>([&](auto jc) {
+    constexpr int j0 = lz_j0<k>();
+    sfor<j0, k + 1>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
       cf acc = cf{0.0f, 0.0f};
       sfor<0, NB>([&](auto tc) {
@@ -1118,11 +1127,11 @@ DANSE_DEV bool lanczos2d(const Blk<NB>& A, LDS2<NB, G>& S, int li, int D, const 
       });
       h[j] = acc;
     });
-    sfor<0, k + 1>([&](auto jc) { h[decltype(jc)::value] = sumq<G>(h[decltype(jc)::value]); });
+    sfor<j0, k + 1>([&](auto jc) { h[decltype(jc)::value] = sumq<G>(h[decltype(jc)::value]); });
     // (the basis entries are read again below, not kept in registers from the
     // coefficient pass: at k = 7 they were 80 VGPRs)
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    sfor<0, k + 1>([&](auto jc) {
+    sfor<j0, k + 1>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
       sfor<0, NB>([&](auto tc) {
         constexpr int t = decltype(tc)::value;
