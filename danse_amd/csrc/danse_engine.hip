@@ -1466,11 +1466,25 @@ static void launch_bcast(danse_engine* e, int r, int synth, int bc, hipStream_t 
 // the installed speculative gate candidates of round r (danse_engine_set_gate)
 // whose node is in `mask`
 // the gate checks of n candidates (GateCand) of filter dimensions up to dmax:
-// gate_kernel (one wave per (candidate, bin), the matrix in LDS) up to
-// kGateMaxD, gate_wide_kernel (one workgroup per (candidate, bin), the matrix
-// in eng->gateWork, in chunks) above
+// gate_kernel_reg (one wave per (candidate, bin), the matrix in registers) up
+// to kGateRegMaxD, gate_kernel (the matrix in LDS) up to kGateMaxD,
+// gate_wide_kernel (one workgroup per (candidate, bin), the matrix in
+// eng->gateWork, in chunks) above; DANSE_GATE_LDS=1: gate_kernel up to
+// kGateMaxD (A/B)
 static void launch_gate(danse_engine* eng, const UpdateArgs& a, const GateCand* cand, int n, int dmax, int* verdict,
                         hipStream_t s) {
+  if (dmax <= kGateRegMaxD && !std::getenv("DANSE_GATE_LDS")) {
+    const int ne = gate_reg_ne(dmax);
+#define DANSE_GATE_REG(NE)                                                                                    \
+  hipLaunchKernelGGL(gate_kernel_reg<NE>, dim3(eng->F, n), dim3(64), 0, s, a, eng->dFnAll, cand, eng->dInitScmOff, \
+                     eng->dScm0, eng->scmPerBin, verdict)
+    if (ne == 2) DANSE_GATE_REG(2);
+    else if (ne == 4) DANSE_GATE_REG(4);
+    else if (ne == 8) DANSE_GATE_REG(8);
+    else DANSE_GATE_REG(13);
+#undef DANSE_GATE_REG
+    return;
+  }
   if (dmax <= kGateMaxD || !eng->gateWork) {
     const size_t lds = (size_t)dmax * (dmax + 1) * sizeof(cd);
     hipLaunchKernelGGL(gate_kernel, dim3(eng->F, n), dim3(64), lds, s, a, eng->dFnAll, cand, eng->dInitScmOff,

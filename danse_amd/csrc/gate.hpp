@@ -246,5 +246,125 @@ __global__ void __launch_bounds__(kGateWideThr) gate_wide_kernel(const UpdateArg
   if (tid == 0 && !pass) atomicAnd(&verdict[ci], 0);
 }
 
+// The same checks for D <= kGateRegMaxD with the matrix in REGISTERS: lane li
+// holds the packed lower entries e = li + 64 m (m < NE, NE = ceil(T / 64)
+// rounded to 2, 4, 8 or 13) of its
+// (candidate, bin), their (row, column) found once; per Cholesky step only
+// column j goes through LDS (its owners write it, every lane reads the
+// entries its updates need).  The arithmetic of every entry is gate_kernel's
+// (the column scaled by 1 / sqrt|p_j| as each lane reads it, then
+// X[i][c] -= l_i conj(l_c)), so the verdicts are the same; no per-entry
+// index arithmetic and no LDS read-modify-write per step (gate_kernel keeps
+// the larger D).
+constexpr int kGateRegMaxD = 40;
+// entries per lane, NE = ceil(T / 64) rounded up to an instantiated size
+constexpr int gate_reg_ne(int dmax) {
+  const int n = (dmax * (dmax + 1) / 2 + 63) / 64;
+  return n <= 2 ? 2 : n <= 4 ? 4 : n <= 8 ? 8 : 13;
+}
+template <int kGateRegNE>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kGateRegNE <= 4 ? 4 : 2)))
+gate_kernel_reg(const UpdateArgs a, const FamNode* fns, const GateCand* cand, const long long* initOff, const cd* scm0,
+                int perBin, int* verdict) {
+  const int li = threadIdx.x;
+  const int f = blockIdx.x;
+  const GateCand c = cand[blockIdx.y];
+  const FamNode d = fns[c.fni];
+  if (!node_in(a.nodeMask, d.k)) return;
+  const int D = d.D, s = c.s, F = a.F;
+  const int T = D * (D + 1) / 2;
+  const uint8_t fl = a.flags[(((long long)a.r * a.S + s) * kMaxFam + d.fam) * a.K + d.k];
+  __shared__ cf gy[kGateRegMaxD];
+  __shared__ cd colv[kGateRegMaxD];
+  for (int i = li; i < D; i += 64) gy[i] = load_y(a, d, s, f, i, true);
+  // this lane's entries: rows / columns (T <= 1176: 11 bits each)
+  int rc[kGateRegNE];
+  sfor<0, kGateRegNE>([&](auto mc) {
+    constexpr int m = decltype(mc)::value;
+    const int e = li + 64 * m;
+    int i = 0, j = 0;
+    if (e < T) tri_ij(e, i, j);
+    rc[m] = (e < T) ? (i << 16) | j : -1;
+  });
+  __syncthreads();
+  const double beta = a.beta[s * a.K + d.k];
+  const cd* R0 = scm0 + initOff[c.fni] + (perBin ? (long long)f * D * D : 0ll);
+  bool pass = true;
+  for (int which = 0; which < 2 && pass; ++which) {   // 0: Ryy, 1: Rnn
+    const int op = which == 0 ? (fl & 3) : ((fl >> 2) & 3);
+    const double q = which == 0 ? c.qY : c.qN;
+    const double cy = (op == DANSE_OP_SET) ? 1.0 / D : (1.0 - beta) / D;
+    const double cx = (op == DANSE_OP_SET) ? 0.0 : beta;
+    bool herm = true;
+    double tr = 0.0;
+    cd X[kGateRegNE];
+    sfor<0, kGateRegNE>([&](auto mc) {
+      constexpr int m = decltype(mc)::value;
+      // (a compiler fence every 4 entries: their loads are not all hoisted
+      // over the earlier entries' arithmetic, which would spill)
+      if constexpr (m % 4 == 0) asm volatile("" ::: "memory");
+      X[m] = cd{0.0, 0.0};
+      if (rc[m] >= 0) {
+        const int i = rc[m] >> 16, j = rc[m] & 0xffff;
+        const long long ee = scm_lower(d, a.scmStride, s, F, f, i, j);
+        cd x = scm_entry(a, d, which == 0, ee);
+        if (i == j) x.im = 0.0;
+        if (op != DANSE_OP_KEEP) {
+          cd yy = cd{0.0, 0.0};
+          fma_cc(yy, cdk(gy[i]), cdk(gy[j]));
+          x = cx * x;
+          x.re = fma(cy, yy.re, x.re);
+          x.im = fma(cy, (i == j) ? 0.0 : yy.im, x.im);
+        }
+        const cd r0ij = R0[i * D + j], r0ji = R0[j * D + i];
+        const cd Q = cd{0.5 * q * (r0ij.re - r0ji.re), 0.5 * q * (r0ij.im + r0ji.im)};
+        if (i == j) {
+          const double qi = q * r0ij.im;
+          herm = herm && (2.0 * fabs(qi) <= 1e-8 + 1e-5 * sqrt(x.re * x.re + qi * qi));
+          tr += x.re;
+          X[m] = cd{x.re, 0.0};
+        } else {
+          const double aq = 2.0 * sqrt(Q.re * Q.re + Q.im * Q.im);
+          const double xr = x.re, xi = x.im;
+          const double mr = xr - 2.0 * Q.re, mi = xi - 2.0 * Q.im;
+          herm = herm && (aq <= 1e-8 + 1e-5 * sqrt(xr * xr + xi * xi)) &&
+                 (aq <= 1e-8 + 1e-5 * sqrt(mr * mr + mi * mi));
+          X[m] = cd{xr, xi};
+        }
+      }
+    });
+    if (a.gevd && __ballot(!herm) != 0ull) pass = false;
+    for (int o = 32; o >= 1; o >>= 1) tr += __shfl_xor(tr, o);
+    const double tol = (double)D * 2.220446049250313e-16 * fabs(tr);
+    for (int j = 0; j < D && pass; ++j) {
+      // column j (rows >= j) from its owners to LDS
+      sfor<0, kGateRegNE>([&](auto mc) {
+        constexpr int m = decltype(mc)::value;
+        if (rc[m] >= 0 && (rc[m] & 0xffff) == j) colv[rc[m] >> 16] = X[m];
+      });
+      __syncthreads();
+      const double pj = colv[j].re;   // (uniform)
+      if (!(a.gevd ? pj > tol : fabs(pj) > tol)) {
+        pass = false;
+        break;
+      }
+      const double inv = 1.0 / sqrt(fabs(pj));
+      sfor<0, kGateRegNE>([&](auto mc) {
+        constexpr int m = decltype(mc)::value;
+        if constexpr (m % 4 == 0) asm volatile("" ::: "memory");
+        const int i = rc[m] >> 16, cc = rc[m] & 0xffff;
+        if (rc[m] >= 0 && cc > j) {
+          const cd xi = colv[i], xc = colv[cc];
+          const cd lij = cd{inv * xi.re, inv * xi.im}, lcj = cd{inv * xc.re, inv * xc.im};
+          if (pj > 0.0) fms_cc(X[m], lij, lcj);
+          else fma_cc(X[m], lij, lcj);
+        }
+      });
+      __syncthreads();   // (every read of column j before the next column's writes)
+    }
+  }
+  if (li == 0 && !pass) atomicAnd(&verdict[blockIdx.y], 0);
+}
+
 }  // namespace danse
 
