@@ -52,6 +52,9 @@ struct Class {
   std::vector<int> creCount, cnCount;
   int* dFbList = nullptr;
   int* dFbCount = nullptr;
+  // lane classes (G = 1), GEVD: the factor records in wave order
+  // (UpdateArgs.liLane, [block][entry][64])
+  cf* liLane = nullptr;
 };
 
 template <typename T>
@@ -975,6 +978,14 @@ int danse_engine_create(const danse_cfg* c, int device, danse_engine** out) {
   HIPCHK(dalloc(&eng->d, (size_t)kMaxFam * S * K * c->T));
   HIPCHK(dalloc(&eng->diag, (size_t)S * K * kMaxFam));
   if (eng->liStride > 0) HIPCHK(dalloc(&eng->liCache, (size_t)S * eng->liStride));
+  if (c->gevd && eng->liStride > 0) {
+    for (auto& cl : eng->classes) {
+      if (cl.G != 1) continue;
+      const long long blocks = ((long long)S * (long long)cl.host.size() * F + 63) / 64;
+      // (whole 1 KiB DMA pieces per block: kernels_lane.hpp lr_rows)
+      HIPCHK(dalloc(&cl.liLane, (size_t)blocks * 64 * ((cl.DMAX * (cl.DMAX + 1) / 2 + cl.DMAX + 1) & ~1)));
+    }
+  }
   if (eng->vStride > 0) HIPCHK(dalloc(&eng->vCache, (size_t)S * eng->vStride));
   if (eng->vStride > 0) HIPCHK(dalloc(&eng->lzStats, (size_t)2 * R * kLzSlots));
   if (c->desSigConv) {
@@ -1176,6 +1187,7 @@ void danse_engine_destroy(danse_engine* eng) {
     if (cl.dev) (void)hipFree(cl.dev);
     if (cl.devIds) (void)hipFree(cl.devIds);
     if (cl.dSolveItems) (void)hipFree(cl.dSolveItems);
+    if (cl.liLane) (void)hipFree(cl.liLane);
     if (cl.dCreItems) (void)hipFree(cl.dCreItems);
     if (cl.dCnItems) (void)hipFree(cl.dCnItems);
     if (cl.dFbList) (void)hipFree(cl.dFbList);
@@ -1355,6 +1367,7 @@ static void launch_update(danse_engine* e, int r, hipStream_t st, unsigned mask 
     a.fn = cl.dev;
     a.famNodeId = cl.devIds;
     a.splitSolve = cl.split ? 1 : 0;
+    a.liLane = cl.liLane;
     a.noSolve = (!e->noRO && (int)cl.anySolve.size() > r && !cl.anySolve[r]) ? 1 : 0;
     if (r == e->updTraceRound) a.stamps = e->resTrace;
     // the solves on the cached factor and C: update_kernel_2dc (whole-round

@@ -73,6 +73,7 @@ struct UpdateArgs {
   int gevd, rank;
   int* diag;               // [S*K*kMaxFam]
   cf* liCache;             // GEVD factor cache per family-node [NT + D][F] (Li = L^-1 packed, g = L^H e_ref)
+  cf* liLane;              // lane classes: the same records in wave order, [block][entry][64] (kernels_lane.hpp)
   const double* cdPhase;   // CohDrift phase accumulator [S][K][K] (adds to zPhase), or null
   long long liStride;      // per scene; null cache = always refactor
   // centralised / SSBC under asynchronous clocks (danse_cfg.cEnd): channel
@@ -221,6 +222,20 @@ DANSE_DEV bool li_reusable(const UpdateArgs& a, const FamNode& d, int s, int opN
   return false;
 }
 
+// li_reusable with the flags of round r - 1 already loaded (flPrev; the
+// caller's own flags when r = 0, which the r > 0 test ignores)
+DANSE_DEV bool li_reusable_prev(const UpdateArgs& a, const FamNode& d, int s, int opN, uint8_t flPrev) {
+  if (!a.liCache || opN != DANSE_OP_KEEP || a.r == 0) return false;
+  if ((flPrev & DANSE_FLAG_SOLVE) && !(flPrev & DANSE_FLAG_PREGIVEN)) return true;
+  if (((flPrev >> 2) & 3) != DANSE_OP_KEEP) return false;
+  for (int rr = a.r - 2; rr >= 0 && rr >= a.r - kLiScan; --rr) {
+    const uint8_t f2 = a.flags[(((long long)rr * a.S + s) * kMaxFam + d.fam) * a.K + d.k];
+    if ((f2 & DANSE_FLAG_SOLVE) && !(f2 & DANSE_FLAG_PREGIVEN)) return true;
+    if (((f2 >> 2) & 3) != DANSE_OP_KEEP) return false;
+  }
+  return false;
+}
+
 // The float64 factor record of the last solve is the factor of Rnn before
 // this round's single rank-one update (opN == AVG; every round since that
 // solve left Rnn alone): solver2d.hpp li_rank1_2d moves it to this round's.
@@ -307,8 +322,13 @@ DANSE_DEV cf load_y_c(const UpdateArgs& a, const FamNode& d, int s, int f, int c
 // each stage is one memory round trip (hold()) instead of a dependent chain
 // per entry under per-entry branches.  Indices of the loads an entry does not
 // need are clamped to valid ones and their values discarded.
-template <int D>
-DANSE_DEV void load_y_all(const UpdateArgs& a, const FamNode& d, int s, int f, cf (&y)[D]) {
+// (afterIssue: called once the vector is complete -- a caller's own loads that
+// should neither queue ahead of these nor be waited for by their conversions)
+struct NoHook {
+  DANSE_DEV void operator()() const {}
+};
+template <int D, typename Hook = NoHook>
+DANSE_DEV void load_y_all(const UpdateArgs& a, const FamNode& d, int s, int f, cf (&y)[D], Hook&& afterIssue = Hook{}) {
   const int F = a.F, r = a.r, K = a.K, MT = a.MT;
   const int rawBase = MT + K;
   int c[D];
@@ -357,7 +377,7 @@ DANSE_DEV void load_y_all(const UpdateArgs& a, const FamNode& d, int s, int f, c
 #pragma unroll
     for (int i = 0; i < D; ++i) ph[i] += a.cdPhase[((long long)s * K + d.k) * K + q[i]];
   }
-  cf v[D];
+  const cf* pv[D];
 #pragma unroll
   for (int i = 0; i < D; ++i) {
     const bool loc = c[i] < MT, raw = c[i] >= rawBase;
@@ -371,9 +391,20 @@ DANSE_DEV void load_y_all(const UpdateArgs& a, const FamNode& d, int s, int f, c
       p = a.zAll ? a.Zspec + ((((long long)(r - lag[i] + 1)) * K + q[i]) * a.S + s) * F + f
                  : a.Zspec + ((((long long)((r - lag[i]) & 1)) * K + q[i]) * a.S + s) * F + f;
     }
-    v[i] = a.zAll ? ld_sc1(p) : *p;
+    pv[i] = p;
   }
-  hold(v);
+  // (the load kind tested once: a select per element between the plain and
+  // the sc1 load was a branch per element, each load waited for in its own)
+  cf v[D];
+  if (a.zAll) {
+#pragma unroll
+    for (int i = 0; i < D; ++i) v[i] = ld_sc1(pv[i]);
+    hold(v);
+  } else {
+#pragma unroll
+    for (int i = 0; i < D; ++i) v[i] = *pv[i];
+    hold(v);
+  }
 #pragma unroll
   for (int i = 0; i < D; ++i) {
     const bool loc = c[i] < MT, raw = c[i] >= rawBase;
@@ -382,6 +413,7 @@ DANSE_DEV void load_y_all(const UpdateArgs& a, const FamNode& d, int s, int f, c
     if (a.cPhase && d.fam == DANSE_FAM_CENTR) x = sro_rotate(x, f, F, cph[i]);
     y[i] = x;
   }
+  if constexpr (!__is_same(__remove_cvref(Hook), NoHook)) afterIssue();
 }
 
 // Relaxed external filter entry b wExt[i] + (1 - b) target (one function

@@ -23,6 +23,28 @@
 
 namespace danse {
 
+// The float32 factor record of a lane class (Li entries 0..NT-1, g entries
+// NT..NT+D-1) is cached in wave order, UpdateArgs.liLane: block b's record
+// is [entry][64 lanes] contiguous, exactly the LDS array the solve reads, so
+// it reaches LDS by LDS-DMA in 1 KiB pieces (global_load_lds_dwordx4, lane l
+// carrying bytes 16 l .. 16 l + 15 of a piece: two bins' entries), issued
+// right behind the Ryy loads.  A piece carries other lanes' bins, so the DMA
+// runs only in waves whose every lane takes the cached factor (the whole
+// wave in the branch); other waves copy their record through registers.
+namespace lane {
+constexpr int lr_rows(int D) { return (tri_n(D) + D + 1) & ~1; }   // whole pieces
+template <int D>
+DANSE_DEV void li_dma_lane(cf (*Lr)[64], const cf* rec) {
+  const char* src = reinterpret_cast<const char*>(rec) + 16 * threadIdx.x;
+  char* dst = reinterpret_cast<char*>(&Lr[0][0]);
+  sfor<0, lr_rows(D) / 2>([&](auto jc) {
+    constexpr int j = decltype(jc)::value;
+    __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src + 1024 * j),
+                                     (__attribute__((address_space(3))) void*)(dst + 1024 * j), 16, 0, 0);
+  });
+}
+}  // namespace lane
+
 struct LaneIdx {
   int f, s, fni;
   bool valid;
@@ -59,19 +81,28 @@ __global__ void __launch_bounds__(64) update_kernel_lane(const UpdateArgs a) {
   const FamNode d = a.fn[ix.fni];
   // (lanes of nodes outside the launch's node mask compute and store nothing)
   const bool valid = ix.valid && node_in(a.nodeMask, d.k);
-  const uint8_t fl = a.flags[(((long long)r * a.S + s) * kMaxFam + d.fam) * a.K + d.k];
+  const long long flIdx = (((long long)r * a.S + s) * kMaxFam + d.fam) * a.K + d.k;
+  const uint8_t fl = a.flags[flIdx];
+  // (the previous round's flags in the same round trip: li_reusable's first step)
+  const uint8_t flPrev = a.flags[r > 0 ? flIdx - (long long)a.S * kMaxFam * a.K : flIdx];
   const int opY = fl & 3, opN = (fl >> 2) & 3;
   const bool solve = !RO && (fl & DANSE_FLAG_SOLVE) != 0 && (fl & DANSE_FLAG_PREGIVEN) == 0;
   if (a.splitSolve && solve) return;   // this item's round runs on update_kernel_2d<.., PK = true>
   // GEVD: reuse the cached float32 Li / g when Rnn has not changed since the
   // last factorisation (skips the float64 load, Cholesky and inverse)
-  const bool reuse = GEVD && solve && li_reusable(a, d, s, opN);
-  cf* liC = a.liCache ? a.liCache + (long long)s * a.liStride + d.liOff + f : nullptr;
-  __shared__ cf Ls[NT][64];
-  __shared__ cf Gs[D][64];
+  const bool reuse = GEVD && solve && a.liLane && li_reusable_prev(a, d, s, opN, flPrev);
+  // this block's record in the wave-ordered cache, this lane's column
+  cf* const liRec = a.liLane ? a.liLane + (long long)blockIdx.x * lr_rows(D) * 64 : nullptr;
+  cf* const liC = liRec ? liRec + threadIdx.x : nullptr;
+  // the float32 factor record: Li (entries 0..NT-1) and g (NT..NT+D-1)
+  __shared__ __attribute__((aligned(16))) cf Lr[lr_rows(D)][64];
+  cf (*const Ls)[64] = Lr;
+  cf (*const Gs)[64] = Lr + NT;
+  const bool dma = GEVD && !RO && __any(reuse) && !__any(!reuse);   // (every lane: __all, spelled so that it allocates without spills)
 
+  // the observation vector: the recursion's and, kept in registers, dhat's
   cf y[D];
-  if ((opY || opN) && !(RO && a.noRec)) {
+  if (!RO || ((opY || opN) && !a.noRec)) {
     load_y_all<D>(a, d, s, f, y);
   }
   stamp(1);
@@ -79,8 +110,16 @@ __global__ void __launch_bounds__(64) update_kernel_lane(const UpdateArgs a) {
   const long long base = (long long)s * a.scmStride + d.scmOff + f;
   // Ryy (float32) of this frame into A: load, the recursion when the VAD
   // selects it, store
-  auto ryy_update = [&](PTri<D>& A) {
+  // (dma: the factor record's DMA, issued right behind these loads, so that
+  // the two share one round trip; waited for after the recursion, before the
+  // stores join the count)
+  auto ryy_update = [&](PTri<D>& A, bool dma = false) {
     sfor<0, NT>([&](auto ec) { A.a[decltype(ec)::value] = a.Ryy[base + (long long)decltype(ec)::value * F]; });
+    if (dma) {
+      asm volatile("" ::: "memory");
+      li_dma_lane<D>(Lr, liRec);
+      hold(A.a);
+    }
     if (opY) {
       const float by = (float)beta, cy = (opY == DANSE_OP_SET) ? (float)(1.0 / D) : (float)((1.0 - beta) / D);
       sfor<0, D>([&](auto ic) {
@@ -92,9 +131,12 @@ __global__ void __launch_bounds__(64) update_kernel_lane(const UpdateArgs a) {
           if constexpr (i == j) A.a[P(i, j)].im = 0.0f;
         });
       });
+      if (dma) __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the record has landed
       if (valid) {
         sfor<0, NT>([&](auto ec) { a.Ryy[base + (long long)decltype(ec)::value * F] = A.a[decltype(ec)::value]; });
       }
+    } else if (dma) {
+      __builtin_amdgcn_s_waitcnt(0x0F70);
     }
   };
 
@@ -174,10 +216,9 @@ __global__ void __launch_bounds__(64) update_kernel_lane(const UpdateArgs a) {
   if (solve) {
   if constexpr (GEVD) {
     asm volatile("" ::: "memory");   // (the float64 triangle is dead before the float32 work below)
-    if (reuse) {
-      sfor<0, NT>([&](auto ec) { Ls[decltype(ec)::value][threadIdx.x] = liC[(long long)decltype(ec)::value * F]; });
-      sfor<0, D>([&](auto ic) { Gs[decltype(ic)::value][threadIdx.x] = liC[(long long)(NT + decltype(ic)::value) * F]; });
-    } else {
+    if (reuse && !dma) {
+      sfor<0, NT + D>([&](auto ec) { Lr[decltype(ec)::value][threadIdx.x] = liC[decltype(ec)::value * 64]; });
+    } else if (!reuse) {
       // float64 Cholesky + inverse of Rnn; hand-over in float32 (LDS, and
       // the factor cache for later solves on the same Rnn)
       double invd[D];
@@ -186,13 +227,13 @@ __global__ void __launch_bounds__(64) update_kernel_lane(const UpdateArgs a) {
         cf g[D];   // out of the registers before the inverse
         ref_row<D>(N, d.ref, g);
         sfor<0, D>([&](auto ic) { Gs[decltype(ic)::value][threadIdx.x] = g[decltype(ic)::value]; });
-        if (liC && valid) sfor<0, D>([&](auto ic) { liC[(long long)(NT + decltype(ic)::value) * F] = g[decltype(ic)::value]; });
+        if (liC && valid) sfor<0, D>([&](auto ic) { liC[(NT + decltype(ic)::value) * 64] = g[decltype(ic)::value]; });
       }
       asm volatile("" ::: "memory");
       tri_inv64<D>(N, invd);
       store_tri<D>(N, Ls, threadIdx.x);
       if (liC && valid) {
-        sfor<0, NT>([&](auto ec) { liC[(long long)decltype(ec)::value * F] = cfk(N.a[decltype(ec)::value]); });
+        sfor<0, NT>([&](auto ec) { liC[decltype(ec)::value * 64] = cfk(N.a[decltype(ec)::value]); });
       }
     }
   } else {
@@ -231,6 +272,27 @@ __global__ void __launch_bounds__(64) update_kernel_lane(const UpdateArgs a) {
   const int slotNext = a.wHistory ? r + 1 : ((r + 1) & 1);
   cf* wPrev = a.wHist + wBase + ((long long)slotPrev * F + f) * D;
   cf* wNext = a.wHist + wBase + ((long long)slotNext * F + f) * D;
+  // the tail's external-filter loads (previous entries and targets, d_classes.py:
+  // 1627-1694), issued here so that they share the Ryy loads' round trip
+  // instead of taking one of their own after the solve: clamped indices, this
+  // lane's filter history standing in for a lane without a tail
+  const bool extOn = d.extMode >= 0 && !pregiven && valid;
+  const int eP = a.wExtHistory ? r : (r & 1);
+  const int eN = a.wExtHistory ? r + 1 : ((r + 1) & 1);
+  const long long eb = (long long)s * a.wExtStride + d.wExtOff;
+  cf ep[D], tq[D];
+  if constexpr (!RO) {
+    const int Mx = extOn ? d.M : D;
+    const cf* epSrc = extOn ? a.wExtHist + eb + ((long long)eP * F + f) * d.M : wPrev;
+    const cf* tqSrc = (extOn && a.wExtTarget) ? a.wExtTarget + (long long)s * a.tgtStride + d.tgtOff + (long long)f * d.M
+                                              : wPrev;
+#pragma unroll
+    for (int m = 0; m < D; ++m) ep[m] = epSrc[min(m, Mx - 1)], tq[m] = tqSrc[min(m, Mx - 1)];
+    if (!a.wExtTarget) {
+#pragma unroll
+      for (int m = 0; m < D; ++m) tq[m] = cf{0.0f, 0.0f};
+    }
+  }
   cf w[D];
   if (pregiven || (solveT && !GEVD)) {
     // pre-given history, or the MWF filter scm_factor_kernel_lane solved
@@ -238,10 +300,10 @@ __global__ void __launch_bounds__(64) update_kernel_lane(const UpdateArgs a) {
   } else if (solveT) {
     if constexpr (GEVD) {
       const LdsTri<D> Li{Ls, (int)threadIdx.x};
+      PTri<D> A;
+      ryy_update(A, dma);
       cf g[D];
       sfor<0, D>([&](auto ic) { g[decltype(ic)::value] = Gs[decltype(ic)::value][threadIdx.x]; });
-      PTri<D> A;
-      ryy_update(A);
       stamp(4);
       congruence<D>(A, Li);
       stamp(5);
@@ -258,25 +320,23 @@ __global__ void __launch_bounds__(64) update_kernel_lane(const UpdateArgs a) {
   asm volatile("" ::: "memory");
 
   // external filters (DANSE family), d_classes.py:1627-1694
-  if (d.extMode >= 0 && !pregiven && valid) {
+  if (extOn) {
     const int M = d.M;
-    const long long eb = (long long)s * a.wExtStride + d.wExtOff;
-    const int eP = a.wExtHistory ? r : (r & 1);
-    const int eN = a.wExtHistory ? r + 1 : ((r + 1) & 1);
-    cf* eprev = a.wExtHist + eb + ((long long)eP * F + f) * M;
     cf* enext = a.wExtHist + eb + ((long long)eN * F + f) * M;
     cf* tgt = a.wExtTarget + (long long)s * a.tgtStride + d.tgtOff + (long long)f * M;
     const float be = a.betaExt[s * a.K + d.k];
-    // the previous entries and targets first (clamped, hold())
-    cf ep[D], tq[D];
+    if constexpr (RO) {
+      // the previous entries and targets first (clamped, hold())
+      const cf* eprev = a.wExtHist + eb + ((long long)eP * F + f) * M;
 #pragma unroll
-    for (int m = 0; m < D; ++m) ep[m] = eprev[min(m, M - 1)], tq[m] = cf{0.0f, 0.0f};
-    if (a.wExtTarget) {
+      for (int m = 0; m < D; ++m) ep[m] = eprev[min(m, M - 1)], tq[m] = cf{0.0f, 0.0f};
+      if (a.wExtTarget) {
 #pragma unroll
-      for (int m = 0; m < D; ++m) tq[m] = tgt[min(m, M - 1)];
+        for (int m = 0; m < D; ++m) tq[m] = tgt[min(m, M - 1)];
+      }
+      hold(ep);
+      hold(tq);
     }
-    hold(ep);
-    hold(tq);
     sfor<0, D>([&](auto ic) {
       constexpr int m = decltype(ic)::value;
       if (m < M) {
@@ -295,10 +355,12 @@ __global__ void __launch_bounds__(64) update_kernel_lane(const UpdateArgs a) {
   }
   // dhat = w^H yhat, DC / Nyquist forced real (quirk Q7)
   cf dh = cf{0.0f, 0.0f};
-  {
+  if constexpr (RO) {
     cf yo[D];
     load_y_all<D>(a, d, s, f, yo);
     sfor<0, D>([&](auto ic) { dh = dh + cmul(w[decltype(ic)::value], yo[decltype(ic)::value]); });
+  } else {
+    sfor<0, D>([&](auto ic) { dh = dh + cmul(w[decltype(ic)::value], y[decltype(ic)::value]); });
   }
   if (f == 0 || f == F - 1) dh.im = 0.0f;
   if (valid) a.dhat[((((long long)d.fam * a.S + s) * a.K + d.k) * a.R + r) * F + f] = dh;
