@@ -1484,8 +1484,24 @@ static void launch_bcast(danse_engine* e, int r, int synth, int bc, hipStream_t 
 // gate_wide_kernel (one workgroup per (candidate, bin), the matrix in
 // eng->gateWork, in chunks) above; DANSE_GATE_LDS=1: gate_kernel up to
 // kGateMaxD (A/B)
+// (DANSE_GATE_WAVE=1: the wave-per-bin kernels below also for D <= 12, A/B only)
+static bool gate_wave() {
+  static const bool v = std::getenv("DANSE_GATE_WAVE") != nullptr;
+  return v;
+}
 static void launch_gate(danse_engine* eng, const UpdateArgs& a, const GateCand* cand, int n, int dmax, int* verdict,
                         hipStream_t s) {
+  if (dmax <= kGateLaneMaxD && !gate_wave()) {
+    const unsigned grid = (unsigned)(((long long)n * eng->F + 63) / 64);
+#define DANSE_GATE_LANE(DM)                                                                                  \
+  hipLaunchKernelGGL(gate_kernel_lane<DM>, dim3(grid), dim3(64), 0, s, a, eng->dFnAll, cand, n, eng->dInitScmOff, \
+                     eng->dScm0, eng->scmPerBin, verdict)
+    if (dmax <= 4) DANSE_GATE_LANE(4);
+    else if (dmax <= 8) DANSE_GATE_LANE(8);
+    else DANSE_GATE_LANE(12);
+#undef DANSE_GATE_LANE
+    return;
+  }
   if (dmax <= kGateRegMaxD && !std::getenv("DANSE_GATE_LDS")) {
     const int ne = gate_reg_ne(dmax);
 #define DANSE_GATE_REG(NE)                                                                                    \

@@ -21,6 +21,8 @@
 // pivots (an indefinite full-rank SCM passes, as in the reference).
 // One (candidate, bin) per wavefront, the matrix in LDS.
 #pragma once
+#include <type_traits>
+
 #include "kernels.hpp"
 
 namespace danse {
@@ -364,6 +366,138 @@ gate_kernel_reg(const UpdateArgs a, const FamNode* fns, const GateCand* cand, co
     }
   }
   if (li == 0 && !pass) atomicAnd(&verdict[blockIdx.y], 0);
+}
+
+// The same checks for D <= kGateLaneMaxD with one (candidate, bin) per LANE:
+// the lane's packed lower triangle in float64 registers, the Cholesky
+// sequential in the lane (no LDS, no barriers), the entries in storage order
+// -- for the lane classes' bin-minor SCMs every entry is one coalesced wave
+// access.  Per entry the arithmetic of gate_kernel (the column scaled by
+// 1 / sqrt|p_j|, then X[i][c] -= l_i conj(l_c)); the trace is summed in row
+// order.  DMAX is the launch's largest D (4, 8 or 12); each lane runs its own
+// candidate's D.
+constexpr int kGateLaneMaxD = 12;
+template <int DMAX>
+__global__ void __launch_bounds__(64) gate_kernel_lane(const UpdateArgs a, const FamNode* fns, const GateCand* cand,
+                                                      int nCand, const long long* initOff, const cd* scm0, int perBin,
+                                                      int* verdict) {
+  constexpr int NT = DMAX * (DMAX + 1) / 2;
+  constexpr auto P = [](int i, int j) { return i * (i + 1) / 2 + j; };
+  const int F = a.F;
+  const long long gid = (long long)blockIdx.x * 64 + threadIdx.x;
+  if (gid >= (long long)nCand * F) return;
+  const int ci = (int)(gid / F), f = (int)(gid % F);
+  const GateCand c = cand[ci];
+  const FamNode d = fns[c.fni];
+  if (!node_in(a.nodeMask, d.k)) return;
+  const int D = d.D, s = c.s;
+  const uint8_t fl = a.flags[(((long long)a.r * a.S + s) * kMaxFam + d.fam) * a.K + d.k];
+  // the observation vector (entries past D: a valid channel, unused), also in
+  // LDS for pass 1's runtime-indexed rows (this lane's column)
+  __shared__ cf ys[DMAX][64];
+  cf y[DMAX];
+  load_y_all<DMAX>(a, d, s, f, y, D);
+  sfor<0, DMAX>([&](auto ic) { ys[decltype(ic)::value][threadIdx.x] = y[decltype(ic)::value]; });
+  const double beta = a.beta[s * a.K + d.k];
+  const cd* R0 = scm0 + initOff[c.fni] + (perBin ? (long long)f * D * D : 0ll);
+  bool pass = true;
+  // Ryy (float32 storage), then Rnn (float64): one code path each, so that no
+  // entry load sits behind a per-entry test of which matrix it reads
+  auto check = [&](auto ryyc) {
+    constexpr bool RYY = decltype(ryyc)::value;
+    auto ld = [&](long long ee) -> cd { if constexpr (RYY) return cdk(a.Ryy[ee]); else return a.Rnn[ee]; };
+    const int op = RYY ? (fl & 3) : ((fl >> 2) & 3);
+    const double q = RYY ? c.qY : c.qN;
+    const double cy = (op == DANSE_OP_SET) ? 1.0 / D : (1.0 - beta) / D;
+    const double cx = (op == DANSE_OP_SET) ? 0.0 : beta;
+    // pass 1, a runtime loop over the entries (each one's Hermitian test runs
+    // three square roots: unrolled, their sequences interleave and spill):
+    // the Hermitian test against the init residue and the trace; the entries
+    // are read again for the factorisation
+    bool herm = true;
+    double tr = 0.0;
+#pragma unroll 1
+    for (int i = 0; i < D; ++i) {
+      const cf yi = ys[i][threadIdx.x];
+#pragma unroll 6
+      for (int j = 0; j <= i; ++j) {
+        cd x = ld(scm_lower(d, a.scmStride, s, F, f, i, j));
+        if (i == j) x.im = 0.0;
+        if (op != DANSE_OP_KEEP) {
+          cd yy = cd{0.0, 0.0};
+          fma_cc(yy, cdk(yi), cdk(ys[j][threadIdx.x]));
+          x = cx * x;
+          x.re = fma(cy, yy.re, x.re);
+          x.im = fma(cy, (i == j) ? 0.0 : yy.im, x.im);
+        }
+        const cd r0ij = R0[i * D + j], r0ji = R0[j * D + i];
+        const cd Q = cd{0.5 * q * (r0ij.re - r0ji.re), 0.5 * q * (r0ij.im + r0ji.im)};
+        if (i == j) {
+          const double qi = q * r0ij.im;
+          herm = herm && (2.0 * fabs(qi) <= 1e-8 + 1e-5 * sqrt(x.re * x.re + qi * qi));
+          tr += x.re;
+        } else {
+          const double aq = 2.0 * sqrt(Q.re * Q.re + Q.im * Q.im);
+          const double xr = x.re, xi = x.im;
+          const double mr = xr - 2.0 * Q.re, mi = xi - 2.0 * Q.im;
+          herm = herm && (aq <= 1e-8 + 1e-5 * sqrt(xr * xr + xi * xi)) &&
+                 (aq <= 1e-8 + 1e-5 * sqrt(mr * mr + mi * mi));
+        }
+      }
+    }
+    if (a.gevd && !herm) pass = false;
+    const double tol = (double)D * 2.220446049250313e-16 * fabs(tr);
+    // pass 2: the triangle into registers, padded to DMAX with an identity
+    // block scaled above the tolerance (decoupled: the real pivots are the
+    // same, the padded ones pass), so that the factorisation below runs
+    // without per-lane guards
+    const double pad = 1.0 + 2.0 * tol;
+    cd X[NT];
+    sfor<0, DMAX>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      asm volatile("" ::: "memory");   // (one row's loads in flight at a time)
+      sfor<0, i + 1>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        // (rows past D read row D - 1's entry, then take the pad)
+        cd x = ld(scm_lower(d, a.scmStride, s, F, f, min(i, D - 1), min(j, D - 1)));
+        if constexpr (i == j) x.im = 0.0;
+        if (op != DANSE_OP_KEEP) {
+          cd yy = cd{0.0, 0.0};
+          fma_cc(yy, cdk(ys[i][threadIdx.x]), cdk(ys[j][threadIdx.x]));
+          x = cx * x;
+          x.re = fma(cy, yy.re, x.re);
+          x.im = fma(cy, (i == j) ? 0.0 : yy.im, x.im);
+        }
+        X[P(i, j)] = (i < D) ? x : cd{(i == j) ? pad : 0.0, 0.0};
+      });
+    });
+    // right-looking Cholesky (GEVD) / signed elimination (MWF), every step
+    // run: a failed pivot only clears pass
+    sfor<0, DMAX>([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      const double pj = X[P(j, j)].re;
+      pass = pass && (a.gevd ? pj > tol : fabs(pj) > tol);
+      const double inv = 1.0 / sqrt(fabs(pj));
+      sfor<j + 1, DMAX>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        X[P(i, j)] = cd{inv * X[P(i, j)].re, inv * X[P(i, j)].im};
+      });
+      sfor<j + 1, DMAX>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        // X[i][k] -= l_i conj(l_k) for a positive pivot (fma_cc with -l_i:
+        // the same fused operations as fms_cc), += for a negative one
+        const cd lij = X[P(i, j)];
+        const cd ls = (pj > 0.0) ? cd{-lij.re, -lij.im} : lij;
+        sfor<j + 1, i + 1>([&](auto kc) {
+          constexpr int k = decltype(kc)::value;
+          fma_cc(X[P(i, k)], ls, X[P(k, j)]);
+        });
+      });
+    });
+  };
+  check(std::true_type{});
+  if (pass) check(std::false_type{});
+  if (!pass) atomicAnd(&verdict[ci], 0);
 }
 
 }  // namespace danse

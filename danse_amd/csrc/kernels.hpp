@@ -322,18 +322,15 @@ DANSE_DEV cf load_y_c(const UpdateArgs& a, const FamNode& d, int s, int f, int c
 // each stage is one memory round trip (hold()) instead of a dependent chain
 // per entry under per-entry branches.  Indices of the loads an entry does not
 // need are clamped to valid ones and their values discarded.
-// (afterIssue: called once the vector is complete -- a caller's own loads that
-// should neither queue ahead of these nor be waited for by their conversions)
-struct NoHook {
-  DANSE_DEV void operator()() const {}
-};
-template <int D, typename Hook = NoHook>
-DANSE_DEV void load_y_all(const UpdateArgs& a, const FamNode& d, int s, int f, cf (&y)[D], Hook&& afterIssue = Hook{}) {
+// (nAct: the entries past it repeat entry nAct - 1 -- a caller compiled for a
+// larger size than the family-node's D)
+template <int D>
+DANSE_DEV void load_y_all(const UpdateArgs& a, const FamNode& d, int s, int f, cf (&y)[D], int nAct = D) {
   const int F = a.F, r = a.r, K = a.K, MT = a.MT;
   const int rawBase = MT + K;
   int c[D];
 #pragma unroll
-  for (int i = 0; i < D; ++i) c[i] = a.chanList[d.chanOff + i];
+  for (int i = 0; i < D; ++i) c[i] = a.chanList[d.chanOff + min(i, nAct - 1)];
   hold(c);
   // sender node q (fused spectra) / raw channel's node (centralised vector)
   int q[D];
@@ -413,7 +410,6 @@ DANSE_DEV void load_y_all(const UpdateArgs& a, const FamNode& d, int s, int f, c
     if (a.cPhase && d.fam == DANSE_FAM_CENTR) x = sro_rotate(x, f, F, cph[i]);
     y[i] = x;
   }
-  if constexpr (!__is_same(__remove_cvref(Hook), NoHook)) afterIssue();
 }
 
 // Relaxed external filter entry b wExt[i] + (1 - b) target (one function
