@@ -86,8 +86,10 @@ def test_broadcast_and_dxcp_kernels_use_no_scratch():
     # the broadcast kernels hold five 16-element preload runs next to the FFT
     # registers; DXCP's state preloads spill at 16 per chunk
     asm = _device_asm(CSRC / 'danse_engine.hip')
-    sizes = _scratch_sizes(asm, r'bcast_kernel|fs_chunk_kernel|fs_ir_kernel')
-    assert len(sizes) >= 4, sizes
+    # (and the start-gate kernels: the per-lane form holds a float64 triangle
+    # of up to 78 entries, the register form up to 13 per lane)
+    sizes = _scratch_sizes(asm, r'bcast_kernel|fs_chunk_kernel|fs_ir_kernel|gate_kernel_lane|gate_kernel_reg')
+    assert len(sizes) >= 11, sizes
     assert not {k: v for k, v in sizes.items() if v != 0}, sizes
     asm = _device_asm(CSRC / 'dxcp.hip')
     sizes = _scratch_sizes(asm, r'dxcp_kernel')
