@@ -12,9 +12,12 @@
 //   1. SCM recursion (Ryy float32 or Rnn float64, as the VAD selects); on
 //      solve frames the float64 Cholesky + inverse of Rnn, handed to phase 2
 //      through LDS as the float32 Li = L^-1 and g = L^H e_ref ([entry][lane],
-//      39 KiB per wave at D = 11); MWF solves completely here, in float64;
-//   2. C = Li Ryy Li^H (Ryy re-read, L2), eigen part, w, external filters,
-//      dhat.
+//      39 KiB per wave at D = 11) -- or, when Rnn is unchanged since the
+//      last factorisation, that record from the factor cache (below);
+//      MWF solves completely here, in float64;
+//   2. Ryy's recursion, C = Li Ryy Li^H, eigen part, w, external filters
+//      (their loads issued ahead of the solve), dhat (from the observation
+//      vector kept since phase 1).
 // (No SLP packing in these classes -- build.py -- and no runtime rank test
 // for r = 0 in gevd_eig: either one doubles the register footprint.)
 #pragma once
