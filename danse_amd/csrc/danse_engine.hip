@@ -1491,14 +1491,20 @@ static bool gate_wave() {
 }
 static void launch_gate(danse_engine* eng, const UpdateArgs& a, const GateCand* cand, int n, int dmax, int* verdict,
                         hipStream_t s) {
-  if (dmax <= kGateLaneMaxD && !gate_wave()) {
+  if (dmax <= kGateLaneMaxD - 1 && !gate_wave()) {
     const unsigned grid = (unsigned)(((long long)n * eng->F + 63) / 64);
-#define DANSE_GATE_LANE(DM)                                                                                  \
-  hipLaunchKernelGGL(gate_kernel_lane<DM>, dim3(grid), dim3(64), 0, s, a, eng->dFnAll, cand, n, eng->dInitScmOff, \
-                     eng->dScm0, eng->scmPerBin, verdict)
+#define DANSE_GATE_LANE(DM)                                                                                 \
+  do {                                                                                                      \
+    if (eng->scmPerBin)                                                                                     \
+      hipLaunchKernelGGL((gate_kernel_lane<DM, true>), dim3(grid), dim3(64), 0, s, a, eng->dFnAll, cand, n,  \
+                         eng->dInitScmOff, eng->dScm0, eng->scmPerBin, verdict);                            \
+    else                                                                                                    \
+      hipLaunchKernelGGL((gate_kernel_lane<DM, false>), dim3(grid), dim3(64), 0, s, a, eng->dFnAll, cand, n, \
+                         eng->dInitScmOff, eng->dScm0, eng->scmPerBin, verdict);                            \
+  } while (0)
     if (dmax <= 4) DANSE_GATE_LANE(4);
     else if (dmax <= 8) DANSE_GATE_LANE(8);
-    else DANSE_GATE_LANE(12);
+    else DANSE_GATE_LANE(11);
 #undef DANSE_GATE_LANE
     return;
   }

@@ -368,29 +368,56 @@ gate_kernel_reg(const UpdateArgs a, const FamNode* fns, const GateCand* cand, co
   if (li == 0 && !pass) atomicAnd(&verdict[blockIdx.y], 0);
 }
 
-// The same checks for D <= kGateLaneMaxD with one (candidate, bin) per LANE:
-// the lane's packed lower triangle in float64 registers, the Cholesky
-// sequential in the lane (no LDS, no barriers), the entries in storage order
-// -- for the lane classes' bin-minor SCMs every entry is one coalesced wave
-// access.  Per entry the arithmetic of gate_kernel (the column scaled by
-// 1 / sqrt|p_j|, then X[i][c] -= l_i conj(l_c)); the trace is summed in row
-// order.  DMAX is the launch's largest D (4, 8 or 12); each lane runs its own
+// The same checks for D <= 11 with one (candidate, bin) per LANE: the lane's
+// packed lower triangle in float64 registers and its Cholesky sequential in
+// the lane; for the lane classes' bin-minor SCMs every entry is one
+// coalesced wave access.  When one init slice serves every bin (PB false),
+// the wave's (at most two) candidates' slices are staged in LDS and the
+// Hermitian test runs on the factorisation's registers, one entry at a time
+// (scheduling barriers: the square-root sequences of many entries
+// interleaved would spill); per-bin slices (PB) take a pass of their own over
+// the triangle and the slice.  Per entry the arithmetic of gate_kernel (the
+// column scaled by 1 / sqrt|p_j|, then X[i][c] -= l_i conj(l_c)); the trace
+// is summed in row order.  The triangle is padded to DMAX with a decoupled
+// identity block above the tolerance (the real pivots are unchanged, the
+// factorisation runs without per-lane guards, a failed pivot only clears
+// pass).  DMAX is the launch's largest D (4, 8 or 11; a launch with D = 12
+// takes gate_kernel_reg, whose registers it fits); each lane runs its own
 // candidate's D.
 constexpr int kGateLaneMaxD = 12;
-template <int DMAX>
+template <int DMAX, bool PB>
 __global__ void __launch_bounds__(64) gate_kernel_lane(const UpdateArgs a, const FamNode* fns, const GateCand* cand,
                                                       int nCand, const long long* initOff, const cd* scm0, int perBin,
                                                       int* verdict) {
   constexpr int NT = DMAX * (DMAX + 1) / 2;
   constexpr auto P = [](int i, int j) { return i * (i + 1) / 2 + j; };
   const int F = a.F;
-  const long long gid = (long long)blockIdx.x * 64 + threadIdx.x;
-  if (gid >= (long long)nCand * F) return;
+  const long long total = (long long)nCand * F;
+  const long long gid0 = (long long)blockIdx.x * 64 + threadIdx.x;
+  const bool live = gid0 < total;
+  const long long gid = live ? gid0 : total - 1;
   const int ci = (int)(gid / F), f = (int)(gid % F);
   const GateCand c = cand[ci];
   const FamNode d = fns[c.fni];
-  if (!node_in(a.nodeMask, d.k)) return;
   const int D = d.D, s = c.s;
+  // the init slices of the wave's (at most two) candidates in LDS, when one
+  // slice serves every bin (perBin = 0): the Hermitian test reads them there
+  __shared__ cd r0s[2][kGateLaneMaxD * kGateLaneMaxD];
+  const int c0 = __builtin_amdgcn_readfirstlane(ci);
+  const int c1 = __shfl(ci, 63);
+  if constexpr (!PB) {
+    sfor<0, 2>([&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      const int ck = k == 0 ? c0 : c1;
+      const int fk = cand[ck].fni;
+      const int Dk = fns[fk].D;
+      const cd* src = scm0 + initOff[fk];
+      for (int e = threadIdx.x; e < Dk * Dk; e += 64) r0s[k][e] = src[e];
+    });
+  }
+  __syncthreads();
+  if (!live || !node_in(a.nodeMask, d.k)) return;
+  const cd* R0s = r0s[ci == c0 ? 0 : 1];
   const uint8_t fl = a.flags[(((long long)a.r * a.S + s) * kMaxFam + d.fam) * a.K + d.k];
   // the observation vector (entries past D: a valid channel, unused), also in
   // LDS for pass 1's runtime-indexed rows (this lane's column)
@@ -410,14 +437,14 @@ __global__ void __launch_bounds__(64) gate_kernel_lane(const UpdateArgs a, const
     const double q = RYY ? c.qY : c.qN;
     const double cy = (op == DANSE_OP_SET) ? 1.0 / D : (1.0 - beta) / D;
     const double cx = (op == DANSE_OP_SET) ? 0.0 : beta;
-    // pass 1, a runtime loop over the entries (each one's Hermitian test runs
-    // three square roots: unrolled, their sequences interleave and spill):
-    // the Hermitian test against the init residue and the trace; the entries
-    // are read again for the factorisation
+    // pass 1 (per-bin init slices only), a runtime loop over the entries
+    // (each one's Hermitian test runs three square roots: unrolled, their
+    // sequences interleave and spill): the Hermitian test against the init
+    // residue and the trace; the entries are read again for the factorisation
     bool herm = true;
     double tr = 0.0;
 #pragma unroll 1
-    for (int i = 0; i < D; ++i) {
+    for (int i = 0; i < (PB ? D : 0); ++i) {
       const cf yi = ys[i][threadIdx.x];
 #pragma unroll 6
       for (int j = 0; j <= i; ++j) {
@@ -445,20 +472,14 @@ __global__ void __launch_bounds__(64) gate_kernel_lane(const UpdateArgs a, const
         }
       }
     }
-    if (a.gevd && !herm) pass = false;
-    const double tol = (double)D * 2.220446049250313e-16 * fabs(tr);
-    // pass 2: the triangle into registers, padded to DMAX with an identity
-    // block scaled above the tolerance (decoupled: the real pivots are the
-    // same, the padded ones pass), so that the factorisation below runs
-    // without per-lane guards
-    const double pad = 1.0 + 2.0 * tol;
+    // pass 2: the triangle into registers (rows past D read row D - 1's
+    // entries; the padding replaces them below)
     cd X[NT];
     sfor<0, DMAX>([&](auto ic) {
       constexpr int i = decltype(ic)::value;
       asm volatile("" ::: "memory");   // (one row's loads in flight at a time)
       sfor<0, i + 1>([&](auto jc) {
         constexpr int j = decltype(jc)::value;
-        // (rows past D read row D - 1's entry, then take the pad)
         cd x = ld(scm_lower(d, a.scmStride, s, F, f, min(i, D - 1), min(j, D - 1)));
         if constexpr (i == j) x.im = 0.0;
         if (op != DANSE_OP_KEEP) {
@@ -468,7 +489,49 @@ __global__ void __launch_bounds__(64) gate_kernel_lane(const UpdateArgs a, const
           x.re = fma(cy, yy.re, x.re);
           x.im = fma(cy, (i == j) ? 0.0 : yy.im, x.im);
         }
-        X[P(i, j)] = (i < D) ? x : cd{(i == j) ? pad : 0.0, 0.0};
+        X[P(i, j)] = x;
+      });
+    });
+    if constexpr (!PB) {
+      // the Hermitian test and the trace on the registers, the init residues
+      // from LDS, one entry at a time (scheduling barriers: the square-root
+      // sequences of many entries interleaved would spill)
+      sfor<0, DMAX>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        sfor<0, i + 1>([&](auto jc) {
+          constexpr int j = decltype(jc)::value;
+          __builtin_amdgcn_sched_barrier(0);
+          if (i < D) {
+            const cd x = X[P(i, j)];
+            const cd r0ij = R0s[i * D + j], r0ji = R0s[j * D + i];
+            const cd Q = cd{0.5 * q * (r0ij.re - r0ji.re), 0.5 * q * (r0ij.im + r0ji.im)};
+            if constexpr (i == j) {
+              const double qi = q * r0ij.im;
+              herm = herm && (2.0 * fabs(qi) <= 1e-8 + 1e-5 * sqrt(x.re * x.re + qi * qi));
+              tr += x.re;
+            } else {
+              const double aq = 2.0 * sqrt(Q.re * Q.re + Q.im * Q.im);
+              const double xr = x.re, xi = x.im;
+              const double mr = xr - 2.0 * Q.re, mi = xi - 2.0 * Q.im;
+              herm = herm && (aq <= 1e-8 + 1e-5 * sqrt(xr * xr + xi * xi)) &&
+                     (aq <= 1e-8 + 1e-5 * sqrt(mr * mr + mi * mi));
+            }
+          }
+        });
+      });
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (a.gevd && !herm) pass = false;
+    const double tol = (double)D * 2.220446049250313e-16 * fabs(tr);
+    // the padding past D: an identity block scaled above the tolerance
+    // (decoupled: the real pivots are the same, the padded ones pass), so
+    // that the factorisation below runs without per-lane guards
+    const double pad = 1.0 + 2.0 * tol;
+    sfor<1, DMAX>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      sfor<0, i + 1>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        if (i >= D) X[P(i, j)] = cd{(i == j) ? pad : 0.0, 0.0};
       });
     });
     // right-looking Cholesky (GEVD) / signed elimination (MWF), every step
